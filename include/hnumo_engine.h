@@ -1,0 +1,171 @@
+/*
+ * hnumo_engine.h -- C ABI of the MI355X DG time-step engine for h-NUMO's multilayer
+ * shallow-water (MLSWE) solver.
+ *
+ * Drop-in boundary.  The reference has no plugin/FFI layer: its hot path is the single
+ * Fortran call
+ *
+ *     call ti_rk_bcl(q0_df_mlswe, qb0_df_mlswe, qprime0_df)     ! mod_time_loop.F90:209
+ *
+ * (ti_rk_bcl.F90:9-87) with every other input held in module globals (mod_grid,
+ * mod_face, mod_basis, mod_metrics, mod_initial, mod_input, mod_constants,
+ * mod_variables).  This header replaces that call with
+ *
+ *     hnumo_engine_create(mesh, statics, params, halo, device, &eng)   -- module globals
+ *     hnumo_ti_rk_bcl(eng, q_df, qb_df, qprime_df)                      -- ti_rk_bcl
+ *
+ * and exposes the two inner entry points as parity hooks:
+ *
+ *     hnumo_ti_barotropic_ssprk  -- ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:19-151)
+ *     hnumo_create_rhs_btp       -- create_rhs_btp            (mod_rhs_btp.F90:28-59)
+ *
+ * Layout contract.  Every array is the reference's own Fortran (column-major) array,
+ * 1-based integers where the reference is 1-based.  The reference's face arrays carry
+ * a dead second face index (e.g. normal_vector(3,ngl,ngl,nface) of which only
+ * (:,n,1,f) is read on this path); the ABI takes the compacted slice, e.g.
+ * normal_vector(:,:,1,:) -> (3,ngl,nface), which a Fortran caller passes as that
+ * array section.  Node numbering is the reference's DG convention
+ * I = (e-1)*ngl*ngl + (j-1)*ngl + i (intma_dg, mod_grid.F90:230-239); quad numbering
+ * Iq = (e-1)*nq*nq + (j-1)*nq + i (intma_dg_quad, :242-250).  Any re-layout is internal.
+ *
+ * Errors.  The reference `stop`s; the ABI returns a code and keeps the message for
+ * hnumo_last_error():
+ *   0 OK, 1 negative layer thickness (mod_splitting.F90:74-77,228-231),
+ *   2 non-finite value, 3 HIP / RCCL error, 4 invalid argument / unsupported option.
+ *
+ * Threading.  One host thread per engine, one engine per GPU (rank).  Calls are
+ * synchronous on return unless resident mode is on (hnumo_set_resident), in which
+ * case state stays on the device between steps and hnumo_sync() copies it out.
+ *
+ * No torch, HIP or RCCL types appear in this header.
+ */
+#ifndef HNUMO_ENGINE_H
+#define HNUMO_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HNUMO_ABI_VERSION 1
+
+enum {
+  HNUMO_OK = 0,
+  HNUMO_ERR_NEGATIVE_THICKNESS = 1,
+  HNUMO_ERR_NONFINITE = 2,
+  HNUMO_ERR_DEVICE = 3,
+  HNUMO_ERR_INVALID = 4
+};
+
+/* Mesh, basis and metric terms: mod_grid / mod_face / mod_basis / mod_metrics. */
+typedef struct hnumo_mesh_desc {
+  int32_t nelem, npoin, npoin_q, nface;  /* mod_grid                                  */
+  int32_t ngl, nq, nlayers;              /* mod_basis ngl, nq; mod_input nlayers       */
+  const int32_t *face;                   /* (8,nface): face(7)=el, face(8)=er | -bc | 0 */
+  const int32_t *imapl, *imapr;          /* (3,ngl,nface) = imapl(:,:,1,:)              */
+  const double *normal_vector;           /* (3,ngl,nface) = normal_vector(:,:,1,:)      */
+  const double *normal_vector_q;         /* (3,nq,nface)  = normal_vector_q(:,:,1,:)    */
+  const double *jac_face;                /* (ngl,nface)   = jac_face(:,1,:)             */
+  const double *jac_faceq;               /* (nq,nface)    = jac_faceq(:,1,:)            */
+  const double *massinv;                 /* (npoin)       mod_metrics                   */
+  const double *psiq, *dpsiq;            /* (ngl,nq)      mod_basis                     */
+  const double *psi, *dpsi;              /* (ngl,ngl)     mod_basis                     */
+  /* per-quad-point metrics (mod_metrics ksiq_x.., jacq = w_i w_j |J|)  (nq,nq,nelem)  */
+  const double *ksiq_x, *ksiq_y, *etaq_x, *etaq_y, *jacq;
+  /* per-node metrics (ksi_x.., jac = w_i w_j |J|)                      (ngl,ngl,nelem) */
+  const double *ksi_x, *ksi_y, *eta_x, *eta_y, *jac;
+  /* Optional dense tables of Tensor_product.F90 (mod_initial psih, dpsidx, ...).  Read
+   * only by the CPU oracle; the HIP engine ignores them (NULL allowed).             */
+  const double *psih, *dpsidx, *dpsidy, *wjac;        /* (npts,npoin_q), wjac (npoin_q) */
+  const int32_t *indexq;                              /* (npts,npoin_q)                 */
+  const double *dpsidx_df, *dpsidy_df, *wjac_df;      /* (npts,npoin), wjac_df (npoin)  */
+  const int32_t *index_df;                            /* (npts,npoin)                   */
+} hnumo_mesh_desc;
+
+/* Reference state and forcing built at start-up: mod_initial (mod_initial.F90:42-53). */
+typedef struct hnumo_static_desc {
+  const double *pbprime;                /* (npoin_q)    */
+  const double *pbprime_df;             /* (npoin)      */
+  const double *one_over_pbprime;       /* (npoin_q)    */
+  const double *one_over_pbprime_df;    /* (npoin)      */
+  const double *pbprime_face;           /* (2,nq,nface) */
+  const double *pbprime_df_face;        /* (2,ngl,nface)*/
+  const double *one_over_pbprime_edge;  /* (nq,nface)   */
+  const double *coeff_pbpert_L, *coeff_pbpert_R, *coeff_pbub_LR;            /* (nq,nface) */
+  const double *coeff_mass_pbub_L, *coeff_mass_pbub_R, *coeff_mass_pbpert_LR;
+  const double *alpha;                  /* (nlayers)  alpha_mlswe = 1/rho_k */
+  const double *tau_wind;               /* (2,npoin_q)  */
+  const double *coriolis_quad;          /* (npoin_q)    */
+  const double *grad_zbot_quad;         /* (2,npoin_q)  */
+  const double *zbot_df;                /* (npoin)      */
+  const double *zbot_face;              /* (2,nq,nface) */
+  const double *fdt2_bcl, *a_bcl, *b_bcl;  /* (npoin)   */
+  const double *ssprk_a;                /* (kstages,3)  */
+  const double *ssprk_beta;             /* (kstages)    */
+} hnumo_static_desc;
+
+/* mod_input / mod_constants scalars used by the path. */
+typedef struct hnumo_params {
+  double dt, dt_btp;                    /* dt_btp = dt/N_btp (mod_initial.F90:176-177) */
+  double visc_mlswe, cd_mlswe, ad_mlswe, gravity;
+  int32_t N_btp, kstages, method_visc, botfr;
+} hnumo_params;
+
+/* Face-halo description (mod_parallel): processor faces have face(8)=0.  Faces are
+ * exchanged per neighbour in the order nbh_send_recv lists them (create_rhs_communicator
+ * / send_receive_bound).  num_nbh = 0 for a single rank.  The engine moves halos with
+ * RCCL point-to-point over xGMI; rank/nranks/comm_id identify the communicator.      */
+typedef struct hnumo_halo_desc {
+  int32_t rank, nranks;
+  int32_t num_nbh;
+  const int32_t *nbh_proc;              /* (num_nbh) neighbour ranks                    */
+  const int32_t *num_send_recv;         /* (num_nbh) shared faces per neighbour         */
+  const int32_t *nbh_send_recv;         /* (sum num_send_recv) 1-based face ids         */
+  const unsigned char *comm_id;         /* 128-byte RCCL unique id (NULL if nranks==1)  */
+} hnumo_halo_desc;
+
+typedef struct hnumo_engine hnumo_engine;   /* opaque: device buffers, streams, graphs */
+
+int  hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *statics,
+                         const hnumo_params *params, const hnumo_halo_desc *halo,
+                         int device, hnumo_engine **out);
+void hnumo_engine_destroy(hnumo_engine *eng);
+const char *hnumo_last_error(const hnumo_engine *eng);
+int  hnumo_abi_version(void);
+
+/* = ti_rk_bcl(q_df, qb_df, qprime_df)  (ti_rk_bcl.F90:9-87)
+ *   q_df(3,npoin,nlayers), qb_df(4,npoin), qprime_df(3,npoin,nlayers), all inout.  */
+int hnumo_ti_rk_bcl(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df);
+
+/* = ti_barotropic_ssprk_mlswe(qb_df, qprime_df) (mod_rk_mlswe.F90:19-151).  Uses the
+ *   baroclinic coefficients of the last hnumo_btp_bcl_coeffs / hnumo_ti_rk_bcl call. */
+int hnumo_ti_barotropic_ssprk(hnumo_engine *eng, double *qb_df, const double *qprime_df);
+
+/* = btp_bcl_coeffs_qdf(qprime_df_face, qprime_df) with dpprime_visc = qprime_df(1,:,:)
+ *   and qprime_df_face from extract_qprime_df_face (ti_rk_bcl.F90:43-50).           */
+int hnumo_btp_bcl_coeffs(hnumo_engine *eng, const double *qprime_df);
+
+/* = create_rhs_btp(rhs, qb_df, qprime_df) (mod_rhs_btp.F90:28-59); rhs(3,npoin).    */
+int hnumo_create_rhs_btp(hnumo_engine *eng, double *rhs, const double *qb_df,
+                         const double *qprime_df);
+
+/* Copy out a named engine field (mod_variables equivalents, e.g. "ope_ave", "H_ave",
+ * "Qu_face_ave", "graduvb_ave") in the reference's layout; n = element count.       */
+int hnumo_get_field(hnumo_engine *eng, const char *name, double *out, int64_t n);
+
+/* Resident mode: state stays on the device across hnumo_ti_rk_bcl calls; the host
+ * pointers passed to hnumo_ti_rk_bcl are only read on the first call and written by
+ * hnumo_sync().                                                                      */
+int hnumo_set_resident(hnumo_engine *eng, int on);
+int hnumo_sync(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df);
+
+/* Timing hook for the benchmark: run `nsteps` resident baroclinic steps and return
+ * device-side event timings (ms) of the whole span and of the dominant kernel.       */
+int hnumo_bench_steps(hnumo_engine *eng, int nsteps, double *ms_total,
+                      double *ms_kernel_avg, int64_t *kernel_launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HNUMO_ENGINE_H */

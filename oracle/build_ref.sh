@@ -1,0 +1,45 @@
+#!/usr/bin/env bash
+# TEST INFRASTRUCTURE ONLY.  Builds oracle/_ref/ref_driver: the reference's hot-path
+# Fortran compiled unmodified from /root/reference/src (read in place, never copied)
+# plus oracle/ref_driver.F90.  Needs amdflang (ROCm) and MPICH (/opt/conda); runs only
+# in the build container (the reference does not exist on the GPU box).
+#
+# Left out: amain.F90 / mod_time_loop.F90 (driver), mod_restart.F90 and
+# diagnostics_nc.F90 (need netcdf-fortran, absent).  p4est (absent) is only referenced
+# from mesh-construction routines that are never called; --gc-sections drops them.
+set -euo pipefail
+HERE="$(cd "$(dirname "$0")" && pwd)"
+SRC="${HNUMO_REF_SRC:-/root/reference/src}"
+OUT="$HERE/_ref"
+OBJ="$OUT/obj"
+FC="${FC:-/opt/rocm/lib/llvm/bin/amdflang}"
+MPI_INC=/opt/conda/include
+MPI_LIB=/opt/conda/lib
+# -fdefault-real-8: the reference's own build flag (config.user:25,61)
+FLAGS="-O2 -fdefault-real-8 -cpp -D__PGI"
+[ -d "$SRC" ] || { echo "reference sources not found at $SRC" >&2; exit 2; }
+mkdir -p "$OBJ"
+cd "$OBJ"
+EXCLUDE="amain.F90 mod_time_loop.F90 mod_restart.F90 diagnostics_nc.F90"
+$FC $FLAGS -I"$MPI_INC" -c "$HERE/mpi_module.F90" -o mpi_module.o
+files=""
+for f in $(cd "$SRC" && ls *.F90); do
+  case " $EXCLUDE " in *" $f "*) continue;; esac
+  files="$files $f"
+done
+for pass in $(seq 1 15); do
+  left=0
+  for f in $files; do
+    o="${f%.F90}.o"
+    [ -f "$o" ] && [ "$o" -nt "$SRC/$f" ] && continue
+    if ! $FC $FLAGS -I. -c "$SRC/$f" -o "$o" 2>"${f%.F90}.err"; then left=$((left+1)); rm -f "$o"; fi
+  done
+  [ $left -eq 0 ] && break
+done
+if [ $left -ne 0 ]; then
+  echo "reference build failed; see $OBJ/*.err" >&2; exit 1
+fi
+$FC $FLAGS -I. -c "$HERE/ref_driver.F90" -o ref_driver.o
+$FC -O2 -o "$OUT/ref_driver" ref_driver.o $(ls *.o | grep -v '^ref_driver.o$') \
+    -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi -Wl,--gc-sections
+echo "built $OUT/ref_driver"

@@ -1,0 +1,220 @@
+! ref_driver.F90 -- TEST INFRASTRUCTURE ONLY (oracle/_ref).
+!
+! Drives the REFERENCE Fortran hot path (ti_rk_bcl, ti_barotropic_ssprk_mlswe,
+! create_rhs_btp and everything below them, compiled unmodified from
+! /root/reference/src by oracle/Makefile) on inputs read from a bundle written by
+! h-numo_amd/hnumo/bundle.py, and writes its outputs for the parity tests.
+!
+! The reference's own start-up (p4est mesh, netCDF output, namelists) is not used:
+! this program fills the module globals the path reads (SURVEY.md §8b) directly from
+! the bundle -- the same arrays the CPU oracle and the HIP engine receive through
+! include/hnumo_engine.h.  It is single-rank (num_nbh = 0), so the reference's MPI
+! halo routines run with empty neighbour lists.
+!
+! usage: ref_driver <bundle.bin> <outputs.bin>
+program ref_driver
+
+    use mpi
+    use mod_input, only: nopx, nopy, nopz, nlayers, dt, dt_btp, kstages, method_visc, &
+        visc_mlswe, botfr, cd_mlswe, ad_mlswe, space_method, is_mlswe, dg_integ_exact, &
+        ti_method_btp, is_non_conforming_flg
+    use mod_basis, only: mod_basis_create, ngl, nq, npts, psiq, dpsiq, psi, dpsi, xgl, wgl, xnq, wnq
+    use mod_grid, only: mod_grid_init_unified, npoin, npoin_q, nelem, nface, nboun, face, &
+        npoin_cg, nbsido, nNC, face_type
+    use mod_face, only: normal_vector, normal_vector_q, jac_face, jac_faceq, imapl, imapr, &
+        imapl_q, imapr_q, face_send
+    use mod_metrics, only: massinv
+    use mod_constants, only: gravity
+    use mod_initial, only: psih, dpsidx, dpsidy, indexq, wjac, psih_df, dpsidx_df, dpsidy_df, &
+        index_df, wjac_df, pbprime, pbprime_df, one_over_pbprime, one_over_pbprime_df, &
+        pbprime_face, pbprime_df_face, one_over_pbprime_edge, coeff_pbpert_L, coeff_pbpert_R, &
+        coeff_pbub_LR, coeff_mass_pbub_L, coeff_mass_pbub_R, coeff_mass_pbpert_LR, alpha_mlswe, &
+        tau_wind, coriolis_quad, coriolis_df, grad_zbot_quad, zbot_df, zbot_face, fdt_bcl, &
+        fdt2_bcl, a_bcl, b_bcl, ssprk_a, ssprk_beta, N_btp, nvar
+    use mod_variables, only: mod_allocate_mlswe, ope_ave, H_ave, Qu_ave, Qv_ave, Quv_ave, ope2_ave, &
+        btp_mass_flux_ave, uvb_ave, tau_bot_ave, tau_wind_ave, ope2_ave_df, uvb_ave_df, &
+        uvb_face_ave, btp_mass_flux_face_ave, ope_face_ave, ope2_face_ave, Qu_face_ave, &
+        Qv_face_ave, Quv_face_ave, H_face_ave, one_plus_eta_edge_2_ave, graduvb_ave, &
+        graduvb_face_ave, Q_uu_dp, Q_uv_dp, Q_vv_dp, H_bcl, Q_uu_dp_edge, Q_uv_dp_edge, &
+        Q_vv_dp_edge, H_bcl_edge, btp_dpp_graduv, pbprime_visc, btp_graduv_dpp_face, &
+        sum_layer_mass_flux, sum_layer_mass_flux_face, dpprime_visc
+    use mod_mpi_communicator, only: ireq, status
+    use mod_parallel, only: num_nbh, num_send_recv, nbh_send_recv, nbh_send_recv_multi, nbh_proc
+    use mod_ref, only: q_send, q_recv, recv_data_dg, send_data_dg, lap_q_recv_df1, lap_q_send_df1, &
+        lap_recv_data_dg_df1, lap_send_data_dg_df1, recv_data_dg_quad, send_data_dg_quad, nmessage
+    use mod_rk_mlswe, only: ti_barotropic_ssprk_mlswe
+    use mod_rhs_btp, only: create_rhs_btp
+    use mod_barotropic_terms, only: btp_bcl_coeffs_qdf
+    use mod_layer_terms, only: extract_qprime_df_face
+
+    implicit none
+
+    integer :: hi(16), ierr, u, nsteps, mode, istep, k
+    real(8) :: hd(8)
+    character(len=512) :: fin, fout
+    integer, allocatable :: iface3(:,:,:), iface2(:,:)
+    real(8), allocatable :: r3(:,:,:), r2(:,:)
+    real(8), allocatable :: q_df(:,:,:), qb_df(:,:), qprime_df(:,:,:), rhs(:,:)
+    real(8), allocatable :: qf(:,:,:,:,:)
+    integer :: nl, nelem_in, npoin_in, npoin_q_in, nface_in, ngl_in, nq_in, nop_in
+    real(8), allocatable :: ref_xgl(:), ref_wgl(:), ref_xnq(:), ref_wnq(:)
+    real(8), allocatable :: ref_psiq(:,:), ref_dpsiq(:,:), ref_psi(:,:), ref_dpsi(:,:)
+
+    call mpi_init(ierr)
+    call get_command_argument(1, fin)
+    call get_command_argument(2, fout)
+    open(newunit=u, file=trim(fin), access='stream', form='unformatted', status='old')
+    read(u) hi
+    read(u) hd
+    nelem_in = hi(1); npoin_in = hi(2); npoin_q_in = hi(3); nface_in = hi(4)
+    ngl_in = hi(5); nq_in = hi(6); nl = hi(7); nop_in = hi(8)
+    nsteps = hi(13); mode = hi(14)
+
+    ! ---- mod_input (namelist values of the configuration)
+    nopx = nop_in; nopy = nop_in; nopz = 0
+    nlayers = nl; kstages = hi(9); method_visc = hi(11); botfr = hi(12)
+    dt = hd(1); dt_btp = hd(2); visc_mlswe = hd(3); cd_mlswe = hd(4); ad_mlswe = hd(5)
+    space_method = 'dg'; is_mlswe = .true.; dg_integ_exact = .true.; ti_method_btp = 'rk35'
+    is_non_conforming_flg = 0
+    gravity = hd(6)
+
+    ! ---- mod_basis: the reference builds its own LGL tables (mod_basis.F90:60-186)
+    call mod_basis_create(nopx, nopy, nopz)
+    if (ngl /= ngl_in .or. nq /= nq_in) stop 'basis size mismatch'
+
+    ! ---- mod_grid (what mod_p4est_create_grid would set, mod_p4est.F90:216-415)
+    nelem = nelem_in; nface = nface_in; npoin_cg = npoin_in; nbsido = 0; nNC = 0; nboun = 0
+    call mod_grid_init_unified()
+    if (npoin /= npoin_in .or. npoin_q /= npoin_q_in) stop 'grid size mismatch'
+
+    allocate(iface2(8, nface)); read(u) iface2; face(1:8, 1:nface) = iface2
+    face_type = 0
+    allocate(iface3(3, ngl, nface))
+    allocate(imapl(3, ngl, ngl, nface), imapr(3, ngl, ngl, nface))
+    allocate(imapl_q(3, nq, nq, nface), imapr_q(3, nq, nq, nface))
+    imapl = 0; imapr = 0; imapl_q = 0; imapr_q = 0
+    read(u) iface3; imapl(:, :, 1, :) = iface3
+    read(u) iface3; imapr(:, :, 1, :) = iface3
+    allocate(indexq(npts, npoin_q), index_df(npts, npoin))
+    read(u) indexq
+    read(u) index_df
+
+    ! ---- mod_face
+    allocate(normal_vector(3, ngl, ngl, nface), jac_face(ngl, ngl, nface))
+    allocate(normal_vector_q(3, nq, nq, nface), jac_faceq(nq, nq, nface))
+    normal_vector = 0; jac_face = 0; normal_vector_q = 0; jac_faceq = 0
+    allocate(r3(3, ngl, nface)); read(u) r3; normal_vector(:, :, 1, :) = r3; deallocate(r3)
+    allocate(r3(3, nq, nface)); read(u) r3; normal_vector_q(:, :, 1, :) = r3; deallocate(r3)
+    allocate(r2(ngl, nface)); read(u) r2; jac_face(:, 1, :) = r2; deallocate(r2)
+    allocate(r2(nq, nface)); read(u) r2; jac_faceq(:, 1, :) = r2; deallocate(r2)
+    allocate(face_send(0))
+
+    ! ---- mod_metrics
+    allocate(massinv(npoin)); read(u) massinv
+
+    ! ---- mod_basis tables: keep the reference's own for the setup check, run with the bundle's
+    call write_basis_later()
+    allocate(r2(ngl, nq)); read(u) r2; psiq = r2; read(u) r2; dpsiq = r2; deallocate(r2)
+    allocate(r2(ngl, ngl)); read(u) r2; psi = r2; read(u) r2; dpsi = r2; deallocate(r2)
+
+    ! ---- mod_initial
+    allocate(psih(npts, npoin_q), dpsidx(npts, npoin_q), dpsidy(npts, npoin_q), wjac(npoin_q))
+    allocate(psih_df(npts, npoin), dpsidx_df(npts, npoin), dpsidy_df(npts, npoin), wjac_df(npoin))
+    psih_df = 0
+    read(u) psih; read(u) dpsidx; read(u) dpsidy; read(u) wjac
+    read(u) dpsidx_df; read(u) dpsidy_df; read(u) wjac_df
+    allocate(pbprime(npoin_q), pbprime_df(npoin), one_over_pbprime(npoin_q), one_over_pbprime_df(npoin))
+    allocate(pbprime_face(2, nq, nface), pbprime_df_face(2, ngl, nface), one_over_pbprime_edge(nq, nface))
+    allocate(coeff_pbpert_L(nq, nface), coeff_pbpert_R(nq, nface), coeff_pbub_LR(nq, nface))
+    allocate(coeff_mass_pbub_L(nq, nface), coeff_mass_pbub_R(nq, nface), coeff_mass_pbpert_LR(nq, nface))
+    allocate(alpha_mlswe(nlayers), tau_wind(2, npoin_q), coriolis_quad(npoin_q), coriolis_df(npoin))
+    allocate(grad_zbot_quad(2, npoin_q), zbot_df(npoin), zbot_face(2, nq, nface))
+    allocate(fdt_bcl(npoin), fdt2_bcl(npoin), a_bcl(npoin), b_bcl(npoin))
+    allocate(ssprk_a(kstages, 3), ssprk_beta(kstages))
+    read(u) pbprime; read(u) pbprime_df; read(u) one_over_pbprime; read(u) one_over_pbprime_df
+    read(u) pbprime_face; read(u) pbprime_df_face; read(u) one_over_pbprime_edge
+    read(u) coeff_pbpert_L; read(u) coeff_pbpert_R; read(u) coeff_pbub_LR
+    read(u) coeff_mass_pbub_L; read(u) coeff_mass_pbub_R; read(u) coeff_mass_pbpert_LR
+    read(u) alpha_mlswe; read(u) tau_wind; read(u) coriolis_quad; read(u) grad_zbot_quad
+    read(u) zbot_df; read(u) zbot_face; read(u) fdt2_bcl; read(u) a_bcl; read(u) b_bcl
+    read(u) ssprk_a; read(u) ssprk_beta
+    coriolis_df = 0; fdt_bcl = 2.0d0 * fdt2_bcl
+    N_btp = hi(10); nvar = 5
+
+    allocate(q_df(3, npoin, nlayers), qb_df(4, npoin), qprime_df(3, npoin, nlayers), rhs(3, npoin))
+    read(u) q_df; read(u) qb_df; read(u) qprime_df
+    close(u)
+    rhs = 0
+
+    ! ---- single-rank halo plumbing (mod_parallel, mod_mpi_communicator, mod_ref)
+    num_nbh = 0
+    allocate(num_send_recv(0), nbh_send_recv(0), nbh_send_recv_multi(0), nbh_proc(0))
+    allocate(ireq(0), status(MPI_STATUS_SIZE, 0))
+    allocate(q_send(4, ngl, 0), q_recv(4, ngl, 0), recv_data_dg(0), send_data_dg(0))
+    allocate(lap_q_recv_df1(4, ngl, 0), lap_q_send_df1(4, ngl, 0))
+    allocate(lap_recv_data_dg_df1(0), lap_send_data_dg_df1(0))
+    allocate(recv_data_dg_quad(0), send_data_dg_quad(0))
+    nmessage = 6
+
+    ! ---- mod_variables
+    call mod_allocate_mlswe()
+    call zero_accumulators()
+    Q_uu_dp = 0; Q_uv_dp = 0; Q_vv_dp = 0; H_bcl = 0; Q_uu_dp_edge = 0; Q_uv_dp_edge = 0
+    Q_vv_dp_edge = 0; H_bcl_edge = 0; btp_dpp_graduv = 0; pbprime_visc = 0; btp_graduv_dpp_face = 0
+
+    ! ---- run the reference path
+    select case (mode)
+    case (1, 2)
+        allocate(qf(3, 2, ngl, nface, nlayers))
+        call extract_qprime_df_face(qf, qprime_df)
+        dpprime_visc(:, :) = qprime_df(1, :, :)
+        call btp_bcl_coeffs_qdf(qf, qprime_df)
+        if (mode == 1) then
+            call zero_accumulators()
+            call create_rhs_btp(rhs, qb_df, qprime_df)
+        else
+            call ti_barotropic_ssprk_mlswe(qb_df, qprime_df)
+        end if
+    case (3)
+        do istep = 1, nsteps
+            call ti_rk_bcl(q_df, qb_df, qprime_df)
+        end do
+    case default
+        stop 'unknown mode'
+    end select
+
+    ! ---- outputs
+    open(newunit=u, file=trim(fout), access='stream', form='unformatted', status='replace')
+    write(u) q_df, qb_df, qprime_df, rhs
+    write(u) ope_ave, H_ave, Qu_ave, Qv_ave, Quv_ave, ope2_ave, btp_mass_flux_ave, uvb_ave
+    write(u) tau_bot_ave, tau_wind_ave, ope2_ave_df, uvb_ave_df, uvb_face_ave
+    write(u) btp_mass_flux_face_ave, ope_face_ave, ope2_face_ave, Qu_face_ave, Qv_face_ave
+    write(u) Quv_face_ave, H_face_ave, one_plus_eta_edge_2_ave, graduvb_ave, graduvb_face_ave
+    write(u) Q_uu_dp, Q_uv_dp, Q_vv_dp, H_bcl, Q_uu_dp_edge, Q_uv_dp_edge, Q_vv_dp_edge, H_bcl_edge
+    write(u) btp_dpp_graduv, pbprime_visc, btp_graduv_dpp_face, sum_layer_mass_flux
+    write(u) sum_layer_mass_flux_face
+    write(u) ref_xgl, ref_wgl, ref_xnq, ref_wnq, ref_psiq, ref_dpsiq, ref_psi, ref_dpsi
+    close(u)
+    call mpi_finalize(ierr)
+
+contains
+
+    subroutine write_basis_later()
+        allocate(ref_xgl(ngl), ref_wgl(ngl), ref_xnq(nq), ref_wnq(nq))
+        allocate(ref_psiq(ngl, nq), ref_dpsiq(ngl, nq), ref_psi(ngl, ngl), ref_dpsi(ngl, ngl))
+        ref_xgl = xgl; ref_wgl = wgl; ref_xnq = xnq; ref_wnq = wnq
+        ref_psiq = psiq; ref_dpsiq = dpsiq; ref_psi = psi; ref_dpsi = dpsi
+    end subroutine write_basis_later
+
+    ! accumulators are zeroed by ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:45-72); a lone
+    ! create_rhs_btp call (mode 1) needs the same starting point.
+    subroutine zero_accumulators()
+        ope_ave = 0; H_ave = 0; Qu_ave = 0; Qv_ave = 0; Quv_ave = 0; ope2_ave = 0
+        btp_mass_flux_ave = 0; uvb_ave = 0; tau_bot_ave = 0; tau_wind_ave = 0
+        ope2_ave_df = 0; uvb_ave_df = 0; uvb_face_ave = 0; btp_mass_flux_face_ave = 0
+        ope_face_ave = 0; ope2_face_ave = 0; Qu_face_ave = 0; Qv_face_ave = 0
+        Quv_face_ave = 0; H_face_ave = 0; one_plus_eta_edge_2_ave = 0; graduvb_ave = 0
+        graduvb_face_ave = 0; sum_layer_mass_flux = 0; sum_layer_mass_flux_face = 0
+    end subroutine zero_accumulators
+
+end program ref_driver
