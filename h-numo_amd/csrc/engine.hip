@@ -1,0 +1,696 @@
+// engine.hip -- host side of libhnumo_engine: the C ABI of include/hnumo_engine.h.
+//
+// The engine owns all device state and reproduces the call sequence of ti_rk_bcl
+// (ti_rk_bcl.F90:9-87) with the kernels of kernels_btp.hip / kernels_bcl.hip.  A whole
+// baroclinic step (2 barotropic sub-cycles = 2*N_btp*kstages fused stage kernels plus
+// ~20 baroclinic kernels) is captured once into a hipGraph and replayed.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/hnumo_engine.h"
+#include "engine_internal.h"
+#include "kernels_bcl.hip"
+#include "kernels_btp.hip"
+
+using namespace hnumo;
+
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t err_ = (x);                                                                 \
+    if (err_ != hipSuccess) {                                                              \
+      eng->err = std::string("HIP error: ") + hipGetErrorString(err_) + " at " #x;         \
+      return HNUMO_ERR_DEVICE;                                                             \
+    }                                                                                      \
+  } while (0)
+
+struct hnumo_engine {
+  int device = 0;
+  std::string err;
+  hipStream_t stream = nullptr;
+  DevMesh m{};
+  hnumo_params p{};
+  int nelem, npoin, npq, nface, ngl, nq, L, P, Q, K;
+  size_t FQ, FN;
+  std::vector<void *> allocs;
+  // statics
+  double *basis, *qstat, *nstat, *fstat, *fnstat, *alpha, *tau_wind;
+  int *iconn;
+  std::vector<double> ssprk_a, ssprk_beta;  // host copies (kstages x 3), (kstages)
+  // state and step temporaries
+  double *q, *qb, *qp, *q2, *qp2, *qbp, *qf, *qf2, *dpp2;
+  double *qbuf[4], *gtrace[2];
+  // per-sub-cycle coefficients
+  double *qcoef, *ncoef, *fcoef, *fncoef, *dpp_graduv, *dpprime_visc, *gdpp_face;
+  // accumulators
+  double *qacc, *facc, *nacc, *gfacc, *tau_wind_ave;
+  // baroclinic scratch
+  double *slmf, *slmf_face, *dpp, *fmass, *fcons, *momL, *momR, *lapf, *rhs;
+  int *neg_flag, *h_neg;
+  // graph
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t graph_exec = nullptr;
+  bool resident = false, uploaded = false, alloc_failed = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+template <typename T>
+static T *dalloc(hnumo_engine *eng, size_t n) {
+  void *ptr = nullptr;
+  if (hipMalloc(&ptr, (n ? n : 1) * sizeof(T)) != hipSuccess) {
+    eng->alloc_failed = true;
+    return nullptr;
+  }
+  (void)hipMemset(ptr, 0, (n ? n : 1) * sizeof(T));
+  eng->allocs.push_back(ptr);
+  return (T *)ptr;
+}
+
+// ------------------------------------------------------------------ kernel dispatch
+template <int NGL, int NQ>
+struct Launch {
+  static constexpr int BSE = ((NQ * NQ + 63) / 64) * 64;
+  static void stage(hnumo_engine *e, const StageArgs &a) {
+    hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ>), dim3(e->nelem), dim3(BSE), 0, e->stream, a);
+  }
+  static void grad_trace(hnumo_engine *e, const double *qb, double *gt) {
+    hipLaunchKernelGGL((grad_trace_kernel<NGL, NQ>), dim3(e->nelem), dim3(64), 0, e->stream, e->m, qb, gt);
+  }
+  static void extract(hnumo_engine *e, const double *qp, double *qf, int only_dp) {
+    size_t n = (size_t)e->nface * NGL;
+    hipLaunchKernelGGL((extract_face_kernel<NGL>), dim3((n + 255) / 256), dim3(256), 0, e->stream, e->m, qp, qf,
+                       only_dp);
+  }
+  static void bcl_coeffs(hnumo_engine *e, const double *qp, const double *qf) {
+    hipLaunchKernelGGL((bcl_coeffs_elem_kernel<NGL, NQ>), dim3(e->nelem), dim3(BSE), 0, e->stream, e->m, qp,
+                       e->qcoef, e->ncoef, e->dpp_graduv, e->dpprime_visc);
+    hipLaunchKernelGGL((bcl_coeffs_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf,
+                       e->dpp_graduv, e->dpprime_visc, e->fcoef, e->fncoef, e->gdpp_face);
+  }
+  static void mass_cons(hnumo_engine *e, const double *qp, const double *qf, double *q, double *qp_out,
+                        int finalize_dp) {
+    hipLaunchKernelGGL((mass_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
+                       e->fmass, e->slmf_face);
+    hipLaunchKernelGGL((mass_elem_kernel<NGL, NQ>), dim3(e->nelem), dim3(BSE), 0, e->stream, e->m, qp, e->qacc,
+                       e->fmass, q, e->slmf, e->dpp, e->neg_flag);
+    hipLaunchKernelGGL((cons_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, e->dpp,
+                       e->facc, e->slmf_face, e->fcons);
+    hipLaunchKernelGGL((cons_elem_kernel<NGL, NQ>), dim3(e->nelem), dim3(BSE), 0, e->stream, e->m, e->dpp, e->qacc,
+                       e->slmf, e->fcons, q, qp_out, finalize_dp);
+  }
+  static void momentum(hnumo_engine *e, const double *qf, const double *qp_in, const double *qb, double *q,
+                       double *qp_out, int mode) {
+    hipLaunchKernelGGL((mom_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
+                       e->gdpp_face, e->gfacc, e->momL, e->momR, e->lapf);
+    hipLaunchKernelGGL((mom_elem_kernel<NGL, NQ>), dim3(e->nelem), dim3(BSE), 0, e->stream, e->m, qp_in, e->qacc,
+                       e->nacc, e->dpp_graduv, e->dpprime_visc, e->momL, e->momR, e->lapf, qb, q, qp_out, mode);
+  }
+};
+
+#define DISPATCH(eng, CALL)                                                     \
+  switch ((eng)->ngl) {                                                         \
+    case 3: Launch<3, 5>::CALL; break;                                          \
+    case 4: Launch<4, 7>::CALL; break;                                          \
+    case 5: Launch<5, 9>::CALL; break;                                          \
+    case 6: Launch<6, 11>::CALL; break;                                         \
+    case 8: Launch<8, 15>::CALL; break;                                         \
+    default: break;                                                             \
+  }
+
+static bool supported_ngl(int ngl) { return ngl == 3 || ngl == 4 || ngl == 5 || ngl == 6 || ngl == 8; }
+
+// ------------------------------------------------------------------ step pieces
+__global__ void copy_kernel(double *dst, const double *src, size_t n) {
+  const size_t s = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s) dst[i] = src[i];
+}
+
+// dpp2 = qp2(1); qp2(1) = 0.5*(qp(1) + dpp2)   (ti_rk_bcl.F90:78-79)
+__global__ void dp_average_kernel(double *qp2, const double *qp, double *dpp2, size_t n) {
+  const size_t s = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s) {
+    double d = qp2[i * 3];
+    dpp2[i] = d;
+    qp2[i * 3] = 0.5 * (qp[i * 3] + d);
+  }
+}
+
+// non-finite guard on the barotropic state (ABI return code 2); bit 2 of the flag word
+__global__ void finite_check_kernel(const double *x, size_t n, int *flag) {
+  const size_t s = (size_t)gridDim.x * blockDim.x;
+  bool bad = false;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s) bad |= !isfinite(x[i]);
+  if (__any(bad) && (threadIdx.x % 64) == 0) atomicOr(flag, 2);
+}
+
+// qprime(1) = dpp2; qprime(2:3) = qprime2(2:3)   (ti_rk_bcl.F90:84-85)
+__global__ void qprime_final_kernel(double *qp, const double *qp2, const double *dpp2, size_t n) {
+  const size_t s = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s) {
+    qp[i * 3] = dpp2[i];
+    qp[i * 3 + 1] = qp2[i * 3 + 1];
+    qp[i * 3 + 2] = qp2[i * 3 + 2];
+  }
+}
+
+static void launch_copy(hnumo_engine *e, double *dst, const double *src, size_t n) {
+  (void)hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, e->stream);
+}
+
+static void launch_avg(hnumo_engine *e, double *out, const double *a, const double *b, size_t n, int stride) {
+  int blocks = (int)std::min<size_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(average_kernel, dim3(std::max(blocks, 1)), dim3(256), 0, e->stream, out, a, b, n, stride);
+}
+
+static void zero_accumulators(hnumo_engine *e) {
+  (void)hipMemsetAsync(e->qacc, 0, sizeof(double) * QA_N * e->npq, e->stream);
+  (void)hipMemsetAsync(e->facc, 0, sizeof(double) * FA_N * e->FQ, e->stream);
+  (void)hipMemsetAsync(e->nacc, 0, sizeof(double) * NA_N * e->npoin, e->stream);
+  (void)hipMemsetAsync(e->gfacc, 0, sizeof(double) * 8 * e->FN, e->stream);
+}
+
+static void launch_bcl_coeffs(hnumo_engine *e, const double *qp, double *qf) {
+  DISPATCH(e, extract(e, qp, qf, 0));
+  DISPATCH(e, bcl_coeffs(e, qp, qf));
+}
+
+// ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:19-151) on device state qb_state
+static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp) {
+  zero_accumulators(e);
+  launch_copy(e, e->qbuf[0], qb_state, 4 * (size_t)e->npoin);
+  DISPATCH(e, grad_trace(e, e->qbuf[0], e->gtrace[0]));
+  int cur = 0, gt = 0, qb0i = 0, qb2i = -1;
+  const int K = e->K, NB = e->p.N_btp;
+  for (int mstep = 0; mstep < NB; mstep++) {
+    qb0i = cur;
+    qb2i = -1;
+    for (int ik = 0; ik < K; ik++) {
+      int out = 0;
+      while (out == cur || out == qb0i || out == qb2i) out++;
+      StageArgs a{};
+      a.m = e->m;
+      a.qb_in = e->qbuf[cur];
+      a.qb0 = e->qbuf[qb0i];
+      a.qb2 = qb2i >= 0 ? e->qbuf[qb2i] : e->qbuf[cur];
+      a.qprime = qp;
+      a.qcoef = e->qcoef;
+      a.ncoef = e->ncoef;
+      a.fcoef = e->fcoef;
+      a.fncoef = e->fncoef;
+      a.gtrace_in = e->gtrace[gt];
+      a.gtrace_out = e->gtrace[1 - gt];
+      a.qacc = e->qacc;
+      a.facc = e->facc;
+      a.nacc = e->nacc;
+      a.gfacc = e->gfacc;
+      a.qb_out = e->qbuf[out];
+      a.rhs_out = nullptr;
+      a.a1 = e->ssprk_a[ik + 0 * K];
+      a.a2 = e->ssprk_a[ik + 1 * K];
+      a.a3 = e->ssprk_a[ik + 2 * K];
+      a.dtt = e->p.dt_btp * e->ssprk_beta[ik];
+      a.rhs_only = 0;
+      a.write_grad = !(mstep == NB - 1 && ik == K - 1);
+      a.accumulate = 1;
+      DISPATCH(e, stage(e, a));
+      gt = 1 - gt;
+      cur = out;
+      if (K == 5 && ik == 1) qb2i = out;
+    }
+  }
+  int nblk = 1024;
+  hipLaunchKernelGGL(btp_finalize_kernel, dim3(nblk), dim3(256), 0, e->stream, e->qacc, e->facc, e->nacc, e->gfacc,
+                     e->tau_wind_ave, e->tau_wind, e->npq, (int)e->FQ, e->npoin, (int)e->FN, NB,
+                     1.0 / (double)(K * NB));
+  launch_copy(e, qb_state, e->qbuf[cur], 4 * (size_t)e->npoin);
+}
+
+// the full ti_rk_bcl on device state (e->q, e->qb, e->qp)
+static void launch_step(hnumo_engine *e) {
+  const size_t n3 = 3 * (size_t)e->npoin * e->L, nf = 6 * e->FN * e->L, nl = (size_t)e->npoin * e->L;
+  int blocks = (int)std::min<size_t>((nl + 255) / 256, 4096);
+  // prediction (ti_rk_bcl.F90:43-57)
+  launch_copy(e, e->qbp, e->qb, 4 * (size_t)e->npoin);
+  launch_bcl_coeffs(e, e->qp, e->qf);
+  launch_subcycle(e, e->qbp, e->qp);
+  launch_copy(e, e->q2, e->q, n3);
+  launch_copy(e, e->qp2, e->qp, n3);
+  launch_copy(e, e->qf2, e->qf, nf);
+  DISPATCH(e, mass_cons(e, e->qp2, e->qf2, e->q2, nullptr, 0));
+  DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qbp, e->q2, e->qp2, 0));
+  DISPATCH(e, extract(e, e->qp2, e->qf2, 0));
+  // correction (ti_rk_bcl.F90:62-85)
+  launch_avg(e, e->qp2, e->qp2, e->qp, n3, 1);
+  launch_avg(e, e->qf2, e->qf, e->qf2, nf, 1);
+  DISPATCH(e, bcl_coeffs(e, e->qp2, e->qf2));
+  launch_subcycle(e, e->qb, e->qp2);
+  DISPATCH(e, mass_cons(e, e->qp2, e->qf2, e->q, e->qp2, 1));
+  DISPATCH(e, extract(e, e->qp2, e->qf2, 1));
+  hipLaunchKernelGGL(dp_average_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp2, e->qp, e->dpp2, nl);
+  launch_avg(e, e->qf2, e->qf, e->qf2, nf / 3, 3);
+  DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qb, e->q, e->qp2, 1));
+  hipLaunchKernelGGL(qprime_final_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp, e->qp2, e->dpp2, nl);
+  hipLaunchKernelGGL(finite_check_kernel, dim3(256), dim3(256), 0, e->stream, e->qb, 4 * (size_t)e->npoin, e->neg_flag);
+}
+
+// ------------------------------------------------------------------ C ABI
+extern "C" {
+
+int hnumo_abi_version(void) { return HNUMO_ABI_VERSION; }
+
+const char *hnumo_last_error(const hnumo_engine *eng) { return eng ? eng->err.c_str() : "null engine"; }
+
+void hnumo_engine_destroy(hnumo_engine *eng) {
+  if (!eng) return;
+  (void)hipSetDevice(eng->device);
+  if (eng->graph_exec) (void)hipGraphExecDestroy(eng->graph_exec);
+  if (eng->graph) (void)hipGraphDestroy(eng->graph);
+  for (void *ptr : eng->allocs) (void)hipFree(ptr);
+  if (eng->h_neg) (void)hipHostFree(eng->h_neg);
+  if (eng->stream) (void)hipStreamDestroy(eng->stream);
+  if (eng->ev0) (void)hipEventDestroy(eng->ev0);
+  if (eng->ev1) (void)hipEventDestroy(eng->ev1);
+  delete eng;
+}
+
+static int fail(hnumo_engine *eng, int code, const std::string &msg) {
+  eng->err = msg;
+  return code;
+}
+
+int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st, const hnumo_params *par,
+                        const hnumo_halo_desc *halo, int device, hnumo_engine **out) {
+  hnumo_engine *eng = new hnumo_engine();
+  *out = eng;
+  eng->device = device;
+  if (!mesh || !st || !par) return fail(eng, HNUMO_ERR_INVALID, "null descriptor");
+  if (halo && halo->nranks > 1 && halo->num_nbh > 0)
+    return fail(eng, HNUMO_ERR_INVALID, "multi-rank halo exchange not supported by this build");
+  if (par->method_visc == 1) return fail(eng, HNUMO_ERR_INVALID, "method_visc==1 (quad-point LDG) not supported");
+  if (par->ad_mlswe > 0.0) return fail(eng, HNUMO_ERR_INVALID, "ad_mlswe>0 (vertical shear stress) not supported");
+  if (mesh->nlayers < 1 || mesh->nlayers > MAXL)
+    return fail(eng, HNUMO_ERR_INVALID, "nlayers must be 1..3 (qp(k) quirk, mod_create_rhs_mlswe.F90:382)");
+  if (!supported_ngl(mesh->ngl) || mesh->nq != 2 * mesh->ngl - 1)
+    return fail(eng, HNUMO_ERR_INVALID, "unsupported polynomial order (N in {2,3,4,5,7}, nq=2N+1)");
+  if (par->kstages < 1 || par->kstages > 5 || par->N_btp < 1) return fail(eng, HNUMO_ERR_INVALID, "bad kstages/N_btp");
+  HIPCHK(hipSetDevice(device));
+  HIPCHK(hipStreamCreateWithFlags(&eng->stream, hipStreamNonBlocking));
+  HIPCHK(hipEventCreate(&eng->ev0));
+  HIPCHK(hipEventCreate(&eng->ev1));
+  eng->p = *par;
+  const int E = mesh->nelem, ngl = mesh->ngl, nq = mesh->nq, F = mesh->nface, L = mesh->nlayers;
+  const int P = ngl * ngl, Q = nq * nq;
+  if (mesh->npoin != E * P || mesh->npoin_q != E * Q) return fail(eng, HNUMO_ERR_INVALID, "npoin/npoin_q mismatch");
+  eng->nelem = E; eng->npoin = E * P; eng->npq = E * Q; eng->nface = F; eng->ngl = ngl; eng->nq = nq;
+  eng->L = L; eng->P = P; eng->Q = Q; eng->K = par->kstages;
+  eng->FQ = (size_t)F * nq; eng->FN = (size_t)F * ngl;
+  const size_t npoin = eng->npoin, npq = eng->npq, FQ = eng->FQ, FN = eng->FN;
+
+  // ---- element -> face connectivity from the reference face arrays
+  std::vector<std::vector<std::pair<int, int>>> ef(E);
+  for (int f = 0; f < F; f++) {
+    int el = mesh->face[8 * f + 6] - 1, er = mesh->face[8 * f + 7];
+    if (el < 0 || el >= E) return fail(eng, HNUMO_ERR_INVALID, "face(7) out of range");
+    ef[el].push_back({f, 0});
+    if (er > 0) {
+      if (er > E) return fail(eng, HNUMO_ERR_INVALID, "face(8) out of range");
+      ef[er - 1].push_back({f, 1});
+    } else if (er == 0) {
+      return fail(eng, HNUMO_ERR_INVALID, "processor faces need a halo (multi-rank) description");
+    }
+  }
+  auto lnode = [&](const int32_t *imap, int f, int n) {
+    int i = imap[3 * (n + ngl * f)] - 1, j = imap[3 * (n + ngl * f) + 1] - 1;
+    return j * ngl + i;
+  };
+  std::vector<int> efaces(4 * E), eside(4 * E), ebc(4 * E), efmap(4 * E * ngl), enbr_node(4 * E * ngl, -1);
+  std::vector<int> enbr_e(4 * E, -1), enbr_lf(4 * E, -1), fnodeL(FN), fnodeR(FN, -1), fel(F), fer(F);
+  for (int e = 0; e < E; e++) {
+    if (ef[e].size() != 4) return fail(eng, HNUMO_ERR_INVALID, "every element needs exactly 4 faces");
+    std::sort(ef[e].begin(), ef[e].end());
+  }
+  for (int e = 0; e < E; e++)
+    for (int lf = 0; lf < 4; lf++) {
+      int f = ef[e][lf].first, s = ef[e][lf].second;
+      int el = mesh->face[8 * f + 6] - 1, er = mesh->face[8 * f + 7];
+      efaces[4 * e + lf] = f;
+      eside[4 * e + lf] = s;
+      ebc[4 * e + lf] = er;
+      for (int n = 0; n < ngl; n++) efmap[(4 * e + lf) * ngl + n] = lnode(s == 0 ? mesh->imapl : mesh->imapr, f, n);
+      if (er > 0) {
+        int nb = s == 0 ? er - 1 : el;
+        enbr_e[4 * e + lf] = nb;
+        for (int k = 0; k < 4; k++)
+          if (ef[nb][k].first == f) enbr_lf[4 * e + lf] = k;
+        for (int n = 0; n < ngl; n++)
+          enbr_node[(4 * e + lf) * ngl + n] = nb * P + lnode(s == 0 ? mesh->imapr : mesh->imapl, f, n);
+      }
+    }
+  for (int f = 0; f < F; f++) {
+    int el = mesh->face[8 * f + 6] - 1, er = mesh->face[8 * f + 7];
+    fel[f] = el;
+    fer[f] = er;
+    for (int n = 0; n < ngl; n++) {
+      fnodeL[(size_t)f * ngl + n] = el * P + lnode(mesh->imapl, f, n);
+      if (er > 0) fnodeR[(size_t)f * ngl + n] = (er - 1) * P + lnode(mesh->imapr, f, n);
+    }
+  }
+  std::vector<int> conn;
+  auto append = [&](const std::vector<int> &v) {
+    size_t off = conn.size();
+    conn.insert(conn.end(), v.begin(), v.end());
+    return off;
+  };
+  size_t o_ef = append(efaces), o_es = append(eside), o_eb = append(ebc), o_em = append(efmap);
+  size_t o_en = append(enbr_node), o_ee = append(enbr_e), o_el = append(enbr_lf), o_fl = append(fnodeL);
+  size_t o_fr = append(fnodeR), o_fe = append(fel), o_fer = append(fer);
+  eng->iconn = dalloc<int>(eng, conn.size());
+  if (!eng->iconn) return fail(eng, HNUMO_ERR_DEVICE, "hipMalloc failed");
+  HIPCHK(hipMemcpy(eng->iconn, conn.data(), conn.size() * sizeof(int), hipMemcpyHostToDevice));
+
+  // ---- statics
+  std::vector<double> hb(2 * ngl * nq + ngl * ngl);
+  for (int n = 0; n < ngl; n++)
+    for (int iq = 0; iq < nq; iq++) {
+      hb[n * nq + iq] = mesh->psiq[n + ngl * iq];
+      hb[ngl * nq + n * nq + iq] = mesh->dpsiq[n + ngl * iq];
+    }
+  for (int n = 0; n < ngl; n++)
+    for (int k = 0; k < ngl; k++) hb[2 * ngl * nq + n * ngl + k] = mesh->dpsi[n + ngl * k];
+  std::vector<double> qs(QS_N * npq), ns(NS_N * npoin), fs(FS_N * FQ), fns(FN_N * FN);
+  for (size_t i = 0; i < npq; i++) {
+    qs[QS_W * npq + i] = mesh->jacq[i];
+    qs[QS_COR * npq + i] = st->coriolis_quad[i];
+    qs[QS_TW1 * npq + i] = st->tau_wind[2 * i];
+    qs[QS_TW2 * npq + i] = st->tau_wind[2 * i + 1];
+    qs[QS_GZ1 * npq + i] = st->grad_zbot_quad[2 * i];
+    qs[QS_GZ2 * npq + i] = st->grad_zbot_quad[2 * i + 1];
+    qs[QS_OOP * npq + i] = st->one_over_pbprime[i];
+    qs[QS_EX * npq + i] = mesh->ksiq_x[i];
+    qs[QS_EY * npq + i] = mesh->ksiq_y[i];
+    qs[QS_NX * npq + i] = mesh->etaq_x[i];
+    qs[QS_NY * npq + i] = mesh->etaq_y[i];
+    qs[QS_PB * npq + i] = st->pbprime[i];
+  }
+  for (size_t i = 0; i < npoin; i++) {
+    ns[NS_PB * npoin + i] = st->pbprime_df[i];
+    ns[NS_OOP * npoin + i] = st->one_over_pbprime_df[i];
+    ns[NS_MINV * npoin + i] = mesh->massinv[i];
+    ns[NS_W * npoin + i] = mesh->jac[i];
+    ns[NS_EX * npoin + i] = mesh->ksi_x[i];
+    ns[NS_EY * npoin + i] = mesh->ksi_y[i];
+    ns[NS_NX * npoin + i] = mesh->eta_x[i];
+    ns[NS_NY * npoin + i] = mesh->eta_y[i];
+    ns[NS_ZB * npoin + i] = st->zbot_df[i];
+    ns[NS_F2 * npoin + i] = st->fdt2_bcl[i];
+    ns[NS_A * npoin + i] = st->a_bcl[i];
+    ns[NS_B * npoin + i] = st->b_bcl[i];
+  }
+  for (size_t i = 0; i < FQ; i++) {
+    fs[FS_NX * FQ + i] = mesh->normal_vector_q[3 * i];
+    fs[FS_NY * FQ + i] = mesh->normal_vector_q[3 * i + 1];
+    fs[FS_W * FQ + i] = mesh->jac_faceq[i];
+    fs[FS_CL * FQ + i] = st->coeff_pbpert_L[i];
+    fs[FS_CR * FQ + i] = st->coeff_pbpert_R[i];
+    fs[FS_CLR * FQ + i] = st->coeff_pbub_LR[i];
+    fs[FS_CML * FQ + i] = st->coeff_mass_pbub_L[i];
+    fs[FS_CMR * FQ + i] = st->coeff_mass_pbub_R[i];
+    fs[FS_CMLR * FQ + i] = st->coeff_mass_pbpert_LR[i];
+    fs[FS_OOPE * FQ + i] = st->one_over_pbprime_edge[i];
+    fs[FS_PBL * FQ + i] = st->pbprime_face[2 * i];
+    fs[FS_PBR * FQ + i] = st->pbprime_face[2 * i + 1];
+    fs[FS_ZBL * FQ + i] = st->zbot_face[2 * i];
+    fs[FS_ZBR * FQ + i] = st->zbot_face[2 * i + 1];
+  }
+  for (size_t i = 0; i < FN; i++) {
+    fns[FN_NX * FN + i] = mesh->normal_vector[3 * i];
+    fns[FN_NY * FN + i] = mesh->normal_vector[3 * i + 1];
+    fns[FN_W * FN + i] = mesh->jac_face[i];
+    fns[FN_PBL * FN + i] = st->pbprime_df_face[2 * i];
+    fns[FN_PBR * FN + i] = st->pbprime_df_face[2 * i + 1];
+  }
+  eng->ssprk_a.assign(st->ssprk_a, st->ssprk_a + 3 * par->kstages);
+  eng->ssprk_beta.assign(st->ssprk_beta, st->ssprk_beta + par->kstages);
+
+  eng->basis = dalloc<double>(eng, hb.size());
+  eng->qstat = dalloc<double>(eng, qs.size());
+  eng->nstat = dalloc<double>(eng, ns.size());
+  eng->fstat = dalloc<double>(eng, fs.size());
+  eng->fnstat = dalloc<double>(eng, fns.size());
+  eng->alpha = dalloc<double>(eng, L);
+  eng->tau_wind = dalloc<double>(eng, 2 * npq);
+  const size_t n3 = 3 * npoin * L;
+  eng->q = dalloc<double>(eng, n3); eng->qp = dalloc<double>(eng, n3); eng->qb = dalloc<double>(eng, 4 * npoin);
+  eng->q2 = dalloc<double>(eng, n3); eng->qp2 = dalloc<double>(eng, n3); eng->qbp = dalloc<double>(eng, 4 * npoin);
+  eng->qf = dalloc<double>(eng, 6 * FN * L); eng->qf2 = dalloc<double>(eng, 6 * FN * L);
+  eng->dpp2 = dalloc<double>(eng, npoin * L);
+  for (int i = 0; i < 4; i++) eng->qbuf[i] = dalloc<double>(eng, 4 * npoin);
+  for (int i = 0; i < 2; i++) eng->gtrace[i] = dalloc<double>(eng, (size_t)E * 16 * ngl);
+  eng->qcoef = dalloc<double>(eng, QC_N * npq); eng->ncoef = dalloc<double>(eng, NC_N * npoin);
+  eng->fcoef = dalloc<double>(eng, FC_N * FQ); eng->fncoef = dalloc<double>(eng, 10 * FN);
+  eng->dpp_graduv = dalloc<double>(eng, 4 * npoin * L); eng->dpprime_visc = dalloc<double>(eng, npoin * L);
+  eng->gdpp_face = dalloc<double>(eng, 10 * FN * L);
+  eng->qacc = dalloc<double>(eng, QA_N * npq); eng->facc = dalloc<double>(eng, FA_N * FQ);
+  eng->nacc = dalloc<double>(eng, NA_N * npoin); eng->gfacc = dalloc<double>(eng, 8 * FN);
+  eng->tau_wind_ave = dalloc<double>(eng, 2 * npq);
+  eng->slmf = dalloc<double>(eng, 2 * npq); eng->slmf_face = dalloc<double>(eng, 2 * FQ);
+  eng->dpp = dalloc<double>(eng, npoin * L);
+  eng->fmass = dalloc<double>(eng, FN * L); eng->fcons = dalloc<double>(eng, FN * L);
+  eng->momL = dalloc<double>(eng, 2 * FN * L); eng->momR = dalloc<double>(eng, 2 * FN * L);
+  eng->lapf = dalloc<double>(eng, 2 * FN * L);
+  eng->rhs = dalloc<double>(eng, 3 * npoin);
+  eng->neg_flag = dalloc<int>(eng, 1);
+  if (eng->alloc_failed) return fail(eng, HNUMO_ERR_DEVICE, "hipMalloc failed (out of device memory?)");
+  HIPCHK(hipHostMalloc((void **)&eng->h_neg, sizeof(int)));
+  HIPCHK(hipMemcpy(eng->basis, hb.data(), hb.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->qstat, qs.data(), qs.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->nstat, ns.data(), ns.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->fstat, fs.data(), fs.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->fnstat, fns.data(), fns.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->alpha, st->alpha, L * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->tau_wind, st->tau_wind, 2 * npq * 8, hipMemcpyHostToDevice));
+
+  DevMesh &m = eng->m;
+  m.nelem = E; m.npoin = (int)npoin; m.npoin_q = (int)npq; m.nface = F; m.ngl = ngl; m.nq = nq; m.L = L;
+  m.efaces = eng->iconn + o_ef; m.eside = eng->iconn + o_es; m.ebc = eng->iconn + o_eb; m.efmap = eng->iconn + o_em;
+  m.enbr_node = eng->iconn + o_en; m.enbr_e = eng->iconn + o_ee; m.enbr_lf = eng->iconn + o_el;
+  m.fnodeL = eng->iconn + o_fl; m.fnodeR = eng->iconn + o_fr; m.fel = eng->iconn + o_fe; m.fer = eng->iconn + o_fer;
+  m.basis = eng->basis; m.qstat = eng->qstat; m.nstat = eng->nstat; m.fstat = eng->fstat; m.fnstat = eng->fnstat;
+  m.alpha = eng->alpha;
+  m.gravity = par->gravity; m.cd = par->cd_mlswe; m.visc = par->visc_mlswe; m.dt = par->dt; m.dt_btp = par->dt_btp;
+  m.botfr = par->botfr;
+  HIPCHK(hipDeviceSynchronize());
+  return HNUMO_OK;
+}
+
+static int upload_state(hnumo_engine *eng, const double *q, const double *qb, const double *qp) {
+  const size_t n3 = 3 * (size_t)eng->npoin * eng->L;
+  if (q) HIPCHK(hipMemcpyAsync(eng->q, q, n3 * 8, hipMemcpyHostToDevice, eng->stream));
+  if (qb) HIPCHK(hipMemcpyAsync(eng->qb, qb, 4 * (size_t)eng->npoin * 8, hipMemcpyHostToDevice, eng->stream));
+  if (qp) HIPCHK(hipMemcpyAsync(eng->qp, qp, n3 * 8, hipMemcpyHostToDevice, eng->stream));
+  return 0;
+}
+
+static int download_state(hnumo_engine *eng, double *q, double *qb, double *qp) {
+  const size_t n3 = 3 * (size_t)eng->npoin * eng->L;
+  if (q) HIPCHK(hipMemcpyAsync(q, eng->q, n3 * 8, hipMemcpyDeviceToHost, eng->stream));
+  if (qb) HIPCHK(hipMemcpyAsync(qb, eng->qb, 4 * (size_t)eng->npoin * 8, hipMemcpyDeviceToHost, eng->stream));
+  if (qp) HIPCHK(hipMemcpyAsync(qp, eng->qp, n3 * 8, hipMemcpyDeviceToHost, eng->stream));
+  HIPCHK(hipStreamSynchronize(eng->stream));
+  return 0;
+}
+
+static int ensure_graph(hnumo_engine *eng) {
+  if (eng->graph_exec) return 0;
+  HIPCHK(hipStreamBeginCapture(eng->stream, hipStreamCaptureModeThreadLocal));
+  launch_step(eng);
+  HIPCHK(hipStreamEndCapture(eng->stream, &eng->graph));
+  HIPCHK(hipGraphInstantiate(&eng->graph_exec, eng->graph, nullptr, nullptr, 0));
+  return 0;
+}
+
+static int run_steps(hnumo_engine *eng, int nsteps) {
+  int rc = ensure_graph(eng);
+  if (rc) return rc;
+  HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
+  for (int s = 0; s < nsteps; s++) HIPCHK(hipGraphLaunch(eng->graph_exec, eng->stream));
+  HIPCHK(hipMemcpyAsync(eng->h_neg, eng->neg_flag, sizeof(int), hipMemcpyDeviceToHost, eng->stream));
+  HIPCHK(hipStreamSynchronize(eng->stream));
+  HIPCHK(hipGetLastError());
+  if (*eng->h_neg & 1) return fail(eng, HNUMO_ERR_NEGATIVE_THICKNESS, "Negative mass in thickness at some points");
+  if (*eng->h_neg & 2) return fail(eng, HNUMO_ERR_NONFINITE, "non-finite barotropic state");
+  return 0;
+}
+
+int hnumo_ti_rk_bcl(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df) {
+  if (!eng) return HNUMO_ERR_INVALID;
+  HIPCHK(hipSetDevice(eng->device));
+  if (!eng->resident || !eng->uploaded) {
+    int rc = upload_state(eng, q_df, qb_df, qprime_df);
+    if (rc) return rc;
+    eng->uploaded = true;
+  }
+  int rc = run_steps(eng, 1);
+  if (rc) return rc;
+  if (!eng->resident) return download_state(eng, q_df, qb_df, qprime_df);
+  return 0;
+}
+
+int hnumo_set_resident(hnumo_engine *eng, int on) {
+  if (!eng) return HNUMO_ERR_INVALID;
+  eng->resident = on != 0;
+  eng->uploaded = false;
+  return 0;
+}
+
+int hnumo_sync(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df) {
+  if (!eng) return HNUMO_ERR_INVALID;
+  HIPCHK(hipSetDevice(eng->device));
+  return download_state(eng, q_df, qb_df, qprime_df);
+}
+
+int hnumo_btp_bcl_coeffs(hnumo_engine *eng, const double *qprime_df) {
+  if (!eng) return HNUMO_ERR_INVALID;
+  HIPCHK(hipSetDevice(eng->device));
+  int rc = upload_state(eng, nullptr, nullptr, qprime_df);
+  if (rc) return rc;
+  launch_bcl_coeffs(eng, eng->qp, eng->qf);
+  HIPCHK(hipStreamSynchronize(eng->stream));
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int hnumo_ti_barotropic_ssprk(hnumo_engine *eng, double *qb_df, const double *qprime_df) {
+  if (!eng) return HNUMO_ERR_INVALID;
+  HIPCHK(hipSetDevice(eng->device));
+  int rc = upload_state(eng, nullptr, qb_df, qprime_df);
+  if (rc) return rc;
+  launch_subcycle(eng, eng->qb, eng->qp);
+  HIPCHK(hipGetLastError());
+  return download_state(eng, nullptr, qb_df, nullptr);
+}
+
+int hnumo_create_rhs_btp(hnumo_engine *eng, double *rhs, const double *qb_df, const double *qprime_df) {
+  if (!eng) return HNUMO_ERR_INVALID;
+  HIPCHK(hipSetDevice(eng->device));
+  int rc = upload_state(eng, nullptr, qb_df, qprime_df);
+  if (rc) return rc;
+  zero_accumulators(eng);
+  DISPATCH(eng, grad_trace(eng, eng->qb, eng->gtrace[0]));
+  StageArgs a{};
+  a.m = eng->m;
+  a.qb_in = eng->qb; a.qb0 = eng->qb; a.qb2 = eng->qb; a.qprime = eng->qp;
+  a.qcoef = eng->qcoef; a.ncoef = eng->ncoef; a.fcoef = eng->fcoef; a.fncoef = eng->fncoef;
+  a.gtrace_in = eng->gtrace[0]; a.gtrace_out = eng->gtrace[1];
+  a.qacc = eng->qacc; a.facc = eng->facc; a.nacc = eng->nacc; a.gfacc = eng->gfacc;
+  a.qb_out = eng->qbuf[0]; a.rhs_out = eng->rhs;
+  a.rhs_only = 1; a.write_grad = 0; a.accumulate = 1;
+  DISPATCH(eng, stage(eng, a));
+  HIPCHK(hipMemcpyAsync(rhs, eng->rhs, 3 * (size_t)eng->npoin * 8, hipMemcpyDeviceToHost, eng->stream));
+  HIPCHK(hipStreamSynchronize(eng->stream));
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// ---- field copy-out in the reference layouts
+int hnumo_get_field(hnumo_engine *eng, const char *name, double *out, int64_t n) {
+  if (!eng || !name || !out) return HNUMO_ERR_INVALID;
+  HIPCHK(hipSetDevice(eng->device));
+  HIPCHK(hipStreamSynchronize(eng->stream));
+  const size_t npq = eng->npq, npoin = eng->npoin, FQ = eng->FQ, FN = eng->FN, L = eng->L;
+  const int nq = eng->nq, ngl = eng->ngl;
+  auto fetch = [&](const double *src, size_t cnt, std::vector<double> &h) -> int {
+    h.resize(cnt);
+    HIPCHK(hipMemcpy(h.data(), src, cnt * 8, hipMemcpyDeviceToHost));
+    return 0;
+  };
+  std::vector<double> h;
+  std::string s(name);
+  auto soa = [&](const double *base, size_t N, std::initializer_list<int> fields) -> int {
+    // interleave SoA fields [field][N] into reference (ncomp, N)
+    size_t nc = fields.size();
+    if ((size_t)n != nc * N) return fail(eng, HNUMO_ERR_INVALID, "field size mismatch");
+    size_t c = 0;
+    for (int fld : fields) {
+      int rc = fetch(base + (size_t)fld * N, N, h);
+      if (rc) return rc;
+      for (size_t i = 0; i < N; i++) out[i * nc + c] = h[i];
+      c++;
+    }
+    return 0;
+  };
+  struct QF1 { const char *nm; int fld; };
+  static const QF1 qsingle[] = {{"ope_ave", QA_OPE}, {"H_ave", QA_H}, {"Qu_ave", QA_QU}, {"Qv_ave", QA_QV},
+                                {"Quv_ave", QA_QUV}, {"ope2_ave", QA_OPE2}};
+  for (auto &x : qsingle)
+    if (s == x.nm) return soa(eng->qacc, npq, {x.fld});
+  if (s == "btp_mass_flux_ave") return soa(eng->qacc, npq, {QA_MFX, QA_MFY});
+  if (s == "uvb_ave") return soa(eng->qacc, npq, {QA_UB, QA_VB});
+  if (s == "tau_bot_ave") return soa(eng->qacc, npq, {QA_TBU, QA_TBV});
+  if (s == "tau_wind_ave") return soa(eng->tau_wind_ave, npq, {0, 1});
+  if (s == "ope2_ave_df") return soa(eng->nacc, npoin, {NA_OPE2});
+  if (s == "uvb_ave_df") return soa(eng->nacc, npoin, {NA_UB, NA_VB});
+  if (s == "graduvb_ave") return soa(eng->nacc, npoin, {NA_G1, NA_G2, NA_G3, NA_G4});
+  if (s == "uvb_face_ave") return soa(eng->facc, FQ, {FA_UL, FA_VL, FA_UR, FA_VR});
+  if (s == "btp_mass_flux_face_ave") return soa(eng->facc, FQ, {FA_MFX, FA_MFY});
+  if (s == "ope_face_ave") return soa(eng->facc, FQ, {FA_OPEL, FA_OPER});
+  if (s == "ope2_face_ave") return soa(eng->facc, FQ, {FA_OPE2L, FA_OPE2R});
+  if (s == "Qu_face_ave") return soa(eng->facc, FQ, {FA_QUU, FA_QUV});
+  if (s == "Qv_face_ave") return soa(eng->facc, FQ, {FA_QVU, FA_QVV});
+  if (s == "H_face_ave") return soa(eng->facc, FQ, {FA_H});
+  if (s == "one_plus_eta_edge_2_ave") return soa(eng->facc, FQ, {FA_OPEE2});
+  if (s == "Quv_face_ave") {  // never accumulated by the reference (mod_rk_mlswe.F90:114-149)
+    if ((size_t)n != 2 * FQ) return fail(eng, HNUMO_ERR_INVALID, "field size mismatch");
+    std::fill(out, out + n, 0.0);
+    return 0;
+  }
+  if (s == "graduvb_face_ave") return soa(eng->gfacc, FN, {0, 1, 2, 3, 4, 5, 6, 7});
+  if (s == "Q_uu_dp") return soa(eng->qcoef, npq, {QC_QUU});
+  if (s == "Q_uv_dp") return soa(eng->qcoef, npq, {QC_QUV});
+  if (s == "Q_vv_dp") return soa(eng->qcoef, npq, {QC_QVV});
+  if (s == "H_bcl") return soa(eng->qcoef, npq, {QC_HBCL});
+  if (s == "Q_uu_dp_edge") return soa(eng->fcoef, FQ, {FC_QUU});
+  if (s == "Q_uv_dp_edge") return soa(eng->fcoef, FQ, {FC_QUV});
+  if (s == "Q_vv_dp_edge") return soa(eng->fcoef, FQ, {FC_QVV});
+  if (s == "H_bcl_edge") return soa(eng->fcoef, FQ, {FC_HBCL});
+  if (s == "btp_dpp_graduv") return soa(eng->ncoef, npoin, {NC_D1, NC_D2, NC_D3, NC_D4});
+  if (s == "pbprime_visc") return soa(eng->ncoef, npoin, {NC_PV});
+  if (s == "btp_graduv_dpp_face") return soa(eng->fncoef, FN, {0, 1, 2, 3, 4, 5, 6, 7, 8, 9});
+  if (s == "sum_layer_mass_flux") return soa(eng->slmf, npq, {0, 1});
+  if (s == "sum_layer_mass_flux_face") return soa(eng->slmf_face, FQ, {0, 1});
+  if (s == "dpprime_visc") {
+    if ((size_t)n != npoin * L) return fail(eng, HNUMO_ERR_INVALID, "field size mismatch");
+    int rc = fetch(eng->dpprime_visc, npoin * L, h);
+    if (rc) return rc;
+    std::copy(h.begin(), h.end(), out);
+    return 0;
+  }
+  (void)nq;
+  (void)ngl;
+  return fail(eng, HNUMO_ERR_INVALID, "unknown field " + s);
+}
+
+int hnumo_bench_steps(hnumo_engine *eng, int nsteps, double *ms_total, double *ms_kernel_avg,
+                      int64_t *kernel_launches) {
+  if (!eng) return HNUMO_ERR_INVALID;
+  HIPCHK(hipSetDevice(eng->device));
+  int rc = ensure_graph(eng);
+  if (rc) return rc;
+  HIPCHK(hipEventRecord(eng->ev0, eng->stream));
+  for (int s = 0; s < nsteps; s++) HIPCHK(hipGraphLaunch(eng->graph_exec, eng->stream));
+  HIPCHK(hipEventRecord(eng->ev1, eng->stream));
+  HIPCHK(hipEventSynchronize(eng->ev1));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, eng->ev0, eng->ev1));
+  if (ms_total) *ms_total = ms;
+  if (ms_kernel_avg) *ms_kernel_avg = -1.0;
+  if (kernel_launches) *kernel_launches = (int64_t)nsteps * 2 * eng->p.N_btp * eng->K;
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,67 @@
+// engine_internal.h -- device-side data layout of the MI355X MLSWE engine.
+//
+// Layout in HBM (all fp64 unless noted; E elements, P = NGL^2 nodes, Q = NQ^2 quad points,
+// F faces, L layers; node index I = e*P + j*NGL + i, quad index Iq = e*Q + jq*NQ + iq):
+//
+//   state            qb(4,npoin), q(3,npoin,L), qprime(3,npoin,L)   -- reference layouts
+//   quad statics     SoA [field][npoin_q]  (coalesced: lane = quad point of one element)
+//   quad accums      SoA [12][npoin_q]     (read-modify-written once per barotropic stage)
+//   nodal statics    SoA [field][npoin]
+//   face statics     [field][F*NQ] or [field][F*NGL]  (lane = face quad point / face node)
+//   face accums      SoA [16][F*NQ]        (owned by the face's left element)
+//   element->face    efaces[e][4], eside[e][4], ebc[e][4], efmap[e][4][NGL],
+//                    enbr_node[e][4][NGL], enbr_e[e][4], enbr_lf[e][4]
+//   gradient traces  gtrace[e][4][4][NGL]  (nodal grad(u_bar) on each element face,
+//                    written by the stage that produced the state, read by the neighbour)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hnumo {
+
+constexpr int MAXNGL = 8;
+constexpr int MAXNQ = 15;
+constexpr int MAXL = 3;
+
+// quad accumulators (mod_variables): index into the [12][npoin_q] block
+enum QAcc { QA_H = 0, QA_QU, QA_QV, QA_QUV, QA_TBU, QA_TBV, QA_OPE, QA_OPE2, QA_MFX, QA_MFY, QA_UB, QA_VB, QA_N };
+// face accumulators: [16][F*NQ]
+enum FAcc {
+  FA_MFX = 0, FA_MFY, FA_H, FA_QUU, FA_QUV, FA_QVU, FA_QVV, FA_OPEL, FA_OPER, FA_OPE2L, FA_OPE2R, FA_OPEE2,
+  FA_UL, FA_UR, FA_VL, FA_VR, FA_N
+};
+// nodal accumulators: [7][npoin] (ope2_ave_df, uvb_ave_df(2), graduvb_ave(4))
+enum NAcc { NA_OPE2 = 0, NA_UB, NA_VB, NA_G1, NA_G2, NA_G3, NA_G4, NA_N };
+// quad statics: [QS_N][npoin_q]
+enum QStat { QS_W = 0, QS_COR, QS_TW1, QS_TW2, QS_GZ1, QS_GZ2, QS_OOP, QS_EX, QS_EY, QS_NX, QS_NY, QS_PB, QS_N };
+// per-sub-cycle baroclinic coefficients at quad points: [4][npoin_q]
+enum QCoef { QC_HBCL = 0, QC_QUU, QC_QUV, QC_QVV, QC_N };
+// nodal statics: [NS_N][npoin]
+enum NStat { NS_PB = 0, NS_OOP, NS_MINV, NS_W, NS_EX, NS_EY, NS_NX, NS_NY, NS_ZB, NS_F2, NS_A, NS_B, NS_N };
+// per-sub-cycle nodal coefficients: pbprime_visc, btp_dpp_graduv(4): [5][npoin]
+enum NCoef { NC_PV = 0, NC_D1, NC_D2, NC_D3, NC_D4, NC_N };
+// face statics at face quad points: [FS_N][F*NQ]
+enum FStat {
+  FS_NX = 0, FS_NY, FS_W, FS_CL, FS_CR, FS_CLR, FS_CML, FS_CMR, FS_CMLR, FS_OOPE, FS_PBL, FS_PBR, FS_ZBL, FS_ZBR, FS_N
+};
+// per-sub-cycle face coefficients at face quad points: [4][F*NQ]
+enum FCoef { FC_QUU = 0, FC_QUV, FC_QVV, FC_HBCL, FC_N };
+// face statics at face nodes: [FN_N][F*NGL]
+enum FNStat { FN_NX = 0, FN_NY, FN_W, FN_PBL, FN_PBR, FN_N };
+
+struct DevMesh {
+  int nelem, npoin, npoin_q, nface, ngl, nq, L;
+  const int *efaces, *eside, *ebc, *efmap, *enbr_node, *enbr_e, *enbr_lf;
+  const int *fnodeL, *fnodeR;     // [F][NGL] global node of face node n, left/right (-1 if none)
+  const int *fel, *fer;           // [F] face(7)-1, face(8) (raw: >0 element+1, <=0 code)
+  const double *basis;            // psiq[NGL*NQ] dpsiq[NGL*NQ] dpsi[NGL*NGL]
+  const double *qstat;            // [QS_N][npoin_q]
+  const double *nstat;            // [NS_N][npoin]
+  const double *fstat;            // [FS_N][F*NQ]
+  const double *fnstat;           // [FN_N][F*NGL]
+  const double *alpha;            // [L]
+  double gravity, cd, visc, dt, dt_btp;
+  int botfr;
+};
+
+}  // namespace hnumo

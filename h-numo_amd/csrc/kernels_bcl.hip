@@ -1,0 +1,1068 @@
+// kernels_bcl.hip -- baroclinic (layer) kernels of the MI355X MLSWE engine.
+//
+// Pattern: face kernels (one 64-thread workgroup per face) evaluate numerical fluxes
+// at face quad points from face traces and project them onto the face nodes
+// (per-face contribution buffers, no atomics); element kernels (one workgroup per
+// element, all layers) evaluate volume terms by sum factorisation, gather the four
+// faces' contributions in face-id order and apply the nodal updates.
+//
+// Reference routines restated here (arithmetic per term as in the reference):
+//   btp_bcl_coeffs_qdf            mod_barotropic_terms.F90:219-409
+//   extract_qprime_df_face         mod_layer_terms.F90:354-415 (+ extract_dprime :417-465)
+//   layer_mass_rhs                 mod_create_rhs_mlswe.F90:53-78, :822-877, :922-1034
+//   apply_consistency              mod_splitting.F90:324-366, mod_layer_terms.F90:57-137,
+//                                  mod_create_rhs_mlswe.F90:879-920, :1036-1115
+//   bcl_create_laplacian           mod_laplacian_quad.F90:227-248, :392-425, :521-611
+//   create_rhs_dynamics_volume_layers  mod_create_rhs_mlswe.F90:281-456
+//   Apply_layers_fluxes            mod_create_rhs_mlswe.F90:458-820
+//   momentum / momentum_mass update, implicit Coriolis, layer_mom_boundary_df,
+//   evaluate_bcl / evaluate_bcl_v1 / extract_velocity
+//                                  mod_splitting.F90:94-287, mod_layer_terms.F90:198-320, :529-584
+#include "engine_internal.h"
+
+namespace hnumo {
+
+#define QF(v, s, n, f, k) qf[((((size_t)(k) * F + (f)) * NGL + (n)) * 2 + (s)) * 3 + (v)]
+
+template <int NGL, int NQ>
+struct Blk {
+  static constexpr int P = NGL * NGL, Q = NQ * NQ, BS = ((Q + 63) / 64) * 64;
+};
+
+__device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : (b < a ? b : a); }
+__device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : (b > a ? b : a); }
+
+template <int NGL, int NQ>
+__device__ __forceinline__ void load_basis(const DevMesh &m, double *s_psiq, double *s_dpsiq, double *s_dpsi, int tid,
+                                           int bs) {
+  for (int t = tid; t < NGL * NQ; t += bs) {
+    s_psiq[t] = m.basis[t];
+    s_dpsiq[t] = m.basis[NGL * NQ + t];
+  }
+  for (int t = tid; t < NGL * NGL; t += bs) s_dpsi[t] = m.basis[2 * NGL * NQ + t];
+}
+
+// ===================================================================== face traces
+// extract_qprime_df_face: qf(3,2,ngl,nface,L) from nodal qprime(3,npoin,L), with wall ghosts.
+// only_dp: extract_dprime_df_face into component 1 (no reflection).
+template <int NGL>
+__global__ void extract_face_kernel(DevMesh m, const double *qp, double *qf, int only_dp) {
+  const int F = m.nface, L = m.L, npoin = m.npoin;
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (size_t)F * NGL) return;
+  const int f = gid / NGL, n = gid % NGL;
+  const int IL = m.fnodeL[gid], IR = m.fnodeR[gid], er = m.fer[f];
+  for (int k = 0; k < L; k++) {
+    const double *q = qp + (size_t)k * 3 * npoin;
+    if (only_dp) {
+      double l = q[(size_t)IL * 3];
+      QF(0, 0, n, f, k) = l;
+      QF(0, 1, n, f, k) = er > 0 ? q[(size_t)IR * 3] : l;
+      continue;
+    }
+    double l0 = q[(size_t)IL * 3], l1 = q[(size_t)IL * 3 + 1], l2 = q[(size_t)IL * 3 + 2];
+    QF(0, 0, n, f, k) = l0;
+    QF(1, 0, n, f, k) = l1;
+    QF(2, 0, n, f, k) = l2;
+    if (er > 0) {
+      QF(0, 1, n, f, k) = q[(size_t)IR * 3];
+      QF(1, 1, n, f, k) = q[(size_t)IR * 3 + 1];
+      QF(2, 1, n, f, k) = q[(size_t)IR * 3 + 2];
+    } else {
+      double r1 = l1, r2 = l2;
+      if (er == -4) {
+        double nx = m.fnstat[FN_NX * (size_t)F * NGL + gid], ny = m.fnstat[FN_NY * (size_t)F * NGL + gid];
+        double un = l1 * nx + l2 * ny;
+        r1 = l1 - 2.0 * un * nx;
+        r2 = l2 - 2.0 * un * ny;
+      } else if (er == -2) {
+        r1 = -l1;
+        r2 = -l2;
+      }
+      QF(0, 1, n, f, k) = l0;
+      QF(1, 1, n, f, k) = r1;
+      QF(2, 1, n, f, k) = r2;
+    }
+  }
+}
+
+// out = 0.5*(a + b) elementwise (ti_rk_bcl.F90:64-65,79-80); comp1_only: stride-3 component 1
+__global__ void average_kernel(double *out, const double *a, const double *b, size_t n, int stride) {
+  const size_t stride_ = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride_) {
+    size_t j = i * stride;
+    out[j] = 0.5 * (a[j] + b[j]);
+  }
+}
+
+// ======================================================= btp_bcl_coeffs_qdf: element
+// Q_uu_dp, Q_uv_dp, Q_vv_dp, H_bcl at quad points; dpp_graduv, btp_dpp_graduv,
+// pbprime_visc at nodes (dpprime_visc = qprime(1,:,:) is stored for the layer LDG).
+template <int NGL, int NQ>
+__global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
+    bcl_coeffs_elem_kernel(DevMesh m, const double *qp, double *qcoef, double *ncoef, double *dpp_graduv,
+                           double *dpprime_visc) {
+  constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BS;
+  const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q;
+  __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL];
+  __shared__ double s_q[MAXL][3][P];
+  __shared__ double s_T[MAXL * 3][NQ * NGL];
+  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, tid, BS);
+  for (int t = tid; t < L * 3 * P; t += BS) {
+    int k = t / (3 * P), r = t % (3 * P);
+    s_q[k][r % 3][r / 3] = qp[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
+  }
+  __syncthreads();
+  for (int t = tid; t < NQ * NGL; t += BS) {
+    int iq = t / NGL, mm = t % NGL;
+    for (int k = 0; k < L; k++)
+      for (int v = 0; v < 3; v++) {
+        double acc = 0.0;
+        for (int n = 0; n < NGL; n++) acc += s_psiq[n * NQ + iq] * s_q[k][v][mm * NGL + n];
+        s_T[k * 3 + v][t] = acc;
+      }
+  }
+  __syncthreads();
+  for (int q = tid; q < Q; q += BS) {
+    const int iq = q % NQ, jq = q / NQ;
+    double quu = 0.0, quv = 0.0, qvv = 0.0, hb = 0.0, pk = 0.0;
+    for (int k = 0; k < L; k++) {
+      double qq[3];
+      for (int v = 0; v < 3; v++) {
+        double acc = 0.0;
+        for (int mm = 0; mm < NGL; mm++) acc += s_psiq[mm * NQ + jq] * s_T[k * 3 + v][iq * NGL + mm];
+        qq[v] = acc;
+      }
+      quu = quu + qq[1] * (qq[1] * qq[0]);
+      quv = quv + qq[2] * (qq[1] * qq[0]);
+      qvv = qvv + qq[2] * (qq[2] * qq[0]);
+      double pk1 = pk + qq[0];
+      hb = hb + 0.5 * m.alpha[k] * (pk1 * pk1 - pk * pk);
+      pk = pk1;
+    }
+    const size_t Iq = (size_t)e * Q + q;
+    qcoef[QC_QUU * (size_t)npq + Iq] = quu;
+    qcoef[QC_QUV * (size_t)npq + Iq] = quv;
+    qcoef[QC_QVV * (size_t)npq + Iq] = qvv;
+    qcoef[QC_HBCL * (size_t)npq + Iq] = hb;
+  }
+  for (int p = tid; p < P; p += BS) {
+    const int i = p % NGL, j = p / NGL;
+    const size_t I = (size_t)e * P + p;
+    const double ex = m.nstat[NS_EX * (size_t)npoin + I], ey = m.nstat[NS_EY * (size_t)npoin + I];
+    const double nx = m.nstat[NS_NX * (size_t)npoin + I], ny = m.nstat[NS_NY * (size_t)npoin + I];
+    double sum[4] = {0, 0, 0, 0}, pv = 0.0;
+    for (int k = 0; k < L; k++) {
+      double ux = 0, uy = 0, vx = 0, vy = 0;
+      for (int n = 0; n < NGL; n++) {
+        double dx = s_dpsi[n * NGL + i], dy = s_dpsi[n * NGL + j];
+        ux += dx * s_q[k][1][j * NGL + n];
+        vx += dx * s_q[k][2][j * NGL + n];
+        uy += dy * s_q[k][1][n * NGL + i];
+        vy += dy * s_q[k][2][n * NGL + i];
+      }
+      double g[4] = {ex * ux + nx * uy, ey * ux + ny * uy, ex * vx + nx * vy, ey * vx + ny * vy};
+      double d = s_q[k][0][p];
+      dpprime_visc[(size_t)k * npoin + I] = d;
+      for (int c = 0; c < 4; c++) {
+        double dg = d * g[c];
+        dpp_graduv[((size_t)k * 4 + c) * npoin + I] = dg;
+        sum[c] = sum[c] + dg;
+      }
+      pv = pv + d;
+    }
+    ncoef[NC_PV * (size_t)npoin + I] = pv;
+    for (int c = 0; c < 4; c++) ncoef[(NC_D1 + c) * (size_t)npoin + I] = sum[c];
+  }
+}
+
+// ========================================================= btp_bcl_coeffs_qdf: faces
+// Q_*_dp_edge, H_bcl_edge at face quad points (mod_barotropic_terms.F90:306-337) and the
+// face traces graduv_dpp_face + their layer sum btp_graduv_dpp_face (:339-407).
+template <int NGL, int NQ>
+__global__ void __launch_bounds__(64)
+    bcl_coeffs_face_kernel(DevMesh m, const double *qf, const double *dpp_graduv, const double *dpprime_visc,
+                           double *fcoef, double *fncoef, double *gdpp_face) {
+  const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L, npoin = m.npoin;
+  __shared__ double s_psiq[NGL * NQ];
+  for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
+  __syncthreads();
+  const size_t FQ = (size_t)F * NQ, FN = (size_t)F * NGL;
+  if (tid < NQ) {
+    const int iq = tid;
+    double quu = 0, quv = 0, qvv = 0, hb = 0, pl = 0, pr = 0;
+    for (int k = 0; k < L; k++) {
+      double ql[3] = {0, 0, 0}, qr[3] = {0, 0, 0};
+      for (int n = 0; n < NGL; n++) {
+        double hi = s_psiq[n * NQ + iq];
+        for (int v = 0; v < 3; v++) {
+          ql[v] = ql[v] + hi * QF(v, 0, n, f, k);
+          qr[v] = qr[v] + hi * QF(v, 1, n, f, k);
+        }
+      }
+      quu = quu + 0.5 * ((ql[1] * ql[1] * ql[0]) + (qr[1] * qr[1] * qr[0]));
+      quv = quv + 0.5 * ((ql[2] * ql[1] * ql[0]) + (qr[2] * qr[1] * qr[0]));
+      qvv = qvv + 0.5 * ((ql[2] * ql[2] * ql[0]) + (qr[2] * qr[2] * qr[0]));
+      double pl1 = pl + ql[0];
+      double left_dp = 0.5 * m.alpha[k] * (pl1 * pl1 - pl * pl);
+      double pr1 = pr + qr[0];
+      double right_dp = 0.5 * m.alpha[k] * (pr1 * pr1 - pr * pr);
+      hb = hb + 0.5 * (left_dp + right_dp);
+      pl = pl1;
+      pr = pr1;
+    }
+    const size_t fq = (size_t)f * NQ + iq;
+    fcoef[FC_QUU * FQ + fq] = quu;
+    fcoef[FC_QUV * FQ + fq] = quv;
+    fcoef[FC_QVV * FQ + fq] = qvv;
+    fcoef[FC_HBCL * FQ + fq] = hb;
+  } else if (tid >= 32 && tid < 32 + NGL) {
+    const int n = tid - 32, er = m.fer[f];
+    const size_t fn = (size_t)f * NGL + n;
+    const int IL = m.fnodeL[fn], IR = m.fnodeR[fn];
+    double nx = m.fnstat[FN_NX * FN + fn], ny = m.fnstat[FN_NY * FN + fn];
+    double bsum[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < L; k++) {
+      double l[5], r[5];
+      for (int c = 0; c < 4; c++) l[c] = dpp_graduv[((size_t)k * 4 + c) * npoin + IL];
+      l[4] = dpprime_visc[(size_t)k * npoin + IL];
+      if (er > 0) {
+        for (int c = 0; c < 4; c++) r[c] = dpp_graduv[((size_t)k * 4 + c) * npoin + IR];
+        r[4] = dpprime_visc[(size_t)k * npoin + IR];
+      } else {
+        for (int c = 0; c < 5; c++) r[c] = l[c];
+        if (er == -4) {
+          double un = l[0] * nx + l[1] * ny;
+          r[0] = l[0] - 2.0 * un * nx;
+          r[1] = l[1] - 2.0 * un * ny;
+          un = l[2] * nx + l[3] * ny;
+          r[2] = l[2] - 2.0 * un * nx;
+          r[3] = l[3] - 2.0 * un * ny;
+        }
+      }
+      for (int c = 0; c < 5; c++) {
+        gdpp_face[((size_t)k * 10 + c) * FN + fn] = l[c];
+        gdpp_face[((size_t)k * 10 + 5 + c) * FN + fn] = r[c];
+      }
+      for (int c = 0; c < 5; c++) {
+        bsum[c] = bsum[c] + l[c];
+        bsum[5 + c] = bsum[5 + c] + r[c];
+      }
+    }
+    for (int c = 0; c < 10; c++) fncoef[(size_t)c * FN + fn] = bsum[c];
+  }
+}
+
+// ====================================================== layer mass: face fluxes
+// create_layer_mass_flux (mod_create_rhs_mlswe.F90:922-1034): per face, per layer, upwind
+// mass flux at face quad points projected onto the face nodes.  fmass[k][f][n] is the
+// contribution to the LEFT element's node (the right element receives its negative).
+template <int NGL, int NQ>
+__global__ void __launch_bounds__(64)
+    mass_flux_face_kernel(DevMesh m, const double *qf, const double *facc, double *fmass, double *slmf_face) {
+  const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L;
+  __shared__ double s_psiq[NGL * NQ];
+  __shared__ double s_fl[MAXL][NQ];
+  for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
+  __syncthreads();
+  const size_t FQ = (size_t)F * NQ;
+  if (tid < NQ) {
+    const int iq = tid;
+    const size_t fq = (size_t)f * NQ + iq;
+    double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq], wq = m.fstat[FS_W * FQ + fq];
+    double qbl0 = facc[FA_OPEL * FQ + fq], qbr0 = facc[FA_OPER * FQ + fq];
+    double qbl1 = facc[FA_UL * FQ + fq], qbr1 = facc[FA_UR * FQ + fq];
+    double qbl2 = facc[FA_VL * FQ + fq], qbr2 = facc[FA_VR * FQ + fq];
+    double su = 0.0, sv = 0.0;
+    for (int k = 0; k < L; k++) {
+      double ql[3] = {0, 0, 0}, qr[3] = {0, 0, 0};
+      for (int n = 0; n < NGL; n++) {
+        double hi = s_psiq[n * NQ + iq];
+        for (int v = 0; v < 3; v++) {
+          ql[v] = ql[v] + hi * QF(v, 0, n, f, k);
+          qr[v] = qr[v] + hi * QF(v, 1, n, f, k);
+        }
+      }
+      double uu = 0.5 * ((ql[1] + qbl1) + (qr[1] + qbr1));
+      double vv = 0.5 * ((ql[2] + qbl2) + (qr[2] + qbr2));
+      double dpl = qbl0 * ql[0], dpr = qbr0 * qr[0];
+      double feu = (uu * nxl > 0.0) ? uu * dpl : uu * dpr;
+      double fev = (vv * nyl > 0.0) ? vv * dpl : vv * dpr;
+      su = su + feu;
+      sv = sv + fev;
+      s_fl[k][iq] = -wq * (nxl * feu + nyl * fev);
+    }
+    slmf_face[0 * FQ + fq] = su;
+    slmf_face[1 * FQ + fq] = sv;
+  }
+  __syncthreads();
+  if (tid < L * NGL) {
+    const int k = tid / NGL, n = tid % NGL;
+    double s = 0.0;
+    for (int iq = 0; iq < NQ; iq++) s += s_psiq[n * NQ + iq] * s_fl[k][iq];
+    fmass[((size_t)k * F + f) * NGL + n] = s;
+  }
+}
+
+// =============================================== consistency: face deficit fluxes
+// evaluate_consistency_face + create_consistency_mass_flux: dpp = dp'(npoin,L) nodal.
+template <int NGL, int NQ>
+__global__ void __launch_bounds__(64)
+    cons_flux_face_kernel(DevMesh m, const double *dpp, const double *facc, const double *slmf_face, double *fcons) {
+  const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L, npoin = m.npoin;
+  __shared__ double s_psiq[NGL * NQ];
+  __shared__ double s_fl[MAXL][NQ];
+  for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
+  __syncthreads();
+  const size_t FQ = (size_t)F * NQ;
+  if (tid < NQ) {
+    const int iq = tid, er = m.fer[f];
+    const size_t fq = (size_t)f * NQ + iq;
+    double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq], wq = m.fstat[FS_W * FQ + fq];
+    double d1 = facc[FA_MFX * FQ + fq] - slmf_face[0 * FQ + fq];
+    double d2 = facc[FA_MFY * FQ + fq] - slmf_face[1 * FQ + fq];
+    double pbl = m.fstat[FS_PBL * FQ + fq], pbr = m.fstat[FS_PBR * FQ + fq];
+    for (int k = 0; k < L; k++) {
+      double ql = 0.0, qr = 0.0;
+      for (int n = 0; n < NGL; n++)
+        ql = ql + s_psiq[n * NQ + iq] * dpp[(size_t)k * npoin + m.fnodeL[(size_t)f * NGL + n]];
+      if (er > 0) {
+        for (int n = 0; n < NGL; n++)
+          qr = qr + s_psiq[n * NQ + iq] * dpp[(size_t)k * npoin + m.fnodeR[(size_t)f * NGL + n]];
+      } else {
+        qr = ql;
+      }
+      double wl = ql / pbl, wr = qr / pbr;
+      double m11 = wl * d1, m21 = wl * d2, m12 = wr * d1, m22 = wr * d2;
+      double feu = (m11 * nxl > 0.0) ? m11 : m12;
+      double fev = (m21 * nyl > 0.0) ? m21 : m22;
+      s_fl[k][iq] = -wq * (nxl * feu + nyl * fev);
+    }
+  }
+  __syncthreads();
+  if (tid < L * NGL) {
+    const int k = tid / NGL, n = tid % NGL;
+    double s = 0.0;
+    for (int iq = 0; iq < NQ; iq++) s += s_psiq[n * NQ + iq] * s_fl[k][iq];
+    fcons[((size_t)k * F + f) * NGL + n] = s;
+  }
+}
+
+// gather of an antisymmetric face contribution at local node p of element e (left: +c, right: -c)
+template <int NGL>
+__device__ __forceinline__ double gather_anti(const int *s_map, const int *s_face, const int *s_side, const double *buf,
+                                              int F, int p) {
+  double s = 0.0;
+  for (int lf = 0; lf < 4; lf++)
+    for (int n = 0; n < NGL; n++)
+      if (s_map[lf * NGL + n] == p) {
+        double c = buf[(size_t)s_face[lf] * NGL + n];
+        s += s_side[lf] == 0 ? c : -c;
+      }
+  return s;
+}
+
+// ==================================================== layer mass: element update
+// create_layers_volume_mass + gather + massinv + q(1) += dt*dp_advec + negativity check
+// (mod_splitting.F90:69-78 / :224-232), then dp' = q(1)/(sum_k q(1)/pb') for consistency.
+template <int NGL, int NQ>
+__global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
+    mass_elem_kernel(DevMesh m, const double *qp, const double *qacc, const double *fmass, double *q,
+                     double *slmf, double *dpp, int *neg_flag) {
+  constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BS;
+  const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
+  __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL];
+  __shared__ double s_q[MAXL][3][P];
+  __shared__ double s_T[MAXL * 3][NQ * NGL];
+  __shared__ double s_G[MAXL][2][Q];
+  __shared__ double s_A[MAXL][2][NQ * NGL];
+  __shared__ double s_new[MAXL][P];
+  __shared__ int s_map[4 * NGL], s_face[4], s_side[4];
+  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, tid, BS);
+  if (tid < 4) {
+    s_face[tid] = m.efaces[e * 4 + tid];
+    s_side[tid] = m.eside[e * 4 + tid];
+  }
+  for (int t = tid; t < 4 * NGL; t += BS) s_map[t] = m.efmap[e * 4 * NGL + t];
+  for (int t = tid; t < L * 3 * P; t += BS) {
+    int k = t / (3 * P), r = t % (3 * P);
+    s_q[k][r % 3][r / 3] = qp[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
+  }
+  __syncthreads();
+  for (int t = tid; t < NQ * NGL; t += BS) {
+    int iq = t / NGL, mm = t % NGL;
+    for (int k = 0; k < L; k++)
+      for (int v = 0; v < 3; v++) {
+        double acc = 0.0;
+        for (int n = 0; n < NGL; n++) acc += s_psiq[n * NQ + iq] * s_q[k][v][mm * NGL + n];
+        s_T[k * 3 + v][t] = acc;
+      }
+  }
+  __syncthreads();
+  for (int q = tid; q < Q; q += BS) {
+    const int iq = q % NQ, jq = q / NQ;
+    const size_t Iq = (size_t)e * Q + q;
+    double qb0 = qacc[QA_OPE * (size_t)npq + Iq], qb1 = qacc[QA_UB * (size_t)npq + Iq],
+           qb2 = qacc[QA_VB * (size_t)npq + Iq];
+    double wq = m.qstat[QS_W * (size_t)npq + Iq];
+    double ex = m.qstat[QS_EX * (size_t)npq + Iq], ey = m.qstat[QS_EY * (size_t)npq + Iq];
+    double nx = m.qstat[QS_NX * (size_t)npq + Iq], ny = m.qstat[QS_NY * (size_t)npq + Iq];
+    double su = 0.0, sv = 0.0;
+    for (int k = 0; k < L; k++) {
+      double qq[3];
+      for (int v = 0; v < 3; v++) {
+        double acc = 0.0;
+        for (int mm = 0; mm < NGL; mm++) acc += s_psiq[mm * NQ + jq] * s_T[k * 3 + v][iq * NGL + mm];
+        qq[v] = acc;
+      }
+      double dp_temp = qq[0] * qb0;
+      double udp = (qq[1] + qb1) * dp_temp;
+      double vdp = (qq[2] + qb2) * dp_temp;
+      su = su + udp;
+      sv = sv + vdp;
+      s_G[k][0][q] = wq * (ex * udp + ey * vdp);
+      s_G[k][1][q] = wq * (nx * udp + ny * vdp);
+    }
+    slmf[0 * (size_t)npq + Iq] = su;
+    slmf[1 * (size_t)npq + Iq] = sv;
+  }
+  __syncthreads();
+  for (int t = tid; t < NQ * NGL; t += BS) {
+    int iq = t / NGL, mm = t % NGL;
+    for (int k = 0; k < L; k++) {
+      double ax = 0, ap = 0;
+      for (int jq = 0; jq < NQ; jq++) {
+        ax += s_psiq[mm * NQ + jq] * s_G[k][0][jq * NQ + iq];
+        ap += s_dpsiq[mm * NQ + jq] * s_G[k][1][jq * NQ + iq];
+      }
+      s_A[k][0][t] = ax;
+      s_A[k][1][t] = ap;
+    }
+  }
+  __syncthreads();
+  for (int p = tid; p < P; p += BS) {
+    const int i = p % NGL, j = p / NGL;
+    const size_t I = (size_t)e * P + p;
+    const double mi = m.nstat[NS_MINV * (size_t)npoin + I];
+    double sum = 0.0;
+    for (int k = 0; k < L; k++) {
+      double r = 0.0;
+      for (int iq = 0; iq < NQ; iq++) r += s_dpsiq[i * NQ + iq] * s_A[k][0][iq * NGL + j] + s_psiq[i * NQ + iq] * s_A[k][1][iq * NGL + j];
+      r += gather_anti<NGL>(s_map, s_face, s_side, fmass + (size_t)k * F * NGL, F, p);
+      double adv = mi * r;
+      double v = q[((size_t)k * npoin + I) * 3] + m.dt * adv;
+      if (v < 0.0) atomicOr(neg_flag, 1);
+      q[((size_t)k * npoin + I) * 3] = v;
+      s_new[k][p] = v;
+      sum = sum + v;
+    }
+    double ope = sum / m.nstat[NS_PB * (size_t)npoin + I];
+    for (int k = 0; k < L; k++) dpp[(size_t)k * npoin + I] = s_new[k][p] / ope;
+  }
+}
+
+// ============================================== consistency: element update
+// create_consistency_volume_mass + gather + q(1) += dt*massinv*dp_advec (mod_splitting.F90:362-364).
+// finalize_dp: (thickness) also qprime(1,:,k) = q(1,:,k)/(sum_k q(1)/pb') (mod_splitting.F90:84-87).
+template <int NGL, int NQ>
+__global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
+    cons_elem_kernel(DevMesh m, const double *dpp, const double *qacc, const double *slmf, const double *fcons,
+                     double *q, double *qp_out, int finalize_dp) {
+  constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BS;
+  const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
+  __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL];
+  __shared__ double s_d[MAXL][P];
+  __shared__ double s_T[MAXL][NQ * NGL];
+  __shared__ double s_G[MAXL][2][Q];
+  __shared__ double s_A[MAXL][2][NQ * NGL];
+  __shared__ double s_new[MAXL][P];
+  __shared__ int s_map[4 * NGL], s_face[4], s_side[4];
+  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, tid, BS);
+  if (tid < 4) {
+    s_face[tid] = m.efaces[e * 4 + tid];
+    s_side[tid] = m.eside[e * 4 + tid];
+  }
+  for (int t = tid; t < 4 * NGL; t += BS) s_map[t] = m.efmap[e * 4 * NGL + t];
+  for (int t = tid; t < L * P; t += BS) s_d[t / P][t % P] = dpp[(size_t)(t / P) * npoin + (size_t)e * P + t % P];
+  __syncthreads();
+  for (int t = tid; t < NQ * NGL; t += BS) {
+    int iq = t / NGL, mm = t % NGL;
+    for (int k = 0; k < L; k++) {
+      double acc = 0.0;
+      for (int n = 0; n < NGL; n++) acc += s_psiq[n * NQ + iq] * s_d[k][mm * NGL + n];
+      s_T[k][t] = acc;
+    }
+  }
+  __syncthreads();
+  for (int q = tid; q < Q; q += BS) {
+    const int iq = q % NQ, jq = q / NQ;
+    const size_t Iq = (size_t)e * Q + q;
+    double wq = m.qstat[QS_W * (size_t)npq + Iq];
+    double ex = m.qstat[QS_EX * (size_t)npq + Iq], ey = m.qstat[QS_EY * (size_t)npq + Iq];
+    double nx = m.qstat[QS_NX * (size_t)npq + Iq], ny = m.qstat[QS_NY * (size_t)npq + Iq];
+    double pb = m.qstat[QS_PB * (size_t)npq + Iq];
+    double dx = qacc[QA_MFX * (size_t)npq + Iq] - slmf[0 * (size_t)npq + Iq];
+    double dy = qacc[QA_MFY * (size_t)npq + Iq] - slmf[1 * (size_t)npq + Iq];
+    for (int k = 0; k < L; k++) {
+      double dp = 0.0;
+      for (int mm = 0; mm < NGL; mm++) dp += s_psiq[mm * NQ + jq] * s_T[k][iq * NGL + mm];
+      double weight = dp / pb;
+      double udp = weight * dx, vdp = weight * dy;
+      s_G[k][0][q] = wq * (ex * udp + ey * vdp);
+      s_G[k][1][q] = wq * (nx * udp + ny * vdp);
+    }
+  }
+  __syncthreads();
+  for (int t = tid; t < NQ * NGL; t += BS) {
+    int iq = t / NGL, mm = t % NGL;
+    for (int k = 0; k < L; k++) {
+      double ax = 0, ap = 0;
+      for (int jq = 0; jq < NQ; jq++) {
+        ax += s_psiq[mm * NQ + jq] * s_G[k][0][jq * NQ + iq];
+        ap += s_dpsiq[mm * NQ + jq] * s_G[k][1][jq * NQ + iq];
+      }
+      s_A[k][0][t] = ax;
+      s_A[k][1][t] = ap;
+    }
+  }
+  __syncthreads();
+  for (int p = tid; p < P; p += BS) {
+    const int i = p % NGL, j = p / NGL;
+    const size_t I = (size_t)e * P + p;
+    const double mi = m.nstat[NS_MINV * (size_t)npoin + I];
+    double sum = 0.0;
+    for (int k = 0; k < L; k++) {
+      double r = 0.0;
+      for (int iq = 0; iq < NQ; iq++) r += s_dpsiq[i * NQ + iq] * s_A[k][0][iq * NGL + j] + s_psiq[i * NQ + iq] * s_A[k][1][iq * NGL + j];
+      r += gather_anti<NGL>(s_map, s_face, s_side, fcons + (size_t)k * F * NGL, F, p);
+      double v = q[((size_t)k * npoin + I) * 3] + m.dt * mi * r;
+      q[((size_t)k * npoin + I) * 3] = v;
+      s_new[k][p] = v;
+      sum = sum + v;
+    }
+    if (finalize_dp) {
+      double ope = sum / m.nstat[NS_PB * (size_t)npoin + I];
+      for (int k = 0; k < L; k++) qp_out[((size_t)k * npoin + I) * 3] = s_new[k][p] / ope;
+    }
+  }
+}
+
+// ========================================== layer momentum: face kernel
+// Apply_layers_fluxes (mod_create_rhs_mlswe.F90:458-820) and the layer LDG flux
+// bcl_create_rhs_laplacian_flux (mod_laplacian_quad.F90:521-611).  Outputs per face
+// node: momL/momR[k][2][F][NGL] (advection+pressure, to left / right element) and
+// lap[k][2][F][NGL] (LDG, antisymmetric, value for the left element).
+template <int NGL, int NQ>
+__global__ void __launch_bounds__(64)
+    mom_flux_face_kernel(DevMesh m, const double *qf, const double *facc, const double *gdpp_face,
+                         const double *gfacc, double *momL, double *momR, double *lap) {
+  const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L;
+  __shared__ double s_psiq[NGL * NQ];
+  __shared__ double s_cl[MAXL][2][NQ], s_cr[MAXL][2][NQ];
+  for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
+  __syncthreads();
+  const size_t FQ = (size_t)F * NQ, FN = (size_t)F * NGL;
+  const int er = m.fer[f];
+  const double g = m.gravity, eps1 = 1.0e-20;
+  if (tid < NQ) {
+    const int iq = tid;
+    const size_t fq = (size_t)f * NQ + iq;
+    const double *alpha = m.alpha;
+    double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq], wq = m.fstat[FS_W * FQ + fq];
+    double qbl0 = facc[FA_OPEL * FQ + fq], qbr0 = facc[FA_OPER * FQ + fq];
+    double qbl1 = facc[FA_UL * FQ + fq], qbr1 = facc[FA_UR * FQ + fq];
+    double qbl2 = facc[FA_VL * FQ + fq], qbr2 = facc[FA_VR * FQ + fq];
+    double ql[MAXL][3], qr[MAXL][3], udpl[MAXL], udpr[MAXL], vdpl[MAXL], vdpr[MAXL];
+    double udpf[2][MAXL], vdpf[2][MAXL], Hf[2][MAXL];
+    for (int k = 0; k < L; k++) {
+      for (int v = 0; v < 3; v++) ql[k][v] = qr[k][v] = 0.0;
+      for (int n = 0; n < NGL; n++) {
+        double hi = s_psiq[n * NQ + iq];
+        for (int v = 0; v < 3; v++) {
+          ql[k][v] = ql[k][v] + hi * QF(v, 0, n, f, k);
+          qr[k][v] = qr[k][v] + hi * QF(v, 1, n, f, k);
+        }
+      }
+      double dpl = qbl0 * ql[k][0], dpr = qbr0 * qr[k][0];
+      double ul = ql[k][1] + qbl1, ur = qr[k][1] + qbr1, vl = ql[k][2] + qbl2, vr = qr[k][2] + qbr2;
+      double uu = 0.5 * (ul + ur), vv = 0.5 * (vl + vr);
+      udpl[k] = ul * dpl;
+      udpr[k] = ur * dpr;
+      vdpl[k] = vl * dpl;
+      vdpr[k] = vr * dpr;
+      if (uu * nxl > 0.0) {
+        udpf[0][k] = uu * (ul * dpl);
+        vdpf[0][k] = uu * (vl * dpl);
+      } else {
+        udpf[0][k] = uu * (ur * dpr);
+        vdpf[0][k] = uu * (vr * dpr);
+      }
+      if (vv * nyl > 0.0) {
+        udpf[1][k] = vv * (ul * dpl);
+        vdpf[1][k] = vv * (vl * dpl);
+      } else {
+        udpf[1][k] = vv * (ur * dpr);
+        vdpf[1][k] = vv * (vr * dpr);
+      }
+    }
+    double s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+    for (int k = 0; k < L; k++) s1 = s1 + udpf[0][k];
+    for (int k = 0; k < L; k++) s2 = s2 + udpf[1][k];
+    for (int k = 0; k < L; k++) s3 = s3 + vdpf[0][k];
+    for (int k = 0; k < L; k++) s4 = s4 + vdpf[1][k];
+    double uu_def = facc[FA_QUU * FQ + fq] - s1, uv_def = facc[FA_QUV * FQ + fq] - s2;
+    double vu_def = facc[FA_QVU * FQ + fq] - s3, vv_def = facc[FA_QVV * FQ + fq] - s4;
+    double sl = 0, sr = 0;
+    for (int k = 0; k < L; k++) sl = sl + (fabs(udpl[k]) + eps1);
+    for (int k = 0; k < L; k++) sr = sr + (fabs(udpr[k]) + eps1);
+    double oosl = 1.0 / sl, oosr = 1.0 / sr;
+    for (int k = 0; k < L; k++) {
+      udpf[0][k] = udpf[0][k] + ((uu_def * nxl > 0.0) ? fabs(udpl[k]) * oosl : fabs(udpr[k]) * oosr) * uu_def;
+      udpf[1][k] = udpf[1][k] + ((uv_def * nyl > 0.0) ? fabs(udpl[k]) * oosl : fabs(udpr[k]) * oosr) * uv_def;
+    }
+    sl = 0;
+    sr = 0;
+    for (int k = 0; k < L; k++) sl = sl + (fabs(vdpl[k]) + eps1);
+    for (int k = 0; k < L; k++) sr = sr + (fabs(vdpr[k]) + eps1);
+    oosl = 1.0 / sl;
+    oosr = 1.0 / sr;
+    for (int k = 0; k < L; k++) {
+      vdpf[0][k] = vdpf[0][k] + ((vu_def * nxl > 0.0) ? fabs(vdpl[k]) * oosl : fabs(vdpr[k]) * oosr) * vu_def;
+      vdpf[1][k] = vdpf[1][k] + ((vv_def * nyl > 0.0) ? fabs(vdpl[k]) * oosl : fabs(vdpr[k]) * oosr) * vv_def;
+    }
+    // H_r at the face (layer-overlap pressure, :627-707)
+    double pf[2][MAXL + 1], zf[2][MAXL + 1], pep[MAXL + 1], pem[MAXL + 1], zep[MAXL + 1], zem[MAXL + 1];
+    for (int k = 0; k <= L; k++) zf[0][k] = zf[1][k] = pf[0][k] = pf[1][k] = zep[k] = zem[k] = pep[k] = pem[k] = 0.0;
+    double ope_l = sqrt(facc[FA_OPE2L * FQ + fq]), ope_r = sqrt(facc[FA_OPE2R * FQ + fq]);
+    for (int k = 1; k <= L; k++) {
+      pf[0][k] = pf[0][k - 1] + ope_l * ql[k - 1][0];
+      pf[1][k] = pf[1][k - 1] + ope_r * qr[k - 1][0];
+    }
+    double ope_e = sqrt(facc[FA_OPEE2 * FQ + fq]);
+    double zbl = m.fstat[FS_ZBL * FQ + fq], zbr = m.fstat[FS_ZBR * FQ + fq];
+    zf[0][L] = zbl;
+    zf[1][L] = zbr;
+    zep[L] = zbl;
+    zem[L] = zbr;
+    for (int k = L; k >= 1; k--) {
+      double aog = alpha[k - 1] / g;
+      zf[0][k - 1] = zf[0][k] + aog * (ope_l * ql[k - 1][0]);
+      zf[1][k - 1] = zf[1][k] + aog * (ope_r * qr[k - 1][0]);
+      zep[k - 1] = zep[k] + aog * (ope_e * ql[k - 1][0]);
+      zem[k - 1] = zem[k] + aog * (ope_e * qr[k - 1][0]);
+    }
+    pep[1] = ope_e * ql[0][0];
+    pem[1] = ope_e * qr[0][0];
+    for (int k = 2; k <= L; k++) {
+      pep[k] = pep[k - 1] + ope_e * ql[k - 1][0];
+      pem[k] = pem[k - 1] + ope_e * qr[k - 1][0];
+    }
+    for (int k = 1; k <= L; k++) {
+      double Hrp = 0.5 * alpha[k - 1] * (pep[k] * pep[k] - pep[k - 1] * pep[k - 1]);
+      double Hrm = 0.0;
+      for (int kt = 1; kt <= L; kt++) {
+        double goa = g / alpha[kt - 1];
+        double zt = dmin(zem[kt - 1], zep[k - 1]), zb = dmax(zem[kt], zep[k]);
+        if (zt - zb > 0.0) {
+          double pbot = pem[kt] - goa * (zb - zem[kt]);
+          double ptop = pem[kt] - goa * (zt - zem[kt]);
+          Hrm = Hrm + 0.5 * alpha[kt - 1] * (pbot * pbot - ptop * ptop);
+        }
+      }
+      Hf[0][k - 1] = 0.5 * (Hrp + Hrm);
+      Hrm = 0.5 * alpha[k - 1] * (pem[k] * pem[k] - pem[k - 1] * pem[k - 1]);
+      Hrp = 0.0;
+      for (int kt = 1; kt <= L; kt++) {
+        double goa = g / alpha[kt - 1];
+        double zt = dmin(zep[kt - 1], zem[k - 1]), zb = dmax(zep[kt], zem[k]);
+        if (zt - zb > 0.0) {
+          double pbot = pep[kt] - goa * (zb - zep[kt]);
+          double ptop = pep[kt] - goa * (zt - zep[kt]);
+          Hrp = Hrp + 0.5 * alpha[kt - 1] * (pbot * pbot - ptop * ptop);
+        }
+      }
+      Hf[1][k - 1] = 0.5 * (Hrp + Hrm);
+    }
+    if (er == -4) {
+      for (int k = 1; k <= L; k++) {
+        Hf[0][k - 1] = 0.5 * alpha[k - 1] * (pf[0][k] * pf[0][k] - pf[0][k - 1] * pf[0][k - 1]);
+        Hf[1][k - 1] = 0.5 * alpha[k - 1] * (pf[1][k] * pf[1][k] - pf[1][k - 1] * pf[1][k - 1]);
+      }
+    } else {
+      for (int k = 1; k <= L - 1; k++) {
+        double goa = g / alpha[k - 1];
+        double pinc1 = goa * (zf[0][k] - zep[k]);
+        double Hc1 = 0.5 * alpha[k - 1] * ((pf[0][k] + pinc1) * (pf[0][k] + pinc1) - pf[0][k] * pf[0][k]);
+        Hf[0][k - 1] = Hf[0][k - 1] - Hc1;
+        Hf[0][k] = Hf[0][k] + Hc1;
+        double pinc2 = goa * (zf[1][k] - zem[k]);
+        double Hc2 = 0.5 * alpha[k - 1] * ((pf[1][k] + pinc2) * (pf[1][k] + pinc2) - pf[1][k] * pf[1][k]);
+        Hf[1][k - 1] = Hf[1][k - 1] - Hc2;
+        Hf[1][k] = Hf[1][k] + Hc2;
+      }
+    }
+    double hfa = facc[FA_H * FQ + fq];
+    for (int sd = 0; sd < 2; sd++) {
+      double weight = 1.0, acc = 0.0;
+      for (int k = 0; k < L; k++) acc = acc + Hf[sd][k];
+      if (acc > 0.0) weight = hfa / acc;
+      for (int k = 0; k < L; k++) Hf[sd][k] = Hf[sd][k] * weight;
+    }
+    for (int k = 0; k < L; k++) {
+      double flux_x = nxl * udpf[0][k] + nyl * udpf[1][k];
+      double flux_y = nxl * vdpf[0][k] + nyl * vdpf[1][k];
+      s_cl[k][0][iq] = -wq * (nxl * Hf[0][k] + flux_x);
+      s_cl[k][1][iq] = -wq * (nyl * Hf[0][k] + flux_y);
+      s_cr[k][0][iq] = wq * (nxl * Hf[1][k] + flux_x);
+      s_cr[k][1][iq] = wq * (nyl * Hf[1][k] + flux_y);
+    }
+  } else if (tid >= 32 && tid < 32 + NGL) {
+    // layer LDG flux at face node n for every layer
+    const int n = tid - 32;
+    const size_t fn = (size_t)f * NGL + n;
+    double nx = m.fnstat[FN_NX * FN + fn], ny = m.fnstat[FN_NY * FN + fn], wq = m.fnstat[FN_W * FN + fn];
+    const double beta = 0.5, alpha = 1.0 - beta;
+    for (int k = 0; k < L; k++) {
+      double fl[4], fr[4];
+      for (int iv = 0; iv < 4; iv++) {
+        fl[iv] = gdpp_face[((size_t)k * 10 + 4) * FN + fn] * gfacc[(size_t)iv * FN + fn] +
+                 gdpp_face[((size_t)k * 10 + iv) * FN + fn];
+        fr[iv] = gdpp_face[((size_t)k * 10 + 9) * FN + fn] * gfacc[(size_t)(4 + iv) * FN + fn] +
+                 gdpp_face[((size_t)k * 10 + 5 + iv) * FN + fn];
+      }
+      double qum0 = alpha * fl[0] + beta * fr[0], qum1 = alpha * fl[1] + beta * fr[1];
+      double qvm0 = alpha * fl[2] + beta * fr[2], qvm1 = alpha * fl[3] + beta * fr[3];
+      double flux_qu = (qum0 - fl[0] * nx) + (qum1 - fl[1] * ny);
+      double flux_qv = (qvm0 - fl[2] * nx) + (qvm1 - fl[3] * ny);
+      lap[(((size_t)k * 2 + 0) * F + f) * NGL + n] = wq * flux_qu;
+      lap[(((size_t)k * 2 + 1) * F + f) * NGL + n] = wq * flux_qv;
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * L * NGL) {
+    const int k = tid / (2 * NGL), c = (tid / NGL) % 2, n = tid % NGL;
+    double sl = 0.0, sr = 0.0;
+    for (int iq = 0; iq < NQ; iq++) {
+      double hi = s_psiq[n * NQ + iq];
+      sl += hi * s_cl[k][c][iq];
+      sr += hi * s_cr[k][c][iq];
+    }
+    momL[(((size_t)k * 2 + c) * F + f) * NGL + n] = sl;
+    momR[(((size_t)k * 2 + c) * F + f) * NGL + n] = sr;
+  }
+}
+
+// ===================================== layer momentum: element volume + update
+// create_rhs_dynamics_volume_layers + bcl LDG volume + face gathers; then
+// momentum update with implicit Coriolis, layer_mom_boundary_df and evaluate_bcl(_v1).
+// mode: 0 = momentum_mass (evaluate_bcl: also qprime(1) = q(1)/(sum q(1)/pb')),
+//       1 = momentum (evaluate_bcl_v1).
+template <int NGL, int NQ>
+__global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
+    mom_elem_kernel(DevMesh m, const double *qp_in, const double *qacc, const double *nacc, const double *dpp_graduv,
+                    const double *dpprime_visc, const double *momL, const double *momR, const double *lapf,
+                    const double *qb, double *q, double *qp_out, int mode) {
+  constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BS;
+  const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
+  const double g = m.gravity, eps1 = 1.0e-20;
+  __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL];
+  __shared__ double s_qp[MAXL][3][P], s_qm[MAXL][2][P], s_z[MAXL + 1][P];
+  __shared__ double s_T[MAXL * 5][NQ * NGL];
+  __shared__ double s_Tz[2][MAXL + 1][NQ * NGL];
+  __shared__ double s_G[MAXL][6][Q];
+  __shared__ double s_A[MAXL][4][NQ * NGL];
+  __shared__ double s_lg[MAXL][4][P];
+  __shared__ double s_new[MAXL][3][P];
+  __shared__ int s_map[4 * NGL], s_face[4], s_side[4], s_bc[4];
+  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, tid, BS);
+  if (tid < 4) {
+    s_face[tid] = m.efaces[e * 4 + tid];
+    s_side[tid] = m.eside[e * 4 + tid];
+    s_bc[tid] = m.ebc[e * 4 + tid];
+  }
+  for (int t = tid; t < 4 * NGL; t += BS) s_map[t] = m.efmap[e * 4 * NGL + t];
+  for (int t = tid; t < L * 3 * P; t += BS) {
+    int k = t / (3 * P), r = t % (3 * P);
+    s_qp[k][r % 3][r / 3] = qp_in[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
+    if (r % 3) s_qm[k][r % 3 - 1][r / 3] = q[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
+  }
+  __syncthreads();
+  // layer interfaces at nodes (mod_create_rhs_mlswe.F90:320-325)
+  for (int p = tid; p < P; p += BS) {
+    const size_t I = (size_t)e * P + p;
+    double z = m.nstat[NS_ZB * (size_t)npoin + I];
+    double so = sqrt(nacc[NA_OPE2 * (size_t)npoin + I]);
+    s_z[L][p] = z;
+    for (int k = L - 1; k >= 0; k--) {
+      z = z + (m.alpha[k] / g) * (so * s_qp[k][0][p]);
+      s_z[k][p] = z;
+    }
+  }
+  __syncthreads();
+  for (int t = tid; t < NQ * NGL; t += BS) {
+    int iq = t / NGL, mm = t % NGL;
+    for (int k = 0; k < L; k++) {
+      for (int v = 0; v < 3; v++) {
+        double acc = 0.0;
+        for (int n = 0; n < NGL; n++) acc += s_psiq[n * NQ + iq] * s_qp[k][v][mm * NGL + n];
+        s_T[k * 5 + v][t] = acc;
+      }
+      for (int v = 0; v < 2; v++) {
+        double acc = 0.0;
+        for (int n = 0; n < NGL; n++) acc += s_psiq[n * NQ + iq] * s_qm[k][v][mm * NGL + n];
+        s_T[k * 5 + 3 + v][t] = acc;
+      }
+    }
+    for (int k = 0; k <= L; k++) {
+      double ap = 0.0, ad = 0.0;
+      for (int n = 0; n < NGL; n++) {
+        ap += s_psiq[n * NQ + iq] * s_z[k][mm * NGL + n];
+        ad += s_dpsiq[n * NQ + iq] * s_z[k][mm * NGL + n];
+      }
+      s_Tz[0][k][t] = ap;
+      s_Tz[1][k][t] = ad;
+    }
+  }
+  // bcl LDG volume fluxes at nodes (bcl_compute_laplacian, mod_laplacian_quad.F90:392-425)
+  for (int p = tid; p < P; p += BS) {
+    const size_t I = (size_t)e * P + p;
+    double w_ = m.nstat[NS_W * (size_t)npoin + I];
+    double ex = m.nstat[NS_EX * (size_t)npoin + I], ey = m.nstat[NS_EY * (size_t)npoin + I];
+    double nx = m.nstat[NS_NX * (size_t)npoin + I], ny = m.nstat[NS_NY * (size_t)npoin + I];
+    for (int k = 0; k < L; k++) {
+      double d = dpprime_visc[(size_t)k * npoin + I];
+      double qq[4];
+      for (int c = 0; c < 4; c++)
+        qq[c] = d * nacc[(NA_G1 + c) * (size_t)npoin + I] + dpp_graduv[((size_t)k * 4 + c) * npoin + I];
+      s_lg[k][0][p] = w_ * (ex * qq[0] + ey * qq[1]);
+      s_lg[k][1][p] = w_ * (nx * qq[0] + ny * qq[1]);
+      s_lg[k][2][p] = w_ * (ex * qq[2] + ey * qq[3]);
+      s_lg[k][3][p] = w_ * (nx * qq[2] + ny * qq[3]);
+    }
+  }
+  __syncthreads();
+  const double Pstress = (g / m.alpha[0]) * 50.0;
+  const double Pbstress = (g / m.alpha[L - 1]) * 10.0;
+  for (int q = tid; q < Q; q += BS) {
+    const int iq = q % NQ, jq = q / NQ;
+    const size_t Iq = (size_t)e * Q + q;
+    double qpv[MAXL][3], tuu[MAXL], tvv[MAXL], p_tmp[MAXL + 1], H_tmp[MAXL], u_udp[MAXL], v_vdp[MAXL];
+    double u_vdp[2][MAXL], gz[2][MAXL + 1];
+    double qb0 = qacc[QA_OPE * (size_t)npq + Iq], qb1 = qacc[QA_UB * (size_t)npq + Iq],
+           qb2 = qacc[QA_VB * (size_t)npq + Iq];
+    double so2 = sqrt(qacc[QA_OPE2 * (size_t)npq + Iq]);
+    p_tmp[0] = 0.0;
+    for (int k = 0; k < L; k++) {
+      double vv[5];
+      for (int v = 0; v < 5; v++) {
+        double acc = 0.0;
+        for (int mm = 0; mm < NGL; mm++) acc += s_psiq[mm * NQ + jq] * s_T[k * 5 + v][iq * NGL + mm];
+        vv[v] = acc;
+      }
+      qpv[k][0] = vv[0];
+      qpv[k][1] = vv[1];
+      qpv[k][2] = vv[2];
+      p_tmp[k + 1] = p_tmp[k] + so2 * vv[0];
+      H_tmp[k] = 0.5 * m.alpha[k] * (p_tmp[k + 1] * p_tmp[k + 1] - p_tmp[k] * p_tmp[k]);
+      double dp = vv[0] * qb0, u = vv[1] + qb1, v = vv[2] + qb2;
+      u_udp[k] = dp * u * u;
+      v_vdp[k] = dp * v * v;
+      u_vdp[0][k] = u * v * dp;
+      u_vdp[1][k] = v * u * dp;
+      tuu[k] = fabs(vv[3]) + eps1;
+      tvv[k] = fabs(vv[4]) + eps1;
+    }
+    double ex = m.qstat[QS_EX * (size_t)npq + Iq], ey = m.qstat[QS_EY * (size_t)npq + Iq];
+    double nx = m.qstat[QS_NX * (size_t)npq + Iq], ny = m.qstat[QS_NY * (size_t)npq + Iq];
+    for (int k = 0; k <= L; k++) {
+      double dzx = 0.0, dzy = 0.0;  // d/dxi, d/deta at the quad point
+      for (int mm = 0; mm < NGL; mm++) {
+        dzx += s_psiq[mm * NQ + jq] * s_Tz[1][k][iq * NGL + mm];
+        dzy += s_dpsiq[mm * NQ + jq] * s_Tz[0][k][iq * NGL + mm];
+      }
+      gz[0][k] = ex * dzx + nx * dzy;
+      gz[1][k] = ey * dzx + ny * dzy;
+    }
+    double su = 0, suv = 0, sv = 0, stu = 0, stv = 0, sH = 0;
+    for (int k = 0; k < L; k++) su = su + u_udp[k];
+    for (int k = 0; k < L; k++) suv = suv + u_vdp[0][k];
+    for (int k = 0; k < L; k++) sv = sv + v_vdp[k];
+    double uu_def = qacc[QA_QU * (size_t)npq + Iq] - su;
+    double uv_def = qacc[QA_QUV * (size_t)npq + Iq] - suv;
+    double vv_def = qacc[QA_QV * (size_t)npq + Iq] - sv;
+    for (int k = 0; k < L; k++) stu = stu + tuu[k];
+    for (int k = 0; k < L; k++) stv = stv + tvv[k];
+    for (int k = 0; k < L; k++) sH = sH + H_tmp[k];
+    double oosu = 1.0 / stu, oosv = 1.0 / stv;
+    double wq = m.qstat[QS_W * (size_t)npq + Iq];
+    double weight = 1.0;
+    if (sH > 0.0) weight = qacc[QA_H * (size_t)npq + Iq] / sH;
+    double tw1 = m.qstat[QS_TW1 * (size_t)npq + Iq], tw2 = m.qstat[QS_TW2 * (size_t)npq + Iq];
+    double tb1 = qacc[QA_TBU * (size_t)npq + Iq], tb2 = qacc[QA_TBV * (size_t)npq + Iq];
+    double pb = m.qstat[QS_PB * (size_t)npq + Iq];
+    double ppt0 = 0.0;
+    for (int k = 0; k < L; k++) {
+      // QUIRK (mod_create_rhs_mlswe.F90:382): qp(k) = the LAST layer's (dp',u',v') indexed by k
+      double ppt1 = ppt0 + qpv[L - 1][k];
+      double wgt = tuu[k] * oosu;
+      u_udp[k] = u_udp[k] + wgt * uu_def;
+      u_vdp[0][k] = u_vdp[0][k] + wgt * uv_def;
+      wgt = tvv[k] * oosv;
+      u_vdp[1][k] = u_vdp[1][k] + wgt * uv_def;
+      v_vdp[k] = v_vdp[k] + wgt * vv_def;
+      double Hq = H_tmp[k] * weight;
+      double temp1 = (dmin(ppt1, Pstress) - dmin(ppt0, Pstress)) / Pstress;
+      double tempbot = (dmin(Pbstress, pb - ppt1) - dmin(Pbstress, pb - ppt0)) / Pbstress;
+      double sx = g * (temp1 * tw1 - tempbot * tb1 + p_tmp[k] * gz[0][k] - p_tmp[k + 1] * gz[0][k + 1]);
+      double sy = g * (temp1 * tw2 - tempbot * tb2 + p_tmp[k] * gz[1][k] - p_tmp[k + 1] * gz[1][k + 1]);
+      double f1x = Hq + u_udp[k], f1y = u_vdp[0][k], f2x = u_vdp[1][k], f2y = Hq + v_vdp[k];
+      s_G[k][0][q] = wq * (ex * f1x + ey * f1y);
+      s_G[k][1][q] = wq * (nx * f1x + ny * f1y);
+      s_G[k][2][q] = wq * sx;
+      s_G[k][3][q] = wq * (ex * f2x + ey * f2y);
+      s_G[k][4][q] = wq * (nx * f2x + ny * f2y);
+      s_G[k][5][q] = wq * sy;
+      ppt0 = ppt1;
+    }
+  }
+  __syncthreads();
+  for (int t = tid; t < NQ * NGL; t += BS) {
+    int iq = t / NGL, mm = t % NGL;
+    for (int k = 0; k < L; k++) {
+      double ax1 = 0, ap1 = 0, ax2 = 0, ap2 = 0;
+      for (int jq = 0; jq < NQ; jq++) {
+        double ps = s_psiq[mm * NQ + jq], dps = s_dpsiq[mm * NQ + jq];
+        int qq = jq * NQ + iq;
+        ax1 += ps * s_G[k][0][qq];
+        ap1 += dps * s_G[k][1][qq] + ps * s_G[k][2][qq];
+        ax2 += ps * s_G[k][3][qq];
+        ap2 += dps * s_G[k][4][qq] + ps * s_G[k][5][qq];
+      }
+      s_A[k][0][t] = ax1;
+      s_A[k][1][t] = ap1;
+      s_A[k][2][t] = ax2;
+      s_A[k][3][t] = ap2;
+    }
+  }
+  __syncthreads();
+  // per node: rhs_mom, update, Coriolis
+  for (int p = tid; p < P; p += BS) {
+    const int i = p % NGL, j = p / NGL;
+    const size_t I = (size_t)e * P + p;
+    const double mi = m.nstat[NS_MINV * (size_t)npoin + I];
+    const double f2 = m.nstat[NS_F2 * (size_t)npoin + I], ab = m.nstat[NS_A * (size_t)npoin + I],
+                 bb = m.nstat[NS_B * (size_t)npoin + I];
+    for (int k = 0; k < L; k++) {
+      double r0 = 0.0, r1 = 0.0;
+      for (int iq = 0; iq < NQ; iq++) {
+        double dps = s_dpsiq[i * NQ + iq], ps = s_psiq[i * NQ + iq];
+        r0 += dps * s_A[k][0][iq * NGL + j] + ps * s_A[k][1][iq * NGL + j];
+        r1 += dps * s_A[k][2][iq * NGL + j] + ps * s_A[k][3][iq * NGL + j];
+      }
+      double l0 = 0.0, l1 = 0.0;
+      for (int kk = 0; kk < NGL; kk++) {
+        l0 -= s_dpsi[i * NGL + kk] * s_lg[k][0][j * NGL + kk] + s_dpsi[j * NGL + kk] * s_lg[k][1][kk * NGL + i];
+        l1 -= s_dpsi[i * NGL + kk] * s_lg[k][2][j * NGL + kk] + s_dpsi[j * NGL + kk] * s_lg[k][3][kk * NGL + i];
+      }
+      for (int lf = 0; lf < 4; lf++)
+        for (int n = 0; n < NGL; n++)
+          if (s_map[lf * NGL + n] == p) {
+            size_t b0 = (((size_t)k * 2 + 0) * F + s_face[lf]) * NGL + n;
+            size_t b1 = (((size_t)k * 2 + 1) * F + s_face[lf]) * NGL + n;
+            const double *src = s_side[lf] == 0 ? momL : momR;
+            r0 += src[b0];
+            r1 += src[b1];
+            double sg = s_side[lf] == 0 ? 1.0 : -1.0;
+            l0 += sg * lapf[b0];
+            l1 += sg * lapf[b1];
+          }
+      double rm0 = mi * r0 + m.visc * mi * l0;
+      double rm1 = mi * r1 + m.visc * mi * l1;
+      double q2 = s_qm[k][0][p], q3 = s_qm[k][1][p];
+      double t1 = q2 + m.dt * rm0, t2 = q3 + m.dt * rm1;
+      double tu = t1 + f2 * q3, tv = t2 - f2 * q2;
+      s_new[k][1][p] = ab * tu + bb * tv;
+      s_new[k][2][p] = -bb * tu + ab * tv;
+      s_new[k][0][p] = q[((size_t)k * npoin + I) * 3];
+    }
+  }
+  __syncthreads();
+  // layer_mom_boundary_df on the element's wall faces, face-id order
+  for (int lf = 0; lf < 4; lf++) {
+    const int er = s_bc[lf];
+    if (er != -4 && er != -2) continue;
+    for (int n = tid; n < NGL; n += BS) {
+      const int p = s_map[lf * NGL + n];
+      const size_t fn = (size_t)s_face[lf] * NGL + n, FN = (size_t)F * NGL;
+      double nx = m.fnstat[FN_NX * FN + fn], ny = m.fnstat[FN_NY * FN + fn];
+      for (int k = 0; k < L; k++) {
+        if (er == -4) {
+          double u = s_new[k][1][p], v = s_new[k][2][p];
+          double up = u * nx + v * ny;
+          s_new[k][1][p] = u - up * nx;
+          s_new[k][2][p] = v - up * ny;
+        } else {
+          s_new[k][1][p] = 0.0;
+          s_new[k][2][p] = 0.0;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // evaluate_bcl / evaluate_bcl_v1 with extract_velocity, per node
+  for (int p = tid; p < P; p += BS) {
+    const size_t I = (size_t)e * P + p;
+    const double b1 = qb[I * 4], b3 = qb[I * 4 + 2], b4 = qb[I * 4 + 3];
+    double uv[MAXL][2], h[MAXL];
+    for (int pass = 0; pass < 2; pass++) {
+      for (int k = 0; k < L; k++) {
+        h[k] = s_new[k][0][p];
+        uv[k][0] = s_new[k][1][p] / h[k];
+        uv[k][1] = s_new[k][2][p] / h[k];
+      }
+      double ub = 0.0, vb = 0.0;
+      for (int k = 0; k < L; k++) {
+        ub = ub + uv[k][0] * h[k];
+        vb = vb + uv[k][1] * h[k];
+      }
+      if (b1 > 0.0) {
+        ub = ub / b1;
+        vb = vb / b1;
+        for (int k = 0; k < L; k++) {
+          uv[k][0] = uv[k][0] - ub + b3 / b1;
+          uv[k][1] = uv[k][1] - vb + b4 / b1;
+        }
+      } else {
+        for (int k = 0; k < L; k++) uv[k][0] = uv[k][1] = 0.0;
+      }
+      if (pass == 0)
+        for (int k = 0; k < L; k++) {
+          s_new[k][1][p] = uv[k][0] * h[k];
+          s_new[k][2][p] = uv[k][1] * h[k];
+        }
+    }
+    double ope = 0.0;
+    if (mode == 0) {
+      for (int k = 0; k < L; k++) ope = ope + h[k];
+      ope = ope / m.nstat[NS_PB * (size_t)npoin + I];
+    }
+    for (int k = 0; k < L; k++) {
+      double *qq = q + ((size_t)k * npoin + I) * 3;
+      qq[1] = s_new[k][1][p];
+      qq[2] = s_new[k][2][p];
+      double *o = qp_out + ((size_t)k * npoin + I) * 3;
+      if (mode == 0) o[0] = h[k] / ope;
+      o[1] = uv[k][0] - b3 / b1;
+      o[2] = uv[k][1] - b4 / b1;
+    }
+  }
+}
+
+#define HNUMO_INSTANTIATE_BCL(NGL, NQ)                                                                              \
+  template __global__ void extract_face_kernel<NGL>(DevMesh, const double *, double *, int);                      \
+  template __global__ void bcl_coeffs_elem_kernel<NGL, NQ>(DevMesh, const double *, double *, double *, double *,    \
+                                                           double *);                                              \
+  template __global__ void bcl_coeffs_face_kernel<NGL, NQ>(DevMesh, const double *, const double *, const double *,  \
+                                                           double *, double *, double *);
+
+}  // namespace hnumo

@@ -1,0 +1,549 @@
+// kernels_btp.hip -- barotropic SSP-RK stage as one fused CDNA4 kernel per stage.
+//
+// One workgroup owns one element (BS = Q rounded up to whole wave64s).  A stage
+// (ti_barotropic_ssprk_mlswe body, mod_rk_mlswe.F90:87-114) is:
+//   create_rhs_btp (mod_rhs_btp.F90:28-59)
+//     = volume term  create_rhs_btp_volume_qdf (:102-209)
+//     + face fluxes  creat_btp_fluxes_qdf       (:211-370), traces btp_extract_df
+//                                               (mod_barotropic_terms.F90:25-97)
+//     + LDG viscosity btp_create_laplacian (mod_laplacian_quad.F90:32-121)
+//   then the Shu-Osher update and the wall fix btp_mom_boundary_df (:165-217).
+//
+// Differences from the reference's data flow (same arithmetic per term):
+//   * the dense psih/dpsidx tables are replaced by sum factorisation with the 1-D LGL
+//     basis staged in LDS (interpolate along x then y; weak-form transpose the same way);
+//   * each element computes the numerical flux of its own four faces (gather, no
+//     atomics, deterministic); face time averages are accumulated by the face's left
+//     element only;
+//   * the nodal velocity gradient (compute_gradient_uv) of the NEW state is computed at
+//     the end of the stage that produced it and its face traces are written to gtrace,
+//     so the next stage reads its neighbours' traces (4*NGL doubles per face) instead of
+//     a second kernel.
+#include "engine_internal.h"
+
+namespace hnumo {
+
+struct StageArgs {
+  DevMesh m;
+  const double *qb_in, *qb0, *qb2, *qprime;  // qb(4,npoin); qprime(3,npoin,L)
+  const double *qcoef;                       // [QC_N][npoin_q]
+  const double *ncoef;                       // [NC_N][npoin]
+  const double *fcoef;                       // [FC_N][F*NQ]
+  const double *fncoef;                      // [10][F*NGL]  btp_graduv_dpp_face(v,s) at v+5*s
+  const double *gtrace_in;                   // [E][4][4][NGL]
+  const double *halo_qb, *halo_g;            // processor-face traces (unused single-rank)
+  double *gtrace_out;
+  double *qacc, *facc, *nacc, *gfacc;        // accumulators (see engine_internal.h)
+  double *qb_out;                            // stage result, qb(4,npoin)
+  double *rhs_out;                           // rhs(3,npoin) in rhs-only mode
+  double a1, a2, a3, dtt;
+  int rhs_only, write_grad, accumulate;
+};
+
+template <int NGL, int NQ>
+struct Sizes {
+  static constexpr int P = NGL * NGL;
+  static constexpr int Q = NQ * NQ;
+  static constexpr int BS = ((Q + 63) / 64) * 64;
+};
+
+// nodal gradient of (u, v) on one element (compute_gradient_uv, mod_barotropic_terms.F90:411-443)
+// g[0..3] = (du/dx, du/dy, dv/dx, dv/dy) at node p = j*NGL + i
+template <int NGL>
+__device__ __forceinline__ void nodal_grad(const double *s_dpsi, const double *u, const double *v, int i, int j,
+                                           double ex, double ey, double nx, double ny, double g[4]) {
+  double ux = 0.0, uy = 0.0, vx = 0.0, vy = 0.0;
+#pragma unroll
+  for (int n = 0; n < NGL; n++) {
+    double dx = s_dpsi[n * NGL + i], dy = s_dpsi[n * NGL + j];
+    ux += dx * u[j * NGL + n];
+    vx += dx * v[j * NGL + n];
+    uy += dy * u[n * NGL + i];
+    vy += dy * v[n * NGL + i];
+  }
+  g[0] = ex * ux + nx * uy;
+  g[1] = ey * ux + ny * uy;
+  g[2] = ex * vx + nx * vy;
+  g[3] = ey * vx + ny * vy;
+}
+
+template <int NGL, int NQ>
+__global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64) btp_stage_kernel(StageArgs a) {
+  constexpr int P = Sizes<NGL, NQ>::P, Q = Sizes<NGL, NQ>::Q, BS = Sizes<NGL, NQ>::BS;
+  const DevMesh &m = a.m;
+  const int e = blockIdx.x, tid = threadIdx.x;
+  const int npoin = m.npoin, npq = m.npoin_q, F = m.nface;
+
+  __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL];
+  __shared__ double s_qb[4][P], s_qp[3][P], s_uv[2][P];
+  __shared__ double s_T[7][NQ * NGL];       // x-interpolated: [v][iq*NGL + m]
+  __shared__ double s_G[8][Q];              // weighted contravariant fluxes at quad points
+  __shared__ double s_A[6][NQ * NGL];       // jq-contracted: [iq*NGL + m]
+  __shared__ double s_grad[4][P], s_lg[4][P];
+  __shared__ double s_nb[4][4][NGL], s_ng[4][4][NGL];  // neighbour qb / grad traces per local face
+  __shared__ double s_fq[4][NQ][3], s_fl[4][NGL][2];
+  __shared__ double s_qn[4][P];
+  __shared__ int s_map[4][NGL], s_face[4], s_side[4], s_bc[4], s_nbe[4], s_nblf[4];
+
+  // ---------------------------------------------------------------- phase 0: loads
+  for (int t = tid; t < NGL * NQ; t += BS) {
+    s_psiq[t] = m.basis[t];
+    s_dpsiq[t] = m.basis[NGL * NQ + t];
+  }
+  for (int t = tid; t < NGL * NGL; t += BS) s_dpsi[t] = m.basis[2 * NGL * NQ + t];
+  if (tid < 4) {
+    s_face[tid] = m.efaces[e * 4 + tid];
+    s_side[tid] = m.eside[e * 4 + tid];
+    s_bc[tid] = m.ebc[e * 4 + tid];
+    s_nbe[tid] = m.enbr_e[e * 4 + tid];
+    s_nblf[tid] = m.enbr_lf[e * 4 + tid];
+  }
+  for (int t = tid; t < 4 * NGL; t += BS) s_map[t / NGL][t % NGL] = m.efmap[e * 4 * NGL + t];
+  for (int t = tid; t < 4 * P; t += BS) s_qb[t % 4][t / 4] = a.qb_in[(size_t)e * 4 * P + t];
+  if (m.botfr) {
+    const double *qpL = a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P;
+    for (int t = tid; t < 3 * P; t += BS) s_qp[t % 3][t / 3] = qpL[t];
+  }
+  __syncthreads();
+  // neighbour traces (interior faces)
+  for (int t = tid; t < 4 * 4 * NGL; t += BS) {
+    int lf = t / (4 * NGL), r = t % (4 * NGL), c = r / NGL, n = r % NGL;
+    double vq = 0.0, vg = 0.0;
+    if (s_bc[lf] > 0) {
+      int In = m.enbr_node[(e * 4 + lf) * NGL + n];
+      vq = a.qb_in[(size_t)In * 4 + c];
+      vg = a.gtrace_in[(((size_t)s_nbe[lf] * 4 + s_nblf[lf]) * 4 + c) * NGL + n];
+    }
+    s_nb[lf][c][n] = vq;
+    s_ng[lf][c][n] = vg;
+  }
+  // ---------------------------------------------------------------- phase 1
+  // nodal stage-start terms (mod_rk_mlswe.F90:90-92) and x-interpolation
+  for (int p = tid; p < P; p += BS) {
+    double q1 = s_qb[0][p], q2 = s_qb[1][p], q3 = s_qb[2][p], q4 = s_qb[3][p];
+    s_uv[0][p] = q3 / q1;
+    s_uv[1][p] = q4 / q1;
+    if (a.accumulate) {
+      size_t I = (size_t)e * P + p;
+      double t1 = 1.0 + q2 * m.nstat[NS_OOP * (size_t)npoin + I];
+      a.nacc[NA_OPE2 * (size_t)npoin + I] += t1 * t1;
+      a.nacc[NA_UB * (size_t)npoin + I] += q3 / q1;
+      a.nacc[NA_VB * (size_t)npoin + I] += q4 / q1;
+    }
+  }
+  {
+    const int nv = m.botfr ? 7 : 4;
+    for (int t = tid; t < NQ * NGL; t += BS) {
+      int iq = t / NGL, mm = t % NGL;
+      for (int v = 0; v < nv; v++) {
+        const double *src = v < 4 ? s_qb[v] : s_qp[v - 4];
+        double acc = 0.0;
+#pragma unroll
+        for (int n = 0; n < NGL; n++) acc += s_psiq[n * NQ + iq] * src[mm * NGL + n];
+        s_T[v][t] = acc;
+      }
+    }
+  }
+  __syncthreads();
+  // ---------------------------------------------------------------- phase 2
+  // quad-point physics (mod_rhs_btp.F90:136-192) on threads [0,Q);
+  // nodal gradient of u_bar (mod_laplacian_quad.F90:48-54) on the following threads
+  for (int q = tid; q < Q; q += BS) {
+    const int iq = q % NQ, jq = q / NQ;
+    double val[7];
+    const int nv = m.botfr ? 7 : 4;
+    for (int v = 0; v < nv; v++) {
+      double acc = 0.0;
+#pragma unroll
+      for (int mm = 0; mm < NGL; mm++) acc += s_psiq[mm * NQ + jq] * s_T[v][iq * NGL + mm];
+      val[v] = acc;
+    }
+    const size_t Iq = (size_t)e * Q + q;
+    const double *QS = m.qstat;
+    double dp = val[0], dpp = val[1], udp = val[2], vdp = val[3];
+    double wq = QS[QS_W * (size_t)npq + Iq];
+    double ub = udp / dp, vb = vdp / dp;
+    double tb_u = 0.0, tb_v = 0.0;
+    if (m.botfr == 1) {
+      double ubot = val[5] + ub, vbot = val[6] + vb;
+      double spd = (m.cd / m.gravity) * val[4];
+      tb_u = spd * ubot;
+      tb_v = spd * vbot;
+    } else if (m.botfr == 2) {
+      double ubot = val[5] + ub, vbot = val[6] + vb;
+      double spd = (m.cd / m.alpha[m.L - 1]) * sqrt(ubot * ubot + vbot * vbot);
+      tb_u = spd * ubot;
+      tb_v = spd * vbot;
+    }
+    const double g = m.gravity;
+    double cor = QS[QS_COR * (size_t)npq + Iq];
+    double sc_x = cor * vdp + g * (QS[QS_TW1 * (size_t)npq + Iq] - tb_u) - g * dp * QS[QS_GZ1 * (size_t)npq + Iq];
+    double sc_y = -cor * udp + g * (QS[QS_TW2 * (size_t)npq + Iq] - tb_v) - g * dp * QS[QS_GZ2 * (size_t)npq + Iq];
+    double ope = 1.0 + dpp * QS[QS_OOP * (size_t)npq + Iq];
+    double Hq = (ope * ope) * a.qcoef[QC_HBCL * (size_t)npq + Iq];
+    double qu = ub * udp + ope * a.qcoef[QC_QUU * (size_t)npq + Iq];
+    double quv = ub * vdp + ope * a.qcoef[QC_QUV * (size_t)npq + Iq];
+    double qv = vb * vdp + ope * a.qcoef[QC_QVV * (size_t)npq + Iq];
+    if (a.accumulate) {
+      double *A = a.qacc;
+      A[QA_H * (size_t)npq + Iq] += Hq;
+      A[QA_QU * (size_t)npq + Iq] += qu;
+      A[QA_QV * (size_t)npq + Iq] += qv;
+      A[QA_QUV * (size_t)npq + Iq] += quv;
+      A[QA_TBU * (size_t)npq + Iq] += tb_u;
+      A[QA_TBV * (size_t)npq + Iq] += tb_v;
+      A[QA_OPE * (size_t)npq + Iq] += ope;
+      A[QA_OPE2 * (size_t)npq + Iq] += ope * ope;
+      A[QA_MFX * (size_t)npq + Iq] += udp;
+      A[QA_MFY * (size_t)npq + Iq] += vdp;
+      A[QA_UB * (size_t)npq + Iq] += ub;
+      A[QA_VB * (size_t)npq + Iq] += vb;
+    }
+    double ex = QS[QS_EX * (size_t)npq + Iq], ey = QS[QS_EY * (size_t)npq + Iq];
+    double nx = QS[QS_NX * (size_t)npq + Iq], ny = QS[QS_NY * (size_t)npq + Iq];
+    double f2x = Hq + qu, f2y = quv, f3x = quv, f3y = Hq + qv;
+    s_G[0][q] = wq * (ex * udp + ey * vdp);
+    s_G[1][q] = wq * (nx * udp + ny * vdp);
+    s_G[2][q] = wq * (ex * f2x + ey * f2y);
+    s_G[3][q] = wq * (nx * f2x + ny * f2y);
+    s_G[4][q] = wq * sc_x;
+    s_G[5][q] = wq * (ex * f3x + ey * f3y);
+    s_G[6][q] = wq * (nx * f3x + ny * f3y);
+    s_G[7][q] = wq * sc_y;
+  }
+  for (int p = (tid + BS - Q % BS) % BS; p < P; p += BS) {
+    const int i = p % NGL, j = p / NGL;
+    const size_t I = (size_t)e * P + p;
+    const double *NS = m.nstat;
+    double g4[4];
+    nodal_grad<NGL>(s_dpsi, s_uv[0], s_uv[1], i, j, NS[NS_EX * (size_t)npoin + I], NS[NS_EY * (size_t)npoin + I],
+                    NS[NS_NX * (size_t)npoin + I], NS[NS_NY * (size_t)npoin + I], g4);
+    for (int c = 0; c < 4; c++) {
+      s_grad[c][p] = g4[c];
+      if (a.accumulate) a.nacc[(NA_G1 + c) * (size_t)npoin + I] += g4[c];
+    }
+  }
+  __syncthreads();
+  // ---------------------------------------------------------------- phase 3
+  // (a) jq-contraction of the weighted fluxes, (b) btp face fluxes at face quad points,
+  // (c) LDG fluxes at face nodes, (d) LDG volume fluxes at nodes
+  {
+    constexpr int W1 = NQ * NGL, W2 = 4 * NQ, W3 = 4 * NGL, W4 = P;
+    for (int w = tid; w < W1 + W2 + W3 + W4; w += BS) {
+      if (w < W1) {
+        const int iq = w / NGL, mm = w % NGL;
+        double ax1 = 0, ap1 = 0, ax2 = 0, ap2 = 0, ax3 = 0, ap3 = 0;
+#pragma unroll
+        for (int jq = 0; jq < NQ; jq++) {
+          double ps = s_psiq[mm * NQ + jq], dps = s_dpsiq[mm * NQ + jq];
+          int q = jq * NQ + iq;
+          ax1 += ps * s_G[0][q];
+          ap1 += dps * s_G[1][q];
+          ax2 += ps * s_G[2][q];
+          ap2 += dps * s_G[3][q] + ps * s_G[4][q];
+          ax3 += ps * s_G[5][q];
+          ap3 += dps * s_G[6][q] + ps * s_G[7][q];
+        }
+        s_A[0][w] = ax1; s_A[1][w] = ap1; s_A[2][w] = ax2; s_A[3][w] = ap2; s_A[4][w] = ax3; s_A[5][w] = ap3;
+      } else if (w < W1 + W2) {
+        // ---- creat_btp_fluxes_qdf at (face lf, quad iq) (mod_rhs_btp.F90:246-362)
+        const int t = w - W1, lf = t / NQ, iq = t % NQ;
+        const int f = s_face[lf], side = s_side[lf], er = s_bc[lf];
+        double ql[4] = {0, 0, 0, 0}, qr[4] = {0, 0, 0, 0}, pbl = 0.0, pbr = 0.0;
+        for (int n = 0; n < NGL; n++) {
+          const double hi = s_psiq[n * NQ + iq];
+          const int p = s_map[lf][n];
+          double own[4] = {s_qb[0][p], s_qb[1][p], s_qb[2][p], s_qb[3][p]};
+          double oth[4];
+          if (er > 0) {
+            for (int c = 0; c < 4; c++) oth[c] = s_nb[lf][c][n];
+          } else {
+            // ghost state of btp_extract_df (mod_barotropic_terms.F90:75-91)
+            for (int c = 0; c < 4; c++) oth[c] = own[c];
+            if (er == -4) {
+              double nxn = m.fnstat[FN_NX * (size_t)F * NGL + (size_t)f * NGL + n];
+              double nyn = m.fnstat[FN_NY * (size_t)F * NGL + (size_t)f * NGL + n];
+              double un = nxn * own[2] + nyn * own[3];
+              oth[2] = own[2] - 2.0 * un * nxn;
+              oth[3] = own[3] - 2.0 * un * nyn;
+            } else if (er == -2) {
+              oth[2] = -own[2];
+              oth[3] = -own[3];
+            }
+          }
+          const double *L_ = side == 0 ? own : oth;
+          const double *R_ = side == 0 ? oth : own;
+          for (int c = 0; c < 4; c++) {
+            ql[c] = ql[c] + hi * L_[c];
+            qr[c] = qr[c] + hi * R_[c];
+          }
+          pbl = pbl + hi * m.fnstat[FN_PBL * (size_t)F * NGL + (size_t)f * NGL + n];
+          pbr = pbr + hi * m.fnstat[FN_PBR * (size_t)F * NGL + (size_t)f * NGL + n];
+        }
+        const size_t fq = (size_t)f * NQ + iq, FQ = (size_t)F * NQ;
+        const double *FS = m.fstat;
+        double nxl = FS[FS_NX * FQ + fq], nyl = FS[FS_NY * FQ + fq];
+        double nxr = -nxl, nyr = -nyl;
+        double pU_L = nxl * ql[2] + nyl * ql[3];
+        double pU_R = nxr * qr[2] + nyr * qr[3];
+        double pbpert_edge = FS[FS_CL * FQ + fq] * ql[1] + FS[FS_CR * FQ + fq] * qr[1] + FS[FS_CLR * FQ + fq] * (pU_L + pU_R);
+        double ope_e = 1.0 + pbpert_edge * FS[FS_OOPE * FQ + fq];
+        double cml = FS[FS_CML * FQ + fq], cmr = FS[FS_CMR * FQ + fq], cmlr = FS[FS_CMLR * FQ + fq];
+        double fex = cml * ql[2] + cmr * qr[2] + cmlr * (nxl * ql[1] + nxr * qr[1]);
+        double fey = cml * ql[3] + cmr * qr[3] + cmlr * (nyl * ql[1] + nyr * qr[1]);
+        double ul = ql[2] / ql[0], ur = qr[2] / qr[0], vl = ql[3] / ql[0], vr = qr[3] / qr[0];
+        const double *FC = a.fcoef;
+        double quu = 0.5 * (ul * ql[2] + ur * qr[2]) + ope_e * FC[FC_QUU * FQ + fq];
+        double quv = 0.5 * (vl * ql[2] + vr * qr[2]) + ope_e * FC[FC_QUV * FQ + fq];
+        double qvu = 0.5 * (ul * ql[3] + ur * qr[3]) + ope_e * FC[FC_QUV * FQ + fq];
+        double qvv = 0.5 * (vl * ql[3] + vr * qr[3]) + ope_e * FC[FC_QVV * FQ + fq];
+        double Hf = (ope_e * ope_e) * FC[FC_HBCL * FQ + fq];
+        if (a.accumulate && side == 0) {
+          double *A = a.facc;
+          A[FA_MFX * FQ + fq] += fex;
+          A[FA_MFY * FQ + fq] += fey;
+          A[FA_H * FQ + fq] += Hf;
+          A[FA_QUU * FQ + fq] += quu;
+          A[FA_QUV * FQ + fq] += quv;
+          A[FA_QVU * FQ + fq] += qvu;
+          A[FA_QVV * FQ + fq] += qvv;
+          double opl = 1.0 + (ql[1] / pbl), opr = 1.0 + (qr[1] / pbr);
+          A[FA_OPEL * FQ + fq] += opl;
+          A[FA_OPER * FQ + fq] += opr;
+          A[FA_OPE2L * FQ + fq] += opl * opl;
+          A[FA_OPE2R * FQ + fq] += opr * opr;
+          A[FA_OPEE2 * FQ + fq] += ope_e * ope_e;
+          A[FA_UL * FQ + fq] += ul;
+          A[FA_UR * FQ + fq] += ur;
+          A[FA_VL * FQ + fq] += vl;
+          A[FA_VR * FQ + fq] += vr;
+        }
+        double wq = FS[FS_W * FQ + fq];
+        double H_kx = nxl * Hf, H_ky = nyl * Hf;
+        double lamb = cmlr;
+        double dispu = 0.5 * lamb * (qr[2] - ql[2]);
+        double dispv = 0.5 * lamb * (qr[3] - ql[3]);
+        double flux_x = nxl * quu + nyl * quv - dispu;
+        double flux_y = nxl * qvu + nyl * qvv - dispv;
+        double flux = nxl * fex + nyl * fey;
+        double sg = side == 0 ? -wq : wq;
+        s_fq[lf][iq][0] = sg * flux;
+        s_fq[lf][iq][1] = sg * (H_kx + flux_x);
+        s_fq[lf][iq][2] = sg * (H_ky + flux_y);
+      } else if (w < W1 + W2 + W3) {
+        // ---- create_rhs_laplacian_flux at (face lf, node n) (mod_laplacian_quad.F90:452-517)
+        const int t = w - W1 - W2, lf = t / NGL, n = t % NGL;
+        const int f = s_face[lf], side = s_side[lf], er = s_bc[lf];
+        const int p = s_map[lf][n];
+        const size_t fn = (size_t)f * NGL + n, FN = (size_t)F * NGL;
+        double own[4] = {s_grad[0][p], s_grad[1][p], s_grad[2][p], s_grad[3][p]};
+        double oth[4];
+        double nxn = m.fnstat[FN_NX * FN + fn], nyn = m.fnstat[FN_NY * FN + fn];
+        if (er > 0) {
+          for (int c = 0; c < 4; c++) oth[c] = s_ng[lf][c][n];
+        } else {
+          for (int c = 0; c < 4; c++) oth[c] = own[c];
+          if (er == -4) {  // mod_laplacian_quad.F90:85-98
+            double un = own[0] * nxn + own[1] * nyn;
+            oth[0] = own[0] - 2.0 * un * nxn;
+            oth[1] = own[1] - 2.0 * un * nyn;
+            un = own[2] * nxn + own[3] * nyn;
+            oth[2] = own[2] - 2.0 * un * nxn;
+            oth[3] = own[3] - 2.0 * un * nyn;
+          }
+        }
+        const double *gl = side == 0 ? own : oth;
+        const double *gr = side == 0 ? oth : own;
+        if (a.accumulate && side == 0) {
+          for (int c = 0; c < 4; c++) {
+            a.gfacc[(size_t)c * FN + fn] += gl[c];
+            a.gfacc[(size_t)(4 + c) * FN + fn] += gr[c];
+          }
+        }
+        const double *B = a.fncoef;
+        double fl[4], fr[4];
+        for (int iv = 0; iv < 4; iv++) {
+          fl[iv] = B[4 * FN + fn] * gl[iv] + B[(size_t)iv * FN + fn];
+          fr[iv] = B[9 * FN + fn] * gr[iv] + B[(size_t)(5 + iv) * FN + fn];
+        }
+        const double beta = 0.5, alpha = 1.0 - beta;
+        double qum0 = alpha * fl[0] + beta * fr[0], qum1 = alpha * fl[1] + beta * fr[1];
+        double qvm0 = alpha * fl[2] + beta * fr[2], qvm1 = alpha * fl[3] + beta * fr[3];
+        double wq = m.fnstat[FN_W * FN + fn];
+        double flux_qu = (qum0 - fl[0] * nxn) + (qum1 - fl[1] * nyn);
+        double flux_qv = (qvm0 - fl[2] * nxn) + (qvm1 - fl[3] * nyn);
+        double sg = side == 0 ? wq : -wq;
+        s_fl[lf][n][0] = sg * flux_qu;
+        s_fl[lf][n][1] = sg * flux_qv;
+      } else {
+        // ---- btp_compute_laplacian volume fluxes at node p (mod_laplacian_quad.F90:372-388)
+        const int p = w - W1 - W2 - W3;
+        const size_t I = (size_t)e * P + p;
+        const double *NS = m.nstat, *NC = a.ncoef;
+        double pv = NC[NC_PV * (size_t)npoin + I];
+        double qq1 = pv * s_grad[0][p] + NC[NC_D1 * (size_t)npoin + I];
+        double qq2 = pv * s_grad[1][p] + NC[NC_D2 * (size_t)npoin + I];
+        double qq3 = pv * s_grad[2][p] + NC[NC_D3 * (size_t)npoin + I];
+        double qq4 = pv * s_grad[3][p] + NC[NC_D4 * (size_t)npoin + I];
+        double w_ = NS[NS_W * (size_t)npoin + I];
+        double ex = NS[NS_EX * (size_t)npoin + I], ey = NS[NS_EY * (size_t)npoin + I];
+        double nx = NS[NS_NX * (size_t)npoin + I], ny = NS[NS_NY * (size_t)npoin + I];
+        s_lg[0][p] = w_ * (ex * qq1 + ey * qq2);
+        s_lg[1][p] = w_ * (nx * qq1 + ny * qq2);
+        s_lg[2][p] = w_ * (ex * qq3 + ey * qq4);
+        s_lg[3][p] = w_ * (nx * qq3 + ny * qq4);
+      }
+    }
+  }
+  __syncthreads();
+  // ---------------------------------------------------------------- phase 4: per node
+  for (int p = tid; p < P; p += BS) {
+    const int i = p % NGL, j = p / NGL;
+    const size_t I = (size_t)e * P + p;
+    double r[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int iq = 0; iq < NQ; iq++) {
+      double dps = s_dpsiq[i * NQ + iq], ps = s_psiq[i * NQ + iq];
+      int w = iq * NGL + j;
+      r[0] += dps * s_A[0][w] + ps * s_A[1][w];
+      r[1] += dps * s_A[2][w] + ps * s_A[3][w];
+      r[2] += dps * s_A[4][w] + ps * s_A[5][w];
+    }
+    double lap0 = 0.0, lap1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < NGL; k++) {
+      lap0 -= s_dpsi[i * NGL + k] * s_lg[0][j * NGL + k] + s_dpsi[j * NGL + k] * s_lg[1][k * NGL + i];
+      lap1 -= s_dpsi[i * NGL + k] * s_lg[2][j * NGL + k] + s_dpsi[j * NGL + k] * s_lg[3][k * NGL + i];
+    }
+    for (int lf = 0; lf < 4; lf++) {
+      for (int n = 0; n < NGL; n++) {
+        if (s_map[lf][n] != p) continue;
+        double f0 = 0, f1 = 0, f2 = 0;
+#pragma unroll
+        for (int iq = 0; iq < NQ; iq++) {
+          double hi = s_psiq[n * NQ + iq];
+          f0 += hi * s_fq[lf][iq][0];
+          f1 += hi * s_fq[lf][iq][1];
+          f2 += hi * s_fq[lf][iq][2];
+        }
+        r[0] += f0;
+        r[1] += f1;
+        r[2] += f2;
+        lap0 += s_fl[lf][n][0];
+        lap1 += s_fl[lf][n][1];
+      }
+    }
+    const double mi = m.nstat[NS_MINV * (size_t)npoin + I];
+    double rh0 = mi * r[0], rh1 = mi * r[1], rh2 = mi * r[2];
+    rh1 = rh1 + m.visc * mi * lap0;
+    rh2 = rh2 + m.visc * mi * lap1;
+    if (a.rhs_only) {
+      a.rhs_out[I * 3 + 0] = rh0;
+      a.rhs_out[I * 3 + 1] = rh1;
+      a.rhs_out[I * 3 + 2] = rh2;
+    } else {
+      // Shu-Osher combination (mod_rk_mlswe.F90:99-106)
+      double rh[3] = {rh0, rh1, rh2};
+      for (int v = 1; v < 4; v++) {
+        double x = 0.0;
+        if (a.a1 != 0.0) x = a.a1 * a.qb0[I * 4 + v];
+        x = x + a.a2 * s_qb[v][p];
+        if (a.a3 != 0.0) x = x + a.a3 * a.qb2[I * 4 + v];
+        s_qn[v][p] = x + a.dtt * rh[v - 1];
+      }
+      s_qn[0][p] = s_qn[1][p] + m.nstat[NS_PB * (size_t)npoin + I];
+    }
+  }
+  if (a.rhs_only) return;
+  __syncthreads();
+  // ---------------------------------------------------------------- phase 5: wall fix
+  // btp_mom_boundary_df (mod_barotropic_terms.F90:180-215), faces in face-id order
+  for (int lf = 0; lf < 4; lf++) {
+    const int er = s_bc[lf];
+    if (er != -4 && er != -2) continue;  // block-uniform
+    const int f = s_face[lf];
+    for (int n = tid; n < NGL; n += BS) {
+      const int p = s_map[lf][n];
+      if (er == -4) {
+        size_t fn = (size_t)f * NGL + n, FN = (size_t)F * NGL;
+        double nx = m.fnstat[FN_NX * FN + fn], ny = m.fnstat[FN_NY * FN + fn];
+        double unl = s_qn[2][p] * nx + s_qn[3][p] * ny;
+        s_qn[2][p] = s_qn[2][p] - unl * nx;
+        s_qn[3][p] = s_qn[3][p] - unl * ny;
+      } else {
+        s_qn[2][p] = 0.0;
+        s_qn[3][p] = 0.0;
+      }
+    }
+    __syncthreads();
+  }
+  // ---------------------------------------------------------------- phase 6: outputs
+  for (int t = tid; t < 4 * P; t += BS) a.qb_out[(size_t)e * 4 * P + t] = s_qn[t % 4][t / 4];
+  if (a.write_grad) {
+    for (int p = tid; p < P; p += BS) {
+      s_uv[0][p] = s_qn[2][p] / s_qn[0][p];
+      s_uv[1][p] = s_qn[3][p] / s_qn[0][p];
+    }
+    __syncthreads();
+    for (int t = tid; t < 4 * NGL; t += BS) {
+      const int lf = t / NGL, n = t % NGL, p = s_map[lf][n];
+      const int i = p % NGL, j = p / NGL;
+      const size_t I = (size_t)e * P + p;
+      const double *NS = m.nstat;
+      double g4[4];
+      nodal_grad<NGL>(s_dpsi, s_uv[0], s_uv[1], i, j, NS[NS_EX * (size_t)npoin + I], NS[NS_EY * (size_t)npoin + I],
+                      NS[NS_NX * (size_t)npoin + I], NS[NS_NY * (size_t)npoin + I], g4);
+      for (int c = 0; c < 4; c++) a.gtrace_out[(((size_t)e * 4 + lf) * 4 + c) * NGL + n] = g4[c];
+    }
+  }
+}
+
+// Face traces of grad(u_bar) of a state (prologue of a sub-cycle / of a lone RHS).
+template <int NGL, int NQ>
+__global__ void __launch_bounds__(64) grad_trace_kernel(DevMesh m, const double *qb, double *gtrace) {
+  constexpr int P = NGL * NGL;
+  const int e = blockIdx.x, tid = threadIdx.x;
+  __shared__ double s_dpsi[NGL * NGL], s_u[P], s_v[P];
+  __shared__ int s_map[4][NGL];
+  for (int t = tid; t < NGL * NGL; t += 64) s_dpsi[t] = m.basis[2 * NGL * NQ + t];
+  for (int t = tid; t < 4 * NGL; t += 64) s_map[t / NGL][t % NGL] = m.efmap[e * 4 * NGL + t];
+  for (int p = tid; p < P; p += 64) {
+    const double *q = qb + ((size_t)e * P + p) * 4;
+    s_u[p] = q[2] / q[0];
+    s_v[p] = q[3] / q[0];
+  }
+  __syncthreads();
+  for (int t = tid; t < 4 * NGL; t += 64) {
+    const int lf = t / NGL, n = t % NGL, p = s_map[lf][n];
+    const size_t I = (size_t)e * P + p;
+    double g4[4];
+    nodal_grad<NGL>(s_dpsi, s_u, s_v, p % NGL, p / NGL, m.nstat[NS_EX * (size_t)m.npoin + I],
+                    m.nstat[NS_EY * (size_t)m.npoin + I], m.nstat[NS_NX * (size_t)m.npoin + I],
+                    m.nstat[NS_NY * (size_t)m.npoin + I], g4);
+    for (int c = 0; c < 4; c++) gtrace[(((size_t)e * 4 + lf) * 4 + c) * NGL + n] = g4[c];
+  }
+}
+
+// Normalisation of the time averages after the sub-cycle (mod_rk_mlswe.F90:124-149).
+// tau_wind_ave = (sum over N_btp of tau_wind) / N_btp, summed the same way as the reference.
+__global__ void btp_finalize_kernel(double *qacc, double *facc, double *nacc, double *gfacc, double *tau_wind_ave,
+                                    const double *tau_wind, int npq, int nfq, int npoin, int nfn, int N_btp,
+                                    double N_inv) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = tid; i < (size_t)QA_N * npq; i += stride) qacc[i] = N_inv * qacc[i];
+  for (size_t i = tid; i < (size_t)FA_N * nfq; i += stride) facc[i] = N_inv * facc[i];
+  for (size_t i = tid; i < (size_t)NA_N * npoin; i += stride) nacc[i] = N_inv * nacc[i];
+  for (size_t i = tid; i < (size_t)8 * nfn; i += stride) gfacc[i] = N_inv * gfacc[i];
+  for (size_t i = tid; i < (size_t)2 * npq; i += stride) {
+    double s = 0.0, t = tau_wind[i];
+    for (int k = 0; k < N_btp; k++) s = s + t;
+    tau_wind_ave[i] = s / (double)N_btp;
+  }
+}
+
+#define HNUMO_INSTANTIATE_BTP(NGL, NQ)                                 \
+  template __global__ void btp_stage_kernel<NGL, NQ>(StageArgs);        \
+  template __global__ void grad_trace_kernel<NGL, NQ>(DevMesh, const double *, double *);
+
+}  // namespace hnumo

@@ -1,0 +1,133 @@
+"""Python host mirror of the reference's engine boundary (ti_rk_bcl and its parity hooks)
+over the C ABI of libhnumo_engine.so (include/hnumo_engine.h).
+
+The product path is the HIP library; there is no CPU fallback.  Loading fails loudly if
+the library is missing or no GPU is visible.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import bundle as _bundle
+from .abi import Descriptors, HaloDesc
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libhnumo_engine.so")
+_lib = None
+
+ERRORS = {1: "negative layer thickness", 2: "non-finite value", 3: "HIP/RCCL error", 4: "invalid argument"}
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"hnumo engine error {code} ({ERRORS.get(code, '?')}): {msg}")
+        self.code = code
+
+
+def lib():
+    """Load libhnumo_engine.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FileNotFoundError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH)
+        vp, dp = C.c_void_p, C.POINTER(C.c_double)
+        L.hnumo_engine_create.argtypes = [vp, vp, vp, vp, C.c_int, C.POINTER(vp)]
+        L.hnumo_engine_destroy.argtypes = [vp]
+        L.hnumo_last_error.argtypes = [vp]
+        L.hnumo_last_error.restype = C.c_char_p
+        L.hnumo_ti_rk_bcl.argtypes = [vp, dp, dp, dp]
+        L.hnumo_ti_barotropic_ssprk.argtypes = [vp, dp, dp]
+        L.hnumo_btp_bcl_coeffs.argtypes = [vp, dp]
+        L.hnumo_create_rhs_btp.argtypes = [vp, dp, dp, dp]
+        L.hnumo_get_field.argtypes = [vp, C.c_char_p, dp, C.c_int64]
+        L.hnumo_set_resident.argtypes = [vp, C.c_int]
+        L.hnumo_sync.argtypes = [vp, dp, dp, dp]
+        L.hnumo_bench_steps.argtypes = [vp, C.c_int, dp, dp, C.POINTER(C.c_int64)]
+        L.hnumo_abi_version.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def _dp(a):
+    assert a.flags["F_CONTIGUOUS"] and a.dtype == np.float64
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class Engine:
+    """One engine per GPU: device-resident ti_rk_bcl for one Case."""
+
+    def __init__(self, case, device: int = 0, halo: HaloDesc | None = None):
+        self.case = case
+        self.desc = Descriptors(case, dense=False)
+        self.dims = _bundle.dims(case)
+        self.h = C.c_void_p()
+        self.halo = halo
+        L = lib()
+        rc = L.hnumo_engine_create(C.byref(self.desc.mesh), C.byref(self.desc.statics), C.byref(self.desc.params),
+                                   C.byref(halo) if halo is not None else None, device, C.byref(self.h))
+        if rc:
+            msg = L.hnumo_last_error(self.h).decode()
+            self._destroy()
+            raise EngineError(rc, msg)
+
+    def _check(self, rc):
+        if rc:
+            raise EngineError(rc, lib().hnumo_last_error(self.h).decode())
+
+    def state(self):
+        A = self.case.arrays
+        return (np.array(A["q_df"], order="F"), np.array(A["qb_df"], order="F"),
+                np.array(A["qprime_df"], order="F"))
+
+    # = ti_rk_bcl (ti_rk_bcl.F90:9)
+    def ti_rk_bcl(self, q, qb, qp):
+        self._check(lib().hnumo_ti_rk_bcl(self.h, _dp(q), _dp(qb), _dp(qp)))
+
+    def btp_bcl_coeffs(self, qp):
+        self._check(lib().hnumo_btp_bcl_coeffs(self.h, _dp(qp)))
+
+    # = ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:19)
+    def ti_barotropic_ssprk(self, qb, qp):
+        self._check(lib().hnumo_ti_barotropic_ssprk(self.h, _dp(qb), _dp(qp)))
+
+    # = create_rhs_btp (mod_rhs_btp.F90:28)
+    def create_rhs_btp(self, qb, qp):
+        rhs = np.zeros((3, self.dims["npoin"]), order="F")
+        self._check(lib().hnumo_create_rhs_btp(self.h, _dp(rhs), _dp(qb), _dp(qp)))
+        return rhs
+
+    def field(self, name):
+        shp = dict(_bundle.FIELDS)[name]
+        out = np.zeros(_bundle.shape_of(shp, self.dims), order="F")
+        self._check(lib().hnumo_get_field(self.h, name.encode(), _dp(out), out.size))
+        return out
+
+    def set_resident(self, on: bool):
+        self._check(lib().hnumo_set_resident(self.h, int(on)))
+
+    def sync(self, q, qb, qp):
+        self._check(lib().hnumo_sync(self.h, _dp(q), _dp(qb), _dp(qp)))
+
+    def bench_steps(self, nsteps: int):
+        t = C.c_double()
+        k = C.c_double()
+        n = C.c_int64()
+        self._check(lib().hnumo_bench_steps(self.h, nsteps, C.byref(t), C.byref(k), C.byref(n)))
+        return t.value, k.value, n.value
+
+    def _destroy(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            lib().hnumo_engine_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def close(self):
+        self._destroy()
+
+    def __del__(self):
+        try:
+            self._destroy()
+        except Exception:
+            pass

@@ -1,0 +1,68 @@
+"""Generates the golden vectors in tests/golden/ by running the REFERENCE Fortran hot path
+(oracle/_ref/ref_driver, built from /root/reference/src by oracle/build_ref.sh) on the
+inputs that h-numo_amd/hnumo/case.py builds.  Run in the build container only:
+
+    python tests/golden/make_golden.py
+
+Each fixture stores the sha256 of the input bundle, so a change to the setup code is
+detected instead of silently comparing against stale outputs.
+"""
+import hashlib
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "h-numo_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import oracle as O  # noqa: E402
+from hnumo import bundle as B  # noqa: E402
+from hnumo.case import build_case, make_config  # noqa: E402
+
+# (fixture name, config, mode, nsteps, node stride for the stored state)
+GOLDEN = [
+    ("bump10_rhs", "bump10", "rhs", 1, 1),
+    ("bump10_btp", "bump10", "btp", 1, 1),
+    ("bump10_step2", "bump10", "step", 2, 1),
+    ("lake10_step1", "lake10", "step", 1, 1),
+    ("dg25_step1", "dg25", "step", 1, 7),
+    ("dg25L3_step1", "dg25L3", "step", 1, 7),
+]
+FIELDS_KEPT = ["ope_ave", "H_ave", "Qu_ave", "btp_mass_flux_ave", "uvb_face_ave", "H_face_ave",
+               "graduvb_ave", "Q_uu_dp", "H_bcl_edge", "btp_graduv_dpp_face"]
+
+
+def bundle_hash(case, mode, nsteps):
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "b.bin")
+        B.write_bundle(p, case, mode, nsteps)
+        return hashlib.sha256(open(p, "rb").read()).hexdigest()
+
+
+def main():
+    for name, cfg, mode, nsteps, stride in GOLDEN:
+        case = build_case(make_config(cfg))
+        out = O.run_reference(case, mode, nsteps)
+        keep = {"bundle_sha256": np.array(bundle_hash(case, mode, nsteps)), "stride": np.array(stride),
+                "mode": np.array(mode), "nsteps": np.array(nsteps), "config": np.array(cfg)}
+        if mode == "rhs":
+            keep["rhs"] = out["rhs"]
+        keep["qb_df"] = out["qb_df"][:, ::stride]
+        if mode == "step":
+            keep["q_df"] = out["q_df"][:, ::stride, :]
+            keep["qprime_df"] = out["qprime_df"][:, ::stride, :]
+        for f in FIELDS_KEPT:
+            a = out[f]
+            keep["field_" + f] = a.reshape(-1, order="F")[::stride]
+        for k in ("ref_xgl", "ref_wgl", "ref_xnq", "ref_wnq", "ref_psiq", "ref_dpsiq", "ref_dpsi"):
+            keep[k] = out[k]
+        path = os.path.join(HERE, name + ".npz")
+        np.savez_compressed(path, **keep)
+        print(name, os.path.getsize(path))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,151 @@
+"""GPU parity tests: the HIP engine (through the C ABI) against the CPU oracle on the same
+inputs, and against the reference's golden vectors.  Tolerance: normwise relative
+difference <= 1e-10 (BASELINE.json north_star) -- the engine sum-factorises the
+integrals, so it agrees to rounding, not bitwise."""
+import os
+
+import numpy as np
+import pytest
+
+from util import layer_mass, rel
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def engines():
+    made = {}
+    yield made
+    for e in made.values():
+        e.close()
+
+
+def get_engine(engines, case):
+    from hnumo.engine import Engine
+    key = id(case)
+    if key not in engines:
+        engines[key] = Engine(case)
+    return engines[key]
+
+
+@pytest.mark.parametrize("cfg", ["bump10", "dg25", "dg25L3"])
+def test_rhs_stage_parity(cfg, case_factory, engines):
+    import oracle as O
+    case = case_factory(cfg)
+    o = O.Oracle(case)
+    e = get_engine(engines, case)
+    q, qb, qp = o.state()
+    # give the state some velocity so every term of the stage is active
+    o.btp_bcl_coeffs(qp)
+    o.ti_barotropic_ssprk(qb, qp)
+    o.btp_bcl_coeffs(qp)
+    r_o = o.create_rhs_btp(qb, qp)
+    e.btp_bcl_coeffs(qp)
+    r_e = e.create_rhs_btp(qb, qp)
+    for v in range(3):
+        assert rel(r_e[v], r_o[v]) < 1e-12, (v, rel(r_e[v], r_o[v]))
+    for f in ["Q_uu_dp", "H_bcl", "Q_uv_dp_edge", "H_bcl_edge", "btp_dpp_graduv", "pbprime_visc",
+              "btp_graduv_dpp_face", "H_ave", "Qu_ave", "ope_face_ave", "graduvb_ave", "graduvb_face_ave",
+              "btp_mass_flux_face_ave", "uvb_face_ave"]:
+        assert rel(e.field(f), o.field(f)) < 1e-12, f
+
+
+@pytest.mark.parametrize("cfg", ["bump10", "dg25L3"])
+def test_barotropic_subcycle_parity(cfg, case_factory, engines):
+    import oracle as O
+    from hnumo import bundle as B
+    case = case_factory(cfg)
+    o = O.Oracle(case)
+    e = get_engine(engines, case)
+    q, qb, qp = o.state()
+    qb_e = qb.copy(order="F")
+    o.btp_bcl_coeffs(qp)
+    o.ti_barotropic_ssprk(qb, qp)
+    e.btp_bcl_coeffs(qp)
+    e.ti_barotropic_ssprk(qb_e, qp)
+    for v in range(4):
+        assert rel(qb_e[v], qb[v]) < 1e-11, v
+    for f, _ in B.FIELDS:
+        if f.startswith("sum_layer"):
+            continue
+        assert rel(e.field(f), o.field(f)) < 1e-10, f
+
+
+@pytest.mark.parametrize("cfg,nsteps", [("bump10", 2), ("lake10", 1), ("dg25", 2), ("dg25L3", 2)])
+def test_baroclinic_step_parity(cfg, nsteps, case_factory, engines):
+    import oracle as O
+    case = case_factory(cfg)
+    o = O.Oracle(case)
+    e = get_engine(engines, case)
+    q, qb, qp = o.state()
+    qe, qbe, qpe = e.state()
+    for _ in range(nsteps):
+        o.ti_rk_bcl(q, qb, qp)
+        e.ti_rk_bcl(qe, qbe, qpe)
+    L = case.scalars["nlayers"]
+    for k in range(L):
+        for v in range(3):
+            assert rel(qe[v, :, k], q[v, :, k]) < TOL, ("q", v, k, rel(qe[v, :, k], q[v, :, k]))
+            assert rel(qpe[v, :, k], qp[v, :, k]) < TOL, ("qprime", v, k, rel(qpe[v, :, k], qp[v, :, k]))
+    for v in range(4):
+        assert rel(qbe[v], qb[v]) < TOL, ("qb", v)
+
+
+@pytest.mark.parametrize("name", ["bump10_step2", "lake10_step1", "dg25_step1", "dg25L3_step1"])
+def test_engine_matches_reference_golden(name, case_factory, engines):
+    g = dict(np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False))
+    case = case_factory(str(g["config"]))
+    e = get_engine(engines, case)
+    q, qb, qp = e.state()
+    for _ in range(int(g["nsteps"])):
+        e.ti_rk_bcl(q, qb, qp)
+    s = int(g["stride"])
+    for k, a in [("q_df", q[:, ::s, :]), ("qprime_df", qp[:, ::s, :]), ("qb_df", qb[:, ::s])]:
+        for v in range(a.shape[0]):
+            assert rel(a[v], g[k][v]) < TOL, (k, v)
+
+
+def test_n7_step_parity(case_factory):
+    """C3 configuration (N=7, 3 layers, LDS-tiled 8x8 nodes / 15x15 quad points)."""
+    import oracle as O
+    from hnumo.engine import Engine
+    case = case_factory("dg25N7L3", nelx=8, nely=8)
+    o = O.Oracle(case)
+    e = Engine(case)
+    q, qb, qp = o.state()
+    qe, qbe, qpe = e.state()
+    o.ti_rk_bcl(q, qb, qp)
+    e.ti_rk_bcl(qe, qbe, qpe)
+    for v in range(4):
+        assert rel(qbe[v], qb[v]) < TOL
+    assert rel(qe, q) < TOL and rel(qpe, qp) < TOL
+    e.close()
+
+
+def test_mass_conservation_and_resident_mode(case_factory):
+    from hnumo.engine import Engine
+    case = case_factory("bump10")
+    e = Engine(case)
+    q, qb, qp = e.state()
+    m0 = layer_mass(case, q)
+    e.set_resident(True)
+    for _ in range(5):
+        e.ti_rk_bcl(q, qb, qp)
+    e.sync(q, qb, qp)
+    loss = np.abs(layer_mass(case, q) - m0) / m0
+    assert (loss <= 1e-12).all(), loss
+    e.close()
+
+
+def test_negative_thickness_is_reported(case_factory):
+    from hnumo.engine import Engine, EngineError
+    case = case_factory("bump10", dt=5.0e4, dt_btp=1.0e4)
+    e = Engine(case)
+    q, qb, qp = e.state()
+    with pytest.raises(EngineError) as ei:
+        for _ in range(3):
+            e.ti_rk_bcl(q, qb, qp)
+    assert ei.value.code in (1, 2)
+    e.close()

@@ -1,0 +1,108 @@
+"""CPU tests: the oracle (C restatement) against the reference's golden vectors and, where
+the reference harness can be built (oracle/_ref), against the reference Fortran itself."""
+import hashlib
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+from util import layer_mass
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+GOLDEN = ["bump10_rhs", "bump10_btp", "bump10_step2", "lake10_step1", "dg25_step1", "dg25L3_step1"]
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False))
+
+
+def bundle_hash(case, mode, nsteps):
+    from hnumo import bundle as B
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "b.bin")
+        B.write_bundle(p, case, mode, nsteps)
+        return hashlib.sha256(open(p, "rb").read()).hexdigest()
+
+
+def test_basis_matches_reference_bitwise():
+    """LGL nodes/weights and the interpolation/derivative tables equal the reference's
+    mod_basis_create output (mod_basis.F90:60-186) bit for bit."""
+    from hnumo.basis import Basis
+    g = load("bump10_rhs")
+    b = Basis(4)
+    for k, v in [("xgl", b.xgl), ("wgl", b.wgl), ("xnq", b.xnq), ("wnq", b.wnq), ("psiq", b.psiq),
+                 ("dpsiq", b.dpsiq), ("dpsi", b.dpsi)]:
+        assert np.array_equal(g["ref_" + k], v), k
+
+
+@pytest.mark.parametrize("name", GOLDEN)
+def test_oracle_matches_golden(name, case_factory):
+    import oracle as O
+    g = load(name)
+    cfg, mode, nsteps, stride = str(g["config"]), str(g["mode"]), int(g["nsteps"]), int(g["stride"])
+    case = case_factory(cfg)
+    assert bundle_hash(case, mode, nsteps) == str(g["bundle_sha256"]), "setup inputs changed: regenerate golden"
+    o = O.Oracle(case)
+    q, qb, qp = o.state()
+    if mode == "rhs":
+        o.btp_bcl_coeffs(qp)
+        rhs = o.create_rhs_btp(qb, qp)
+        assert np.array_equal(rhs, g["rhs"])
+    elif mode == "btp":
+        o.btp_bcl_coeffs(qp)
+        o.ti_barotropic_ssprk(qb, qp)
+    else:
+        for _ in range(nsteps):
+            o.ti_rk_bcl(q, qb, qp)
+        assert np.array_equal(q[:, ::stride, :], g["q_df"])
+        assert np.array_equal(qp[:, ::stride, :], g["qprime_df"])
+    assert np.array_equal(qb[:, ::stride], g["qb_df"])
+    for k in g:
+        if k.startswith("field_"):
+            a = o.field(k[6:]).reshape(-1, order="F")[::stride]
+            assert np.array_equal(a, g[k]), k
+
+
+@pytest.mark.ref
+@pytest.mark.parametrize("variant", [
+    dict(name="bump10", botfr=2, cd=1e-3, visc=25.0, method_visc=3, y_boundary=(2, 2)),
+    dict(name="bump10", botfr=1, cd=1e-7, f0=1e-4, beta=1e-11, x_boundary=(2, 4)),
+    dict(name="lake10", nlayers=3),
+])
+def test_oracle_matches_reference_fortran(variant):
+    """Branches the shipped configs do not exercise (quadratic drag, no-slip walls, mixed
+    BCs, 3-layer lake): oracle vs the reference Fortran, bitwise, 1 baroclinic step."""
+    import oracle as O
+    from hnumo.case import build_case, make_config
+    v = dict(variant)
+    case = build_case(make_config(v.pop("name"), **v))
+    ref = O.run_reference(case, "step", 1)
+    o = O.Oracle(case)
+    q, qb, qp = o.state()
+    o.ti_rk_bcl(q, qb, qp)
+    for k, a in [("q_df", q), ("qb_df", qb), ("qprime_df", qp)]:
+        assert np.array_equal(a, ref[k]), k
+
+
+def test_bump_mass_conservation(case_factory):
+    """The reference's only CI assertion: per-layer mass loss <= 1e-12 (CI/bump/check.F90:58)."""
+    import oracle as O
+    case = case_factory("bump10")
+    o = O.Oracle(case)
+    q, qb, qp = o.state()
+    m0 = layer_mass(case, q)
+    for _ in range(2):
+        o.ti_rk_bcl(q, qb, qp)
+    loss = np.abs(layer_mass(case, q) - m0) / m0
+    assert (loss <= 1e-12).all(), loss
+
+
+def test_lake_at_rest_is_well_balanced(case_factory):
+    import oracle as O
+    case = case_factory("lake10")
+    o = O.Oracle(case)
+    q, qb, qp = o.state()
+    o.ti_rk_bcl(q, qb, qp)
+    assert np.abs(qb[2:4]).max() < 1e-6 * np.abs(qb[0]).max()
