@@ -374,14 +374,17 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   HIPCHK(hipMemcpy(eng->iconn, conn.data(), conn.size() * sizeof(int), hipMemcpyHostToDevice));
 
   // ---- statics
-  std::vector<double> hb(2 * ngl * nq + ngl * ngl);
+  std::vector<double> hb(2 * ngl * nq + 2 * ngl * ngl);
   for (int n = 0; n < ngl; n++)
     for (int iq = 0; iq < nq; iq++) {
       hb[n * nq + iq] = mesh->psiq[n + ngl * iq];
       hb[ngl * nq + n * nq + iq] = mesh->dpsiq[n + ngl * iq];
     }
   for (int n = 0; n < ngl; n++)
-    for (int k = 0; k < ngl; k++) hb[2 * ngl * nq + n * ngl + k] = mesh->dpsi[n + ngl * k];
+    for (int k = 0; k < ngl; k++) {
+      hb[2 * ngl * nq + n * ngl + k] = mesh->dpsi[n + ngl * k];
+      hb[2 * ngl * nq + ngl * ngl + n * ngl + k] = mesh->psi[n + ngl * k];
+    }
   std::vector<double> qs(QS_N * npq), ns(NS_N * npoin), fs(FS_N * FQ), fns(FN_N * FN);
   for (size_t i = 0; i < npq; i++) {
     qs[QS_W * npq + i] = mesh->jacq[i];
@@ -460,8 +463,8 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   eng->tau_wind_ave = dalloc<double>(eng, 2 * npq);
   eng->slmf = dalloc<double>(eng, 2 * npq); eng->slmf_face = dalloc<double>(eng, 2 * FQ);
   eng->dpp = dalloc<double>(eng, npoin * L);
-  eng->fmass = dalloc<double>(eng, FN * L); eng->fcons = dalloc<double>(eng, FN * L);
-  eng->momL = dalloc<double>(eng, 2 * FN * L); eng->momR = dalloc<double>(eng, 2 * FN * L);
+  eng->fmass = dalloc<double>(eng, FQ * L); eng->fcons = dalloc<double>(eng, FQ * L);
+  eng->momL = dalloc<double>(eng, 2 * FQ * L); eng->momR = dalloc<double>(eng, 2 * FQ * L);
   eng->lapf = dalloc<double>(eng, 2 * FN * L);
   eng->rhs = dalloc<double>(eng, 3 * npoin);
   eng->neg_flag = dalloc<int>(eng, 1);
@@ -632,7 +635,13 @@ int hnumo_get_field(hnumo_engine *eng, const char *name, double *out, int64_t n)
   if (s == "btp_mass_flux_ave") return soa(eng->qacc, npq, {QA_MFX, QA_MFY});
   if (s == "uvb_ave") return soa(eng->qacc, npq, {QA_UB, QA_VB});
   if (s == "tau_bot_ave") return soa(eng->qacc, npq, {QA_TBU, QA_TBV});
-  if (s == "tau_wind_ave") return soa(eng->tau_wind_ave, npq, {0, 1});
+  if (s == "tau_wind_ave") {  // kept in the reference layout (2,npoin_q)
+    if ((size_t)n != 2 * npq) return fail(eng, HNUMO_ERR_INVALID, "field size mismatch");
+    int rc = fetch(eng->tau_wind_ave, 2 * npq, h);
+    if (rc) return rc;
+    std::copy(h.begin(), h.end(), out);
+    return 0;
+  }
   if (s == "ope2_ave_df") return soa(eng->nacc, npoin, {NA_OPE2});
   if (s == "uvb_ave_df") return soa(eng->nacc, npoin, {NA_UB, NA_VB});
   if (s == "graduvb_ave") return soa(eng->nacc, npoin, {NA_G1, NA_G2, NA_G3, NA_G4});

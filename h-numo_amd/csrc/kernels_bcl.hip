@@ -33,13 +33,58 @@ __device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : 
 __device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : (b > a ? b : a); }
 
 template <int NGL, int NQ>
-__device__ __forceinline__ void load_basis(const DevMesh &m, double *s_psiq, double *s_dpsiq, double *s_dpsi, int tid,
-                                           int bs) {
+__device__ __forceinline__ void load_basis(const DevMesh &m, double *s_psiq, double *s_dpsiq, double *s_dpsi,
+                                           double *s_psi, int tid, int bs) {
   for (int t = tid; t < NGL * NQ; t += bs) {
     s_psiq[t] = m.basis[t];
     s_dpsiq[t] = m.basis[NGL * NQ + t];
   }
-  for (int t = tid; t < NGL * NGL; t += bs) s_dpsi[t] = m.basis[2 * NGL * NQ + t];
+  for (int t = tid; t < NGL * NGL; t += bs) {
+    s_dpsi[t] = m.basis[2 * NGL * NQ + t];
+    s_psi[t] = m.basis[2 * NGL * NQ + NGL * NGL + t];
+  }
+}
+
+// Reference-order term definitions (Tensor_product.F90:71-114); see kernels_btp.hip.
+#define PSIH(n, m, iq, jq) (s_psiq[(n)*NQ + (iq)] * s_psiq[(m)*NQ + (jq)])
+#define HE(n, m, iq, jq) (s_dpsiq[(n)*NQ + (iq)] * s_psiq[(m)*NQ + (jq)])
+#define HN(n, m, iq, jq) (s_psiq[(n)*NQ + (iq)] * s_dpsiq[(m)*NQ + (jq)])
+#define HE_DF(n, m, i, j) (s_dpsi[(n)*NGL + (i)] * s_psi[(m)*NGL + (j)])
+#define HN_DF(n, m, i, j) (s_psi[(n)*NGL + (i)] * s_dpsi[(m)*NGL + (j)])
+
+// sum_q w(q)*(dpsidx(p,q)*fx(q) + dpsidy(p,q)*fy(q)) accumulated onto acc in quad order
+// (the weak-form divergence of mod_create_rhs_mlswe.F90:866-868 / :911-913)
+template <int NGL, int NQ>
+__device__ __forceinline__ double weak_div(const double *s_psiq, const double *s_dpsiq, const double *qm0,
+                                           const double *qm1, const double *qm2, const double *qm3, const double *w,
+                                           const double *fx, const double *fy, int i, int j, double acc) {
+  for (int q = 0; q < NQ * NQ; q++) {
+    const int iq = q % NQ, jq = q / NQ;
+    const double h_e = HE(i, j, iq, jq), h_n = HN(i, j, iq, jq);
+    const double dhdx = h_e * qm0[q] + h_n * qm2[q];
+    const double dhdy = h_e * qm1[q] + h_n * qm3[q];
+    acc = acc + w[q] * (dhdx * fx[q] + dhdy * fy[q]);
+  }
+  return acc;
+}
+
+// face terms of one face onto node p: acc -/+ (wq*hi)*flux(iq), quad order (left: -, right: +)
+template <int NGL, int NQ>
+__device__ __forceinline__ double face_terms(const double *s_psiq, const int *s_map, const int *s_face,
+                                             const int *s_side, const double *fw, const double *flux, size_t fstride,
+                                             int p, double acc) {
+  for (int lf = 0; lf < 4; lf++)
+    for (int n = 0; n < NGL; n++) {
+      if (s_map[lf * NGL + n] != p) continue;
+      const size_t b = (size_t)s_face[lf] * NQ;
+      const bool left = s_side[lf] == 0;
+      for (int iq = 0; iq < NQ; iq++) {
+        const double c = fw[b + iq] * s_psiq[n * NQ + iq] * flux[b + iq];
+        acc = left ? acc - c : acc + c;
+      }
+    }
+  (void)fstride;
+  return acc;
 }
 
 // ===================================================================== face traces
@@ -96,43 +141,37 @@ __global__ void average_kernel(double *out, const double *a, const double *b, si
 }
 
 // ======================================================= btp_bcl_coeffs_qdf: element
-// Q_uu_dp, Q_uv_dp, Q_vv_dp, H_bcl at quad points; dpp_graduv, btp_dpp_graduv,
-// pbprime_visc at nodes (dpprime_visc = qprime(1,:,:) is stored for the layer LDG).
+// Q_uu_dp, Q_uv_dp, Q_vv_dp, H_bcl at quad points (mod_barotropic_terms.F90:265-283);
+// dpp_graduv, btp_dpp_graduv, pbprime_visc at nodes (:287-304).  dpprime_visc =
+// qprime(1,:,:) is stored for the layer LDG (ti_rk_bcl.F90:47,66).
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     bcl_coeffs_elem_kernel(DevMesh m, const double *qp, double *qcoef, double *ncoef, double *dpp_graduv,
                            double *dpprime_visc) {
   constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BS;
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q;
-  __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL];
+  __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
   __shared__ double s_q[MAXL][3][P];
-  __shared__ double s_T[MAXL * 3][NQ * NGL];
-  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, tid, BS);
+  __shared__ double s_nm[4][P];
+  __shared__ double s_g[MAXL][4][P];
+  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
   for (int t = tid; t < L * 3 * P; t += BS) {
     int k = t / (3 * P), r = t % (3 * P);
     s_q[k][r % 3][r / 3] = qp[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
   }
-  __syncthreads();
-  for (int t = tid; t < NQ * NGL; t += BS) {
-    int iq = t / NGL, mm = t % NGL;
-    for (int k = 0; k < L; k++)
-      for (int v = 0; v < 3; v++) {
-        double acc = 0.0;
-        for (int n = 0; n < NGL; n++) acc += s_psiq[n * NQ + iq] * s_q[k][v][mm * NGL + n];
-        s_T[k * 3 + v][t] = acc;
-      }
-  }
+  for (int t = tid; t < 4 * P; t += BS)
+    s_nm[t / P][t % P] = m.nstat[(NS_EX + t / P) * (size_t)npoin + (size_t)e * P + t % P];
   __syncthreads();
   for (int q = tid; q < Q; q += BS) {
     const int iq = q % NQ, jq = q / NQ;
     double quu = 0.0, quv = 0.0, qvv = 0.0, hb = 0.0, pk = 0.0;
     for (int k = 0; k < L; k++) {
-      double qq[3];
-      for (int v = 0; v < 3; v++) {
-        double acc = 0.0;
-        for (int mm = 0; mm < NGL; mm++) acc += s_psiq[mm * NQ + jq] * s_T[k * 3 + v][iq * NGL + mm];
-        qq[v] = acc;
-      }
+      double qq[3] = {0.0, 0.0, 0.0};
+      for (int mm = 0; mm < NGL; mm++)
+        for (int n = 0; n < NGL; n++) {
+          const double hi = PSIH(n, mm, iq, jq);
+          for (int v = 0; v < 3; v++) qq[v] = qq[v] + hi * s_q[k][v][mm * NGL + n];
+        }
       quu = quu + qq[1] * (qq[1] * qq[0]);
       quv = quv + qq[2] * (qq[1] * qq[0]);
       qvv = qvv + qq[2] * (qq[2] * qq[0]);
@@ -146,26 +185,25 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     qcoef[QC_QVV * (size_t)npq + Iq] = qvv;
     qcoef[QC_HBCL * (size_t)npq + Iq] = hb;
   }
+  // compute_gradient_uv of (u'_k, v'_k), reference order, one thread per (layer, comp, node)
+  for (int t = tid; t < L * 4 * P; t += BS) {
+    const int k = t / (4 * P), c = (t / P) % 4, p = t % P, i = p % NGL, j = p / NGL;
+    const double *u = s_q[k][1 + (c >> 1)];
+    const double ex = s_nm[(c & 1) ? 1 : 0][p], nx = s_nm[(c & 1) ? 3 : 2][p];
+    double gsum = 0.0;
+    for (int mm = 0; mm < NGL; mm++)
+      for (int n = 0; n < NGL; n++) gsum = gsum + (HE_DF(n, mm, i, j) * ex + HN_DF(n, mm, i, j) * nx) * u[mm * NGL + n];
+    s_g[k][c][p] = gsum;
+  }
+  __syncthreads();
   for (int p = tid; p < P; p += BS) {
-    const int i = p % NGL, j = p / NGL;
     const size_t I = (size_t)e * P + p;
-    const double ex = m.nstat[NS_EX * (size_t)npoin + I], ey = m.nstat[NS_EY * (size_t)npoin + I];
-    const double nx = m.nstat[NS_NX * (size_t)npoin + I], ny = m.nstat[NS_NY * (size_t)npoin + I];
     double sum[4] = {0, 0, 0, 0}, pv = 0.0;
     for (int k = 0; k < L; k++) {
-      double ux = 0, uy = 0, vx = 0, vy = 0;
-      for (int n = 0; n < NGL; n++) {
-        double dx = s_dpsi[n * NGL + i], dy = s_dpsi[n * NGL + j];
-        ux += dx * s_q[k][1][j * NGL + n];
-        vx += dx * s_q[k][2][j * NGL + n];
-        uy += dy * s_q[k][1][n * NGL + i];
-        vy += dy * s_q[k][2][n * NGL + i];
-      }
-      double g[4] = {ex * ux + nx * uy, ey * ux + ny * uy, ex * vx + nx * vy, ey * vx + ny * vy};
       double d = s_q[k][0][p];
       dpprime_visc[(size_t)k * npoin + I] = d;
       for (int c = 0; c < 4; c++) {
-        double dg = d * g[c];
+        double dg = d * s_g[k][c][p];
         dpp_graduv[((size_t)k * 4 + c) * npoin + I] = dg;
         sum[c] = sum[c] + dg;
       }
@@ -254,22 +292,21 @@ __global__ void __launch_bounds__(64)
 }
 
 // ====================================================== layer mass: face fluxes
-// create_layer_mass_flux (mod_create_rhs_mlswe.F90:922-1034): per face, per layer, upwind
-// mass flux at face quad points projected onto the face nodes.  fmass[k][f][n] is the
-// contribution to the LEFT element's node (the right element receives its negative).
+// create_layer_mass_flux (mod_create_rhs_mlswe.F90:922-1034): upwind mass flux per face,
+// layer and face quad point: fmass[k][f*NQ+iq] = nx*flux_edge_u + ny*flux_edge_v; the
+// element kernels apply -/+ (wq*hi)*flux in the reference's order.
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(64)
     mass_flux_face_kernel(DevMesh m, const double *qf, const double *facc, double *fmass, double *slmf_face) {
   const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L;
   __shared__ double s_psiq[NGL * NQ];
-  __shared__ double s_fl[MAXL][NQ];
   for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
   __syncthreads();
   const size_t FQ = (size_t)F * NQ;
   if (tid < NQ) {
     const int iq = tid;
     const size_t fq = (size_t)f * NQ + iq;
-    double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq], wq = m.fstat[FS_W * FQ + fq];
+    double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
     double qbl0 = facc[FA_OPEL * FQ + fq], qbr0 = facc[FA_OPER * FQ + fq];
     double qbl1 = facc[FA_UL * FQ + fq], qbr1 = facc[FA_UR * FQ + fq];
     double qbl2 = facc[FA_VL * FQ + fq], qbr2 = facc[FA_VR * FQ + fq];
@@ -290,35 +327,28 @@ __global__ void __launch_bounds__(64)
       double fev = (vv * nyl > 0.0) ? vv * dpl : vv * dpr;
       su = su + feu;
       sv = sv + fev;
-      s_fl[k][iq] = -wq * (nxl * feu + nyl * fev);
+      fmass[(size_t)k * FQ + fq] = nxl * feu + nyl * fev;
     }
     slmf_face[0 * FQ + fq] = su;
     slmf_face[1 * FQ + fq] = sv;
   }
-  __syncthreads();
-  if (tid < L * NGL) {
-    const int k = tid / NGL, n = tid % NGL;
-    double s = 0.0;
-    for (int iq = 0; iq < NQ; iq++) s += s_psiq[n * NQ + iq] * s_fl[k][iq];
-    fmass[((size_t)k * F + f) * NGL + n] = s;
-  }
 }
 
 // =============================================== consistency: face deficit fluxes
-// evaluate_consistency_face + create_consistency_mass_flux: dpp = dp'(npoin,L) nodal.
+// evaluate_consistency_face (mod_layer_terms.F90:57-137) + the upwind selection of
+// create_consistency_mass_flux (mod_create_rhs_mlswe.F90:1036-1115); dpp = dp'(npoin,L).
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(64)
     cons_flux_face_kernel(DevMesh m, const double *dpp, const double *facc, const double *slmf_face, double *fcons) {
   const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L, npoin = m.npoin;
   __shared__ double s_psiq[NGL * NQ];
-  __shared__ double s_fl[MAXL][NQ];
   for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
   __syncthreads();
   const size_t FQ = (size_t)F * NQ;
   if (tid < NQ) {
     const int iq = tid, er = m.fer[f];
     const size_t fq = (size_t)f * NQ + iq;
-    double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq], wq = m.fstat[FS_W * FQ + fq];
+    double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
     double d1 = facc[FA_MFX * FQ + fq] - slmf_face[0 * FQ + fq];
     double d2 = facc[FA_MFY * FQ + fq] - slmf_face[1 * FQ + fq];
     double pbl = m.fstat[FS_PBL * FQ + fq], pbr = m.fstat[FS_PBR * FQ + fq];
@@ -336,49 +366,28 @@ __global__ void __launch_bounds__(64)
       double m11 = wl * d1, m21 = wl * d2, m12 = wr * d1, m22 = wr * d2;
       double feu = (m11 * nxl > 0.0) ? m11 : m12;
       double fev = (m21 * nyl > 0.0) ? m21 : m22;
-      s_fl[k][iq] = -wq * (nxl * feu + nyl * fev);
+      fcons[(size_t)k * FQ + fq] = nxl * feu + nyl * fev;
     }
   }
-  __syncthreads();
-  if (tid < L * NGL) {
-    const int k = tid / NGL, n = tid % NGL;
-    double s = 0.0;
-    for (int iq = 0; iq < NQ; iq++) s += s_psiq[n * NQ + iq] * s_fl[k][iq];
-    fcons[((size_t)k * F + f) * NGL + n] = s;
-  }
-}
-
-// gather of an antisymmetric face contribution at local node p of element e (left: +c, right: -c)
-template <int NGL>
-__device__ __forceinline__ double gather_anti(const int *s_map, const int *s_face, const int *s_side, const double *buf,
-                                              int F, int p) {
-  double s = 0.0;
-  for (int lf = 0; lf < 4; lf++)
-    for (int n = 0; n < NGL; n++)
-      if (s_map[lf * NGL + n] == p) {
-        double c = buf[(size_t)s_face[lf] * NGL + n];
-        s += s_side[lf] == 0 ? c : -c;
-      }
-  return s;
 }
 
 // ==================================================== layer mass: element update
-// create_layers_volume_mass + gather + massinv + q(1) += dt*dp_advec + negativity check
-// (mod_splitting.F90:69-78 / :224-232), then dp' = q(1)/(sum_k q(1)/pb') for consistency.
+// create_layers_volume_mass (mod_create_rhs_mlswe.F90:822-877) + face terms + massinv
+// (:74-76), q(1) += dt*dp_advec and the negativity check (mod_splitting.F90:69-78 /
+// :224-232), then dp' = q(1)/(sum_k q(1)/pb') for the consistency step (:350-353).
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     mass_elem_kernel(DevMesh m, const double *qp, const double *qacc, const double *fmass, double *q,
                      double *slmf, double *dpp, int *neg_flag) {
   constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BS;
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
-  __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL];
+  __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
   __shared__ double s_q[MAXL][3][P];
-  __shared__ double s_T[MAXL * 3][NQ * NGL];
-  __shared__ double s_G[MAXL][2][Q];
-  __shared__ double s_A[MAXL][2][NQ * NGL];
-  __shared__ double s_new[MAXL][P];
+  __shared__ double s_qm[5][Q];             // e_x, e_y, n_x, n_y, w
+  __shared__ double s_f[MAXL][2][Q];        // udp, vdp per layer
+  __shared__ double s_adv[MAXL][P];
   __shared__ int s_map[4 * NGL], s_face[4], s_side[4];
-  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, tid, BS);
+  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
   if (tid < 4) {
     s_face[tid] = m.efaces[e * 4 + tid];
     s_side[tid] = m.eside[e * 4 + tid];
@@ -388,15 +397,9 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     int k = t / (3 * P), r = t % (3 * P);
     s_q[k][r % 3][r / 3] = qp[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
   }
-  __syncthreads();
-  for (int t = tid; t < NQ * NGL; t += BS) {
-    int iq = t / NGL, mm = t % NGL;
-    for (int k = 0; k < L; k++)
-      for (int v = 0; v < 3; v++) {
-        double acc = 0.0;
-        for (int n = 0; n < NGL; n++) acc += s_psiq[n * NQ + iq] * s_q[k][v][mm * NGL + n];
-        s_T[k * 3 + v][t] = acc;
-      }
+  for (int t = tid; t < 5 * Q; t += BS) {
+    const int c = t / Q;
+    s_qm[c][t % Q] = m.qstat[(c < 4 ? QS_EX + c : QS_W) * (size_t)npq + (size_t)e * Q + t % Q];
   }
   __syncthreads();
   for (int q = tid; q < Q; q += BS) {
@@ -404,162 +407,129 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     const size_t Iq = (size_t)e * Q + q;
     double qb0 = qacc[QA_OPE * (size_t)npq + Iq], qb1 = qacc[QA_UB * (size_t)npq + Iq],
            qb2 = qacc[QA_VB * (size_t)npq + Iq];
-    double wq = m.qstat[QS_W * (size_t)npq + Iq];
-    double ex = m.qstat[QS_EX * (size_t)npq + Iq], ey = m.qstat[QS_EY * (size_t)npq + Iq];
-    double nx = m.qstat[QS_NX * (size_t)npq + Iq], ny = m.qstat[QS_NY * (size_t)npq + Iq];
     double su = 0.0, sv = 0.0;
     for (int k = 0; k < L; k++) {
-      double qq[3];
-      for (int v = 0; v < 3; v++) {
-        double acc = 0.0;
-        for (int mm = 0; mm < NGL; mm++) acc += s_psiq[mm * NQ + jq] * s_T[k * 3 + v][iq * NGL + mm];
-        qq[v] = acc;
-      }
+      double qq[3] = {0.0, 0.0, 0.0};
+      for (int mm = 0; mm < NGL; mm++)
+        for (int n = 0; n < NGL; n++) {
+          const double hi = PSIH(n, mm, iq, jq);
+          for (int v = 0; v < 3; v++) qq[v] = qq[v] + hi * s_q[k][v][mm * NGL + n];
+        }
       double dp_temp = qq[0] * qb0;
       double udp = (qq[1] + qb1) * dp_temp;
       double vdp = (qq[2] + qb2) * dp_temp;
       su = su + udp;
       sv = sv + vdp;
-      s_G[k][0][q] = wq * (ex * udp + ey * vdp);
-      s_G[k][1][q] = wq * (nx * udp + ny * vdp);
+      s_f[k][0][q] = udp;
+      s_f[k][1][q] = vdp;
     }
     slmf[0 * (size_t)npq + Iq] = su;
     slmf[1 * (size_t)npq + Iq] = sv;
   }
   __syncthreads();
-  for (int t = tid; t < NQ * NGL; t += BS) {
-    int iq = t / NGL, mm = t % NGL;
-    for (int k = 0; k < L; k++) {
-      double ax = 0, ap = 0;
-      for (int jq = 0; jq < NQ; jq++) {
-        ax += s_psiq[mm * NQ + jq] * s_G[k][0][jq * NQ + iq];
-        ap += s_dpsiq[mm * NQ + jq] * s_G[k][1][jq * NQ + iq];
-      }
-      s_A[k][0][t] = ax;
-      s_A[k][1][t] = ap;
-    }
+  for (int t = tid; t < L * P; t += BS) {
+    const int k = t / P, p = t % P, i = p % NGL, j = p / NGL;
+    double acc = weak_div<NGL, NQ>(s_psiq, s_dpsiq, s_qm[0], s_qm[1], s_qm[2], s_qm[3], s_qm[4], s_f[k][0], s_f[k][1],
+                                   i, j, 0.0);
+    acc = face_terms<NGL, NQ>(s_psiq, s_map, s_face, s_side, m.fstat + FS_W * (size_t)F * NQ,
+                              fmass + (size_t)k * F * NQ, 0, p, acc);
+    const size_t I = (size_t)e * P + p;
+    double adv = m.nstat[NS_MINV * (size_t)npoin + I] * acc;
+    double v = q[((size_t)k * npoin + I) * 3] + m.dt * adv;
+    if (v < 0.0) atomicOr(neg_flag, 1);
+    q[((size_t)k * npoin + I) * 3] = v;
+    s_adv[k][p] = v;
   }
   __syncthreads();
   for (int p = tid; p < P; p += BS) {
-    const int i = p % NGL, j = p / NGL;
     const size_t I = (size_t)e * P + p;
-    const double mi = m.nstat[NS_MINV * (size_t)npoin + I];
     double sum = 0.0;
-    for (int k = 0; k < L; k++) {
-      double r = 0.0;
-      for (int iq = 0; iq < NQ; iq++) r += s_dpsiq[i * NQ + iq] * s_A[k][0][iq * NGL + j] + s_psiq[i * NQ + iq] * s_A[k][1][iq * NGL + j];
-      r += gather_anti<NGL>(s_map, s_face, s_side, fmass + (size_t)k * F * NGL, F, p);
-      double adv = mi * r;
-      double v = q[((size_t)k * npoin + I) * 3] + m.dt * adv;
-      if (v < 0.0) atomicOr(neg_flag, 1);
-      q[((size_t)k * npoin + I) * 3] = v;
-      s_new[k][p] = v;
-      sum = sum + v;
-    }
+    for (int k = 0; k < L; k++) sum = sum + s_adv[k][p];
     double ope = sum / m.nstat[NS_PB * (size_t)npoin + I];
-    for (int k = 0; k < L; k++) dpp[(size_t)k * npoin + I] = s_new[k][p] / ope;
+    for (int k = 0; k < L; k++) dpp[(size_t)k * npoin + I] = s_adv[k][p] / ope;
   }
 }
 
 // ============================================== consistency: element update
-// create_consistency_volume_mass + gather + q(1) += dt*massinv*dp_advec (mod_splitting.F90:362-364).
-// finalize_dp: (thickness) also qprime(1,:,k) = q(1,:,k)/(sum_k q(1)/pb') (mod_splitting.F90:84-87).
+// create_consistency_volume_mass (mod_create_rhs_mlswe.F90:879-920) + face terms, then
+// q(1) += dt*massinv*dp_advec (mod_splitting.F90:362-364).  finalize_dp (thickness): also
+// qprime(1,:,k) = q(1,:,k)/(sum_k q(1)/pb') (mod_splitting.F90:84-87).
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     cons_elem_kernel(DevMesh m, const double *dpp, const double *qacc, const double *slmf, const double *fcons,
                      double *q, double *qp_out, int finalize_dp) {
   constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BS;
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
-  __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL];
+  __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
   __shared__ double s_d[MAXL][P];
-  __shared__ double s_T[MAXL][NQ * NGL];
-  __shared__ double s_G[MAXL][2][Q];
-  __shared__ double s_A[MAXL][2][NQ * NGL];
+  __shared__ double s_qm[5][Q];
+  __shared__ double s_f[MAXL][2][Q];
   __shared__ double s_new[MAXL][P];
   __shared__ int s_map[4 * NGL], s_face[4], s_side[4];
-  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, tid, BS);
+  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
   if (tid < 4) {
     s_face[tid] = m.efaces[e * 4 + tid];
     s_side[tid] = m.eside[e * 4 + tid];
   }
   for (int t = tid; t < 4 * NGL; t += BS) s_map[t] = m.efmap[e * 4 * NGL + t];
   for (int t = tid; t < L * P; t += BS) s_d[t / P][t % P] = dpp[(size_t)(t / P) * npoin + (size_t)e * P + t % P];
-  __syncthreads();
-  for (int t = tid; t < NQ * NGL; t += BS) {
-    int iq = t / NGL, mm = t % NGL;
-    for (int k = 0; k < L; k++) {
-      double acc = 0.0;
-      for (int n = 0; n < NGL; n++) acc += s_psiq[n * NQ + iq] * s_d[k][mm * NGL + n];
-      s_T[k][t] = acc;
-    }
+  for (int t = tid; t < 5 * Q; t += BS) {
+    const int c = t / Q;
+    s_qm[c][t % Q] = m.qstat[(c < 4 ? QS_EX + c : QS_W) * (size_t)npq + (size_t)e * Q + t % Q];
   }
   __syncthreads();
   for (int q = tid; q < Q; q += BS) {
     const int iq = q % NQ, jq = q / NQ;
     const size_t Iq = (size_t)e * Q + q;
-    double wq = m.qstat[QS_W * (size_t)npq + Iq];
-    double ex = m.qstat[QS_EX * (size_t)npq + Iq], ey = m.qstat[QS_EY * (size_t)npq + Iq];
-    double nx = m.qstat[QS_NX * (size_t)npq + Iq], ny = m.qstat[QS_NY * (size_t)npq + Iq];
     double pb = m.qstat[QS_PB * (size_t)npq + Iq];
     double dx = qacc[QA_MFX * (size_t)npq + Iq] - slmf[0 * (size_t)npq + Iq];
     double dy = qacc[QA_MFY * (size_t)npq + Iq] - slmf[1 * (size_t)npq + Iq];
     for (int k = 0; k < L; k++) {
       double dp = 0.0;
-      for (int mm = 0; mm < NGL; mm++) dp += s_psiq[mm * NQ + jq] * s_T[k][iq * NGL + mm];
+      for (int mm = 0; mm < NGL; mm++)
+        for (int n = 0; n < NGL; n++) dp = dp + PSIH(n, mm, iq, jq) * s_d[k][mm * NGL + n];
       double weight = dp / pb;
-      double udp = weight * dx, vdp = weight * dy;
-      s_G[k][0][q] = wq * (ex * udp + ey * vdp);
-      s_G[k][1][q] = wq * (nx * udp + ny * vdp);
+      s_f[k][0][q] = weight * dx;
+      s_f[k][1][q] = weight * dy;
     }
   }
   __syncthreads();
-  for (int t = tid; t < NQ * NGL; t += BS) {
-    int iq = t / NGL, mm = t % NGL;
-    for (int k = 0; k < L; k++) {
-      double ax = 0, ap = 0;
-      for (int jq = 0; jq < NQ; jq++) {
-        ax += s_psiq[mm * NQ + jq] * s_G[k][0][jq * NQ + iq];
-        ap += s_dpsiq[mm * NQ + jq] * s_G[k][1][jq * NQ + iq];
-      }
-      s_A[k][0][t] = ax;
-      s_A[k][1][t] = ap;
-    }
+  for (int t = tid; t < L * P; t += BS) {
+    const int k = t / P, p = t % P, i = p % NGL, j = p / NGL;
+    double acc = weak_div<NGL, NQ>(s_psiq, s_dpsiq, s_qm[0], s_qm[1], s_qm[2], s_qm[3], s_qm[4], s_f[k][0], s_f[k][1],
+                                   i, j, 0.0);
+    acc = face_terms<NGL, NQ>(s_psiq, s_map, s_face, s_side, m.fstat + FS_W * (size_t)F * NQ,
+                              fcons + (size_t)k * F * NQ, 0, p, acc);
+    const size_t I = (size_t)e * P + p;
+    double v = q[((size_t)k * npoin + I) * 3] + m.dt * m.nstat[NS_MINV * (size_t)npoin + I] * acc;
+    q[((size_t)k * npoin + I) * 3] = v;
+    s_new[k][p] = v;
   }
+  if (!finalize_dp) return;
   __syncthreads();
   for (int p = tid; p < P; p += BS) {
-    const int i = p % NGL, j = p / NGL;
     const size_t I = (size_t)e * P + p;
-    const double mi = m.nstat[NS_MINV * (size_t)npoin + I];
     double sum = 0.0;
-    for (int k = 0; k < L; k++) {
-      double r = 0.0;
-      for (int iq = 0; iq < NQ; iq++) r += s_dpsiq[i * NQ + iq] * s_A[k][0][iq * NGL + j] + s_psiq[i * NQ + iq] * s_A[k][1][iq * NGL + j];
-      r += gather_anti<NGL>(s_map, s_face, s_side, fcons + (size_t)k * F * NGL, F, p);
-      double v = q[((size_t)k * npoin + I) * 3] + m.dt * mi * r;
-      q[((size_t)k * npoin + I) * 3] = v;
-      s_new[k][p] = v;
-      sum = sum + v;
-    }
-    if (finalize_dp) {
-      double ope = sum / m.nstat[NS_PB * (size_t)npoin + I];
-      for (int k = 0; k < L; k++) qp_out[((size_t)k * npoin + I) * 3] = s_new[k][p] / ope;
-    }
+    for (int k = 0; k < L; k++) sum = sum + s_new[k][p];
+    double ope = sum / m.nstat[NS_PB * (size_t)npoin + I];
+    for (int k = 0; k < L; k++) qp_out[((size_t)k * npoin + I) * 3] = s_new[k][p] / ope;
   }
 }
 
 // ========================================== layer momentum: face kernel
 // Apply_layers_fluxes (mod_create_rhs_mlswe.F90:458-820) and the layer LDG flux
 // bcl_create_rhs_laplacian_flux (mod_laplacian_quad.F90:521-611).  Outputs per face
-// node: momL/momR[k][2][F][NGL] (advection+pressure, to left / right element) and
-// lap[k][2][F][NGL] (LDG, antisymmetric, value for the left element).
+// face quad point: momL/momR[k][2][F*NQ] = (nx*H_face + flux_x, ny*H_face + flux_y) of the
+// left / right side (the element kernels apply -/+ (wq*hi)*value in reference order), and
+// per face node lap[k][2][F*NGL] = wq*psi(n,n)*flux (LDG; + for left, - for right).
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(64)
     mom_flux_face_kernel(DevMesh m, const double *qf, const double *facc, const double *gdpp_face,
                          const double *gfacc, double *momL, double *momR, double *lap) {
   const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L;
-  __shared__ double s_psiq[NGL * NQ];
-  __shared__ double s_cl[MAXL][2][NQ], s_cr[MAXL][2][NQ];
+  __shared__ double s_psiq[NGL * NQ], s_psi[NGL * NGL];
   for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
+  for (int t = tid; t < NGL * NGL; t += 64) s_psi[t] = m.basis[2 * NGL * NQ + NGL * NGL + t];
   __syncthreads();
   const size_t FQ = (size_t)F * NQ, FN = (size_t)F * NGL;
   const int er = m.fer[f];
@@ -568,7 +538,7 @@ __global__ void __launch_bounds__(64)
     const int iq = tid;
     const size_t fq = (size_t)f * NQ + iq;
     const double *alpha = m.alpha;
-    double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq], wq = m.fstat[FS_W * FQ + fq];
+    double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
     double qbl0 = facc[FA_OPEL * FQ + fq], qbr0 = facc[FA_OPER * FQ + fq];
     double qbl1 = facc[FA_UL * FQ + fq], qbr1 = facc[FA_UR * FQ + fq];
     double qbl2 = facc[FA_VL * FQ + fq], qbr2 = facc[FA_VR * FQ + fq];
@@ -709,12 +679,13 @@ __global__ void __launch_bounds__(64)
       for (int k = 0; k < L; k++) Hf[sd][k] = Hf[sd][k] * weight;
     }
     for (int k = 0; k < L; k++) {
+      double hlx = nxl * Hf[0][k], hrx = nxl * Hf[1][k], hly = nyl * Hf[0][k], hry = nyl * Hf[1][k];
       double flux_x = nxl * udpf[0][k] + nyl * udpf[1][k];
       double flux_y = nxl * vdpf[0][k] + nyl * vdpf[1][k];
-      s_cl[k][0][iq] = -wq * (nxl * Hf[0][k] + flux_x);
-      s_cl[k][1][iq] = -wq * (nyl * Hf[0][k] + flux_y);
-      s_cr[k][0][iq] = wq * (nxl * Hf[1][k] + flux_x);
-      s_cr[k][1][iq] = wq * (nyl * Hf[1][k] + flux_y);
+      momL[((size_t)k * 2 + 0) * FQ + fq] = hlx + flux_x;
+      momL[((size_t)k * 2 + 1) * FQ + fq] = hly + flux_y;
+      momR[((size_t)k * 2 + 0) * FQ + fq] = hrx + flux_x;
+      momR[((size_t)k * 2 + 1) * FQ + fq] = hry + flux_y;
     }
   } else if (tid >= 32 && tid < 32 + NGL) {
     // layer LDG flux at face node n for every layer
@@ -734,29 +705,20 @@ __global__ void __launch_bounds__(64)
       double qvm0 = alpha * fl[2] + beta * fr[2], qvm1 = alpha * fl[3] + beta * fr[3];
       double flux_qu = (qum0 - fl[0] * nx) + (qum1 - fl[1] * ny);
       double flux_qv = (qvm0 - fl[2] * nx) + (qvm1 - fl[3] * ny);
-      lap[(((size_t)k * 2 + 0) * F + f) * NGL + n] = wq * flux_qu;
-      lap[(((size_t)k * 2 + 1) * F + f) * NGL + n] = wq * flux_qv;
+      double h1 = s_psi[n * NGL + n];
+      lap[((size_t)k * 2 + 0) * FN + fn] = wq * h1 * flux_qu;
+      lap[((size_t)k * 2 + 1) * FN + fn] = wq * h1 * flux_qv;
     }
-  }
-  __syncthreads();
-  if (tid < 2 * L * NGL) {
-    const int k = tid / (2 * NGL), c = (tid / NGL) % 2, n = tid % NGL;
-    double sl = 0.0, sr = 0.0;
-    for (int iq = 0; iq < NQ; iq++) {
-      double hi = s_psiq[n * NQ + iq];
-      sl += hi * s_cl[k][c][iq];
-      sr += hi * s_cr[k][c][iq];
-    }
-    momL[(((size_t)k * 2 + c) * F + f) * NGL + n] = sl;
-    momR[(((size_t)k * 2 + c) * F + f) * NGL + n] = sr;
   }
 }
 
 // ===================================== layer momentum: element volume + update
-// create_rhs_dynamics_volume_layers + bcl LDG volume + face gathers; then
-// momentum update with implicit Coriolis, layer_mom_boundary_df and evaluate_bcl(_v1).
-// mode: 0 = momentum_mass (evaluate_bcl: also qprime(1) = q(1)/(sum q(1)/pb')),
-//       1 = momentum (evaluate_bcl_v1).
+// rhs_momentum (mod_splitting.F90:289-322): bcl_create_laplacian (mod_laplacian_quad.F90:
+// 227-248, :392-425, :521-611) and layer_momentum_rhs = create_rhs_dynamics_volume_layers
+// (mod_create_rhs_mlswe.F90:281-456) + Apply_layers_fluxes (:778-817), then the momentum
+// update with implicit Coriolis (mod_splitting.F90:131-173 / :239-280), layer_mom_boundary_df
+// (mod_layer_terms.F90:529-584) and evaluate_bcl (mode 0, :198-238) / evaluate_bcl_v1
+// (mode 1, :240-270).
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     mom_elem_kernel(DevMesh m, const double *qp_in, const double *qacc, const double *nacc, const double *dpp_graduv,
@@ -765,16 +727,16 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
   constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BS;
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
   const double g = m.gravity, eps1 = 1.0e-20;
-  __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL];
-  __shared__ double s_qp[MAXL][3][P], s_qm[MAXL][2][P], s_z[MAXL + 1][P];
-  __shared__ double s_T[MAXL * 5][NQ * NGL];
-  __shared__ double s_Tz[2][MAXL + 1][NQ * NGL];
-  __shared__ double s_G[MAXL][6][Q];
-  __shared__ double s_A[MAXL][4][NQ * NGL];
-  __shared__ double s_lg[MAXL][4][P];
+  __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
+  __shared__ double s_qp[MAXL][3][P], s_qm2[MAXL][2][P], s_z[MAXL + 1][P];
+  __shared__ double s_qm[5][Q];            // e_x, e_y, n_x, n_y, w at quad points
+  __shared__ double s_nm[5][P];            // e_x, e_y, n_x, n_y, w at nodes
+  __shared__ double s_G[MAXL][6][Q];       // source_x, Hq+uu, uv, source_y, vu, Hq+vv
+  __shared__ double s_qq[MAXL][4][P];      // LDG volume fluxes per layer
+  __shared__ double s_r[MAXL][4][P];       // rhs_mom(2) and lap(2) per layer
   __shared__ double s_new[MAXL][3][P];
   __shared__ int s_map[4 * NGL], s_face[4], s_side[4], s_bc[4];
-  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, tid, BS);
+  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
   if (tid < 4) {
     s_face[tid] = m.efaces[e * 4 + tid];
     s_side[tid] = m.eside[e * 4 + tid];
@@ -784,10 +746,19 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
   for (int t = tid; t < L * 3 * P; t += BS) {
     int k = t / (3 * P), r = t % (3 * P);
     s_qp[k][r % 3][r / 3] = qp_in[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
-    if (r % 3) s_qm[k][r % 3 - 1][r / 3] = q[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
+    if (r % 3) s_qm2[k][r % 3 - 1][r / 3] = q[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
+  }
+  for (int t = tid; t < 5 * Q; t += BS) {
+    const int c = t / Q;
+    s_qm[c][t % Q] = m.qstat[(c < 4 ? QS_EX + c : QS_W) * (size_t)npq + (size_t)e * Q + t % Q];
+  }
+  for (int t = tid; t < 5 * P; t += BS) {
+    const int c = t / P;
+    s_nm[c][t % P] = m.nstat[(c < 4 ? NS_EX + c : NS_W) * (size_t)npoin + (size_t)e * P + t % P];
   }
   __syncthreads();
-  // layer interfaces at nodes (mod_create_rhs_mlswe.F90:320-325)
+  // layer interfaces at nodes (mod_create_rhs_mlswe.F90:320-325) and LDG volume fluxes
+  // qq = dpprime_visc*graduvb_ave + dpp_graduv (mod_laplacian_quad.F90:409-413)
   for (int p = tid; p < P; p += BS) {
     const size_t I = (size_t)e * P + p;
     double z = m.nstat[NS_ZB * (size_t)npoin + I];
@@ -797,47 +768,10 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
       z = z + (m.alpha[k] / g) * (so * s_qp[k][0][p]);
       s_z[k][p] = z;
     }
-  }
-  __syncthreads();
-  for (int t = tid; t < NQ * NGL; t += BS) {
-    int iq = t / NGL, mm = t % NGL;
-    for (int k = 0; k < L; k++) {
-      for (int v = 0; v < 3; v++) {
-        double acc = 0.0;
-        for (int n = 0; n < NGL; n++) acc += s_psiq[n * NQ + iq] * s_qp[k][v][mm * NGL + n];
-        s_T[k * 5 + v][t] = acc;
-      }
-      for (int v = 0; v < 2; v++) {
-        double acc = 0.0;
-        for (int n = 0; n < NGL; n++) acc += s_psiq[n * NQ + iq] * s_qm[k][v][mm * NGL + n];
-        s_T[k * 5 + 3 + v][t] = acc;
-      }
-    }
-    for (int k = 0; k <= L; k++) {
-      double ap = 0.0, ad = 0.0;
-      for (int n = 0; n < NGL; n++) {
-        ap += s_psiq[n * NQ + iq] * s_z[k][mm * NGL + n];
-        ad += s_dpsiq[n * NQ + iq] * s_z[k][mm * NGL + n];
-      }
-      s_Tz[0][k][t] = ap;
-      s_Tz[1][k][t] = ad;
-    }
-  }
-  // bcl LDG volume fluxes at nodes (bcl_compute_laplacian, mod_laplacian_quad.F90:392-425)
-  for (int p = tid; p < P; p += BS) {
-    const size_t I = (size_t)e * P + p;
-    double w_ = m.nstat[NS_W * (size_t)npoin + I];
-    double ex = m.nstat[NS_EX * (size_t)npoin + I], ey = m.nstat[NS_EY * (size_t)npoin + I];
-    double nx = m.nstat[NS_NX * (size_t)npoin + I], ny = m.nstat[NS_NY * (size_t)npoin + I];
     for (int k = 0; k < L; k++) {
       double d = dpprime_visc[(size_t)k * npoin + I];
-      double qq[4];
       for (int c = 0; c < 4; c++)
-        qq[c] = d * nacc[(NA_G1 + c) * (size_t)npoin + I] + dpp_graduv[((size_t)k * 4 + c) * npoin + I];
-      s_lg[k][0][p] = w_ * (ex * qq[0] + ey * qq[1]);
-      s_lg[k][1][p] = w_ * (nx * qq[0] + ny * qq[1]);
-      s_lg[k][2][p] = w_ * (ex * qq[2] + ey * qq[3]);
-      s_lg[k][3][p] = w_ * (nx * qq[2] + ny * qq[3]);
+        s_qq[k][c][p] = d * nacc[(NA_G1 + c) * (size_t)npoin + I] + dpp_graduv[((size_t)k * 4 + c) * npoin + I];
     }
   }
   __syncthreads();
@@ -852,37 +786,44 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
            qb2 = qacc[QA_VB * (size_t)npq + Iq];
     double so2 = sqrt(qacc[QA_OPE2 * (size_t)npq + Iq]);
     p_tmp[0] = 0.0;
+    for (int k = 0; k < L; k++) tuu[k] = tvv[k] = 0.0;
     for (int k = 0; k < L; k++) {
-      double vv[5];
-      for (int v = 0; v < 5; v++) {
-        double acc = 0.0;
-        for (int mm = 0; mm < NGL; mm++) acc += s_psiq[mm * NQ + jq] * s_T[k * 5 + v][iq * NGL + mm];
-        vv[v] = acc;
-      }
-      qpv[k][0] = vv[0];
-      qpv[k][1] = vv[1];
-      qpv[k][2] = vv[2];
-      p_tmp[k + 1] = p_tmp[k] + so2 * vv[0];
+      double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+      for (int mm = 0; mm < NGL; mm++)
+        for (int n = 0; n < NGL; n++) {
+          const int ip = mm * NGL + n;
+          const double hi = PSIH(n, mm, iq, jq);
+          v0 = v0 + hi * s_qp[k][0][ip];
+          v1 = v1 + hi * s_qp[k][1][ip];
+          v2 = v2 + hi * s_qp[k][2][ip];
+          tuu[k] = tuu[k] + hi * s_qm2[k][0][ip];
+          tvv[k] = tvv[k] + hi * s_qm2[k][1][ip];
+        }
+      qpv[k][0] = v0;
+      qpv[k][1] = v1;
+      qpv[k][2] = v2;
+      p_tmp[k + 1] = p_tmp[k] + so2 * v0;
       H_tmp[k] = 0.5 * m.alpha[k] * (p_tmp[k + 1] * p_tmp[k + 1] - p_tmp[k] * p_tmp[k]);
-      double dp = vv[0] * qb0, u = vv[1] + qb1, v = vv[2] + qb2;
+      double dp = v0 * qb0, u = v1 + qb1, v = v2 + qb2;
       u_udp[k] = dp * u * u;
       v_vdp[k] = dp * v * v;
       u_vdp[0][k] = u * v * dp;
       u_vdp[1][k] = v * u * dp;
-      tuu[k] = fabs(vv[3]) + eps1;
-      tvv[k] = fabs(vv[4]) + eps1;
+      tuu[k] = fabs(tuu[k]) + eps1;
+      tvv[k] = fabs(tvv[k]) + eps1;
     }
-    double ex = m.qstat[QS_EX * (size_t)npq + Iq], ey = m.qstat[QS_EY * (size_t)npq + Iq];
-    double nx = m.qstat[QS_NX * (size_t)npq + Iq], ny = m.qstat[QS_NY * (size_t)npq + Iq];
-    for (int k = 0; k <= L; k++) {
-      double dzx = 0.0, dzy = 0.0;  // d/dxi, d/deta at the quad point
-      for (int mm = 0; mm < NGL; mm++) {
-        dzx += s_psiq[mm * NQ + jq] * s_Tz[1][k][iq * NGL + mm];
-        dzy += s_dpsiq[mm * NQ + jq] * s_Tz[0][k][iq * NGL + mm];
+    for (int k = 0; k <= L; k++) gz[0][k] = gz[1][k] = 0.0;
+    for (int mm = 0; mm < NGL; mm++)
+      for (int n = 0; n < NGL; n++) {
+        const int ip = mm * NGL + n;
+        const double h_e = HE(n, mm, iq, jq), h_n = HN(n, mm, iq, jq);
+        const double dx = h_e * s_qm[0][q] + h_n * s_qm[2][q];
+        const double dy = h_e * s_qm[1][q] + h_n * s_qm[3][q];
+        for (int k = 0; k <= L; k++) {
+          gz[0][k] = gz[0][k] + dx * s_z[k][ip];
+          gz[1][k] = gz[1][k] + dy * s_z[k][ip];
+        }
       }
-      gz[0][k] = ex * dzx + nx * dzy;
-      gz[1][k] = ey * dzx + ny * dzy;
-    }
     double su = 0, suv = 0, sv = 0, stu = 0, stv = 0, sH = 0;
     for (int k = 0; k < L; k++) su = su + u_udp[k];
     for (int k = 0; k < L; k++) suv = suv + u_vdp[0][k];
@@ -894,7 +835,6 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     for (int k = 0; k < L; k++) stv = stv + tvv[k];
     for (int k = 0; k < L; k++) sH = sH + H_tmp[k];
     double oosu = 1.0 / stu, oosv = 1.0 / stv;
-    double wq = m.qstat[QS_W * (size_t)npq + Iq];
     double weight = 1.0;
     if (sH > 0.0) weight = qacc[QA_H * (size_t)npq + Iq] / sH;
     double tw1 = m.qstat[QS_TW1 * (size_t)npq + Iq], tw2 = m.qstat[QS_TW2 * (size_t)npq + Iq];
@@ -912,73 +852,81 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
       v_vdp[k] = v_vdp[k] + wgt * vv_def;
       double Hq = H_tmp[k] * weight;
       double temp1 = (dmin(ppt1, Pstress) - dmin(ppt0, Pstress)) / Pstress;
-      double tempbot = (dmin(Pbstress, pb - ppt1) - dmin(Pbstress, pb - ppt0)) / Pbstress;
+      double tempbot = dmin(Pbstress, pb - ppt1) - dmin(Pbstress, pb - ppt0);
+      tempbot = tempbot / Pbstress;
       double sx = g * (temp1 * tw1 - tempbot * tb1 + p_tmp[k] * gz[0][k] - p_tmp[k + 1] * gz[0][k + 1]);
       double sy = g * (temp1 * tw2 - tempbot * tb2 + p_tmp[k] * gz[1][k] - p_tmp[k + 1] * gz[1][k + 1]);
-      double f1x = Hq + u_udp[k], f1y = u_vdp[0][k], f2x = u_vdp[1][k], f2y = Hq + v_vdp[k];
-      s_G[k][0][q] = wq * (ex * f1x + ey * f1y);
-      s_G[k][1][q] = wq * (nx * f1x + ny * f1y);
-      s_G[k][2][q] = wq * sx;
-      s_G[k][3][q] = wq * (ex * f2x + ey * f2y);
-      s_G[k][4][q] = wq * (nx * f2x + ny * f2y);
-      s_G[k][5][q] = wq * sy;
+      s_G[k][0][q] = sx;
+      s_G[k][1][q] = Hq + u_udp[k];
+      s_G[k][2][q] = u_vdp[0][k];
+      s_G[k][3][q] = sy;
+      s_G[k][4][q] = u_vdp[1][k];
+      s_G[k][5][q] = Hq + v_vdp[k];
       ppt0 = ppt1;
     }
   }
   __syncthreads();
-  for (int t = tid; t < NQ * NGL; t += BS) {
-    int iq = t / NGL, mm = t % NGL;
-    for (int k = 0; k < L; k++) {
-      double ax1 = 0, ap1 = 0, ax2 = 0, ap2 = 0;
-      for (int jq = 0; jq < NQ; jq++) {
-        double ps = s_psiq[mm * NQ + jq], dps = s_dpsiq[mm * NQ + jq];
-        int qq = jq * NQ + iq;
-        ax1 += ps * s_G[k][0][qq];
-        ap1 += dps * s_G[k][1][qq] + ps * s_G[k][2][qq];
-        ax2 += ps * s_G[k][3][qq];
-        ap2 += dps * s_G[k][4][qq] + ps * s_G[k][5][qq];
+  // weak forms, one thread per (layer, output, node), reference accumulation order
+  for (int t = tid; t < L * 4 * P; t += BS) {
+    const int k = t / (4 * P), o = (t / P) % 4, p = t % P, i = p % NGL, j = p / NGL;
+    double acc = 0.0;
+    if (o < 2) {
+      const double *G = s_G[k][3 * o];
+      for (int q = 0; q < Q; q++) {
+        const int iq = q % NQ, jq = q / NQ;
+        const double hi = PSIH(i, j, iq, jq);
+        const double h_e = HE(i, j, iq, jq), h_n = HN(i, j, iq, jq);
+        const double dhdx = h_e * s_qm[0][q] + h_n * s_qm[2][q];
+        const double dhdy = h_e * s_qm[1][q] + h_n * s_qm[3][q];
+        double term;
+        if (o == 0)
+          term = s_qm[4][q] * (hi * G[q] + dhdx * s_G[k][1][q] + s_G[k][2][q] * dhdy);
+        else
+          term = s_qm[4][q] * (hi * G[q] + s_G[k][4][q] * dhdx + dhdy * s_G[k][5][q]);
+        acc = acc + term;
       }
-      s_A[k][0][t] = ax1;
-      s_A[k][1][t] = ap1;
-      s_A[k][2][t] = ax2;
-      s_A[k][3][t] = ap2;
+      const double *fw = m.fstat + FS_W * (size_t)F * NQ;
+      for (int lf = 0; lf < 4; lf++)
+        for (int n = 0; n < NGL; n++) {
+          if (s_map[lf * NGL + n] != p) continue;
+          const size_t b = (size_t)s_face[lf] * NQ;
+          const bool left = s_side[lf] == 0;
+          const double *src = (left ? momL : momR) + ((size_t)k * 2 + o) * F * NQ;
+          for (int iq = 0; iq < NQ; iq++) {
+            const double c = fw[b + iq] * s_psiq[n * NQ + iq] * src[b + iq];
+            acc = left ? acc - c : acc + c;
+          }
+        }
+    } else {
+      const int c = o - 2;
+      for (int jj = 0; jj < NGL; jj++)
+        for (int ii = 0; ii < NGL; ii++) {
+          const int sn = jj * NGL + ii;
+          const double dx = HE_DF(i, j, ii, jj) * s_nm[0][sn] + HN_DF(i, j, ii, jj) * s_nm[2][sn];
+          const double dy = HE_DF(i, j, ii, jj) * s_nm[1][sn] + HN_DF(i, j, ii, jj) * s_nm[3][sn];
+          acc = acc - s_nm[4][sn] * (dx * s_qq[k][2 * c][sn] + dy * s_qq[k][2 * c + 1][sn]);
+        }
+      for (int lf = 0; lf < 4; lf++)
+        for (int n = 0; n < NGL; n++)
+          if (s_map[lf * NGL + n] == p) {
+            const double v = lapf[((size_t)k * 2 + c) * F * NGL + (size_t)s_face[lf] * NGL + n];
+            acc = s_side[lf] == 0 ? acc + v : acc - v;
+          }
     }
+    s_r[k][o][p] = acc;
   }
   __syncthreads();
-  // per node: rhs_mom, update, Coriolis
+  // per node: rhs_mom, update, implicit Coriolis
   for (int p = tid; p < P; p += BS) {
-    const int i = p % NGL, j = p / NGL;
     const size_t I = (size_t)e * P + p;
     const double mi = m.nstat[NS_MINV * (size_t)npoin + I];
     const double f2 = m.nstat[NS_F2 * (size_t)npoin + I], ab = m.nstat[NS_A * (size_t)npoin + I],
                  bb = m.nstat[NS_B * (size_t)npoin + I];
     for (int k = 0; k < L; k++) {
-      double r0 = 0.0, r1 = 0.0;
-      for (int iq = 0; iq < NQ; iq++) {
-        double dps = s_dpsiq[i * NQ + iq], ps = s_psiq[i * NQ + iq];
-        r0 += dps * s_A[k][0][iq * NGL + j] + ps * s_A[k][1][iq * NGL + j];
-        r1 += dps * s_A[k][2][iq * NGL + j] + ps * s_A[k][3][iq * NGL + j];
-      }
-      double l0 = 0.0, l1 = 0.0;
-      for (int kk = 0; kk < NGL; kk++) {
-        l0 -= s_dpsi[i * NGL + kk] * s_lg[k][0][j * NGL + kk] + s_dpsi[j * NGL + kk] * s_lg[k][1][kk * NGL + i];
-        l1 -= s_dpsi[i * NGL + kk] * s_lg[k][2][j * NGL + kk] + s_dpsi[j * NGL + kk] * s_lg[k][3][kk * NGL + i];
-      }
-      for (int lf = 0; lf < 4; lf++)
-        for (int n = 0; n < NGL; n++)
-          if (s_map[lf * NGL + n] == p) {
-            size_t b0 = (((size_t)k * 2 + 0) * F + s_face[lf]) * NGL + n;
-            size_t b1 = (((size_t)k * 2 + 1) * F + s_face[lf]) * NGL + n;
-            const double *src = s_side[lf] == 0 ? momL : momR;
-            r0 += src[b0];
-            r1 += src[b1];
-            double sg = s_side[lf] == 0 ? 1.0 : -1.0;
-            l0 += sg * lapf[b0];
-            l1 += sg * lapf[b1];
-          }
-      double rm0 = mi * r0 + m.visc * mi * l0;
-      double rm1 = mi * r1 + m.visc * mi * l1;
-      double q2 = s_qm[k][0][p], q3 = s_qm[k][1][p];
+      double v0 = m.visc * mi * s_r[k][2][p], v1 = m.visc * mi * s_r[k][3][p];
+      double rm0 = mi * s_r[k][0][p] + v0;
+      double rm1 = mi * s_r[k][1][p] + v1;
+      double q2 = s_qm2[k][0][p], q3 = s_qm2[k][1][p];
       double t1 = q2 + m.dt * rm0, t2 = q3 + m.dt * rm1;
       double tu = t1 + f2 * q3, tv = t2 - f2 * q2;
       s_new[k][1][p] = ab * tu + bb * tv;
@@ -1009,7 +957,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     }
     __syncthreads();
   }
-  // evaluate_bcl / evaluate_bcl_v1 with extract_velocity, per node
+  // evaluate_bcl / evaluate_bcl_v1 with extract_velocity (mod_layer_terms.F90:272-320), per node
   for (int p = tid; p < P; p += BS) {
     const size_t I = (size_t)e * P + p;
     const double b1 = qb[I * 4], b3 = qb[I * 4 + 2], b4 = qb[I * 4 + 3];

@@ -47,26 +47,6 @@ struct Sizes {
   static constexpr int BS = ((Q + 63) / 64) * 64;
 };
 
-// nodal gradient of (u, v) on one element (compute_gradient_uv, mod_barotropic_terms.F90:411-443)
-// g[0..3] = (du/dx, du/dy, dv/dx, dv/dy) at node p = j*NGL + i
-template <int NGL>
-__device__ __forceinline__ void nodal_grad(const double *s_dpsi, const double *u, const double *v, int i, int j,
-                                           double ex, double ey, double nx, double ny, double g[4]) {
-  double ux = 0.0, uy = 0.0, vx = 0.0, vy = 0.0;
-#pragma unroll
-  for (int n = 0; n < NGL; n++) {
-    double dx = s_dpsi[n * NGL + i], dy = s_dpsi[n * NGL + j];
-    ux += dx * u[j * NGL + n];
-    vx += dx * v[j * NGL + n];
-    uy += dy * u[n * NGL + i];
-    vy += dy * v[n * NGL + i];
-  }
-  g[0] = ex * ux + nx * uy;
-  g[1] = ey * ux + ny * uy;
-  g[2] = ex * vx + nx * vy;
-  g[3] = ey * vx + ny * vy;
-}
-
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64) btp_stage_kernel(StageArgs a) {
   constexpr int P = Sizes<NGL, NQ>::P, Q = Sizes<NGL, NQ>::Q, BS = Sizes<NGL, NQ>::BS;
@@ -74,14 +54,16 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64) btp_stage_kernel(S
   const int e = blockIdx.x, tid = threadIdx.x;
   const int npoin = m.npoin, npq = m.npoin_q, F = m.nface;
 
-  __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL];
+  __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
   __shared__ double s_qb[4][P], s_qp[3][P], s_uv[2][P];
-  __shared__ double s_T[7][NQ * NGL];       // x-interpolated: [v][iq*NGL + m]
-  __shared__ double s_G[8][Q];              // weighted contravariant fluxes at quad points
-  __shared__ double s_A[6][NQ * NGL];       // jq-contracted: [iq*NGL + m]
-  __shared__ double s_grad[4][P], s_lg[4][P];
+  __shared__ double s_qm[4][Q];             // per quad point: e_x, e_y, n_x, n_y
+  __shared__ double s_qv[8][Q];             // wq, udp, vdp, sc_x, sc_y, Hq+qu, quv, Hq+qv
+  __shared__ double s_nm[5][P];             // nodal e_x, e_y, n_x, n_y, w
+  __shared__ double s_grad[4][P], s_qq[4][P];
   __shared__ double s_nb[4][4][NGL], s_ng[4][4][NGL];  // neighbour qb / grad traces per local face
-  __shared__ double s_fq[4][NQ][3], s_fl[4][NGL][2];
+  __shared__ double s_fq[4][NQ][4];         // face: wq, flux, H_kx+flux_x, H_ky+flux_y
+  __shared__ double s_fl[4][NGL][2];        // LDG face: signed wq*flux_qu, wq*flux_qv
+  __shared__ double s_rhs[3][P], s_lap[2][P];
   __shared__ double s_qn[4][P];
   __shared__ int s_map[4][NGL], s_face[4], s_side[4], s_bc[4], s_nbe[4], s_nblf[4];
 
@@ -90,7 +72,10 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64) btp_stage_kernel(S
     s_psiq[t] = m.basis[t];
     s_dpsiq[t] = m.basis[NGL * NQ + t];
   }
-  for (int t = tid; t < NGL * NGL; t += BS) s_dpsi[t] = m.basis[2 * NGL * NQ + t];
+  for (int t = tid; t < NGL * NGL; t += BS) {
+    s_dpsi[t] = m.basis[2 * NGL * NQ + t];
+    s_psi[t] = m.basis[2 * NGL * NQ + NGL * NGL + t];
+  }
   if (tid < 4) {
     s_face[tid] = m.efaces[e * 4 + tid];
     s_side[tid] = m.eside[e * 4 + tid];
@@ -103,6 +88,14 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64) btp_stage_kernel(S
   if (m.botfr) {
     const double *qpL = a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P;
     for (int t = tid; t < 3 * P; t += BS) s_qp[t % 3][t / 3] = qpL[t];
+  }
+  for (int t = tid; t < 4 * Q; t += BS) {
+    const int c = t / Q, q = t % Q;
+    s_qm[c][q] = m.qstat[(QS_EX + c) * (size_t)npq + (size_t)e * Q + q];
+  }
+  for (int t = tid; t < 5 * P; t += BS) {
+    const int c = t / P, p = t % P;
+    s_nm[c][p] = m.nstat[(c < 4 ? NS_EX + c : NS_W) * (size_t)npoin + (size_t)e * P + p];
   }
   __syncthreads();
   // neighbour traces (interior faces)
@@ -117,11 +110,10 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64) btp_stage_kernel(S
     s_nb[lf][c][n] = vq;
     s_ng[lf][c][n] = vg;
   }
-  // ---------------------------------------------------------------- phase 1
-  // nodal stage-start terms (mod_rk_mlswe.F90:90-92) and x-interpolation
+  // nodal stage-start terms (mod_rk_mlswe.F90:90-92)
   for (int p = tid; p < P; p += BS) {
     double q1 = s_qb[0][p], q2 = s_qb[1][p], q3 = s_qb[2][p], q4 = s_qb[3][p];
-    s_uv[0][p] = q3 / q1;
+    s_uv[0][p] = q3 / q1;  // Uk (mod_laplacian_quad.F90:48-49)
     s_uv[1][p] = q4 / q1;
     if (a.accumulate) {
       size_t I = (size_t)e * P + p;
@@ -131,46 +123,39 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64) btp_stage_kernel(S
       a.nacc[NA_VB * (size_t)npoin + I] += q4 / q1;
     }
   }
-  {
-    const int nv = m.botfr ? 7 : 4;
-    for (int t = tid; t < NQ * NGL; t += BS) {
-      int iq = t / NGL, mm = t % NGL;
-      for (int v = 0; v < nv; v++) {
-        const double *src = v < 4 ? s_qb[v] : s_qp[v - 4];
-        double acc = 0.0;
-#pragma unroll
-        for (int n = 0; n < NGL; n++) acc += s_psiq[n * NQ + iq] * src[mm * NGL + n];
-        s_T[v][t] = acc;
-      }
-    }
-  }
   __syncthreads();
-  // ---------------------------------------------------------------- phase 2
-  // quad-point physics (mod_rhs_btp.F90:136-192) on threads [0,Q);
-  // nodal gradient of u_bar (mod_laplacian_quad.F90:48-54) on the following threads
+  // ---------------------------------------------------------------- phase 1
+  // (a) quad-point physics (mod_rhs_btp.F90:136-192), one thread per quad point;
+  // (b) nodal gradient of u_bar (compute_gradient_uv), one thread per (node, component)
   for (int q = tid; q < Q; q += BS) {
     const int iq = q % NQ, jq = q / NQ;
-    double val[7];
-    const int nv = m.botfr ? 7 : 4;
-    for (int v = 0; v < nv; v++) {
-      double acc = 0.0;
-#pragma unroll
-      for (int mm = 0; mm < NGL; mm++) acc += s_psiq[mm * NQ + jq] * s_T[v][iq * NGL + mm];
-      val[v] = acc;
-    }
+    double dp = 0, dpp = 0, udp = 0, vdp = 0, pp = 0, up = 0, vp = 0;
+    for (int mm = 0; mm < NGL; mm++)
+      for (int n = 0; n < NGL; n++) {
+        const int ip = mm * NGL + n;
+        const double hi = PSIH(n, mm, iq, jq);
+        dp = dp + hi * s_qb[0][ip];
+        dpp = dpp + hi * s_qb[1][ip];
+        udp = udp + hi * s_qb[2][ip];
+        vdp = vdp + hi * s_qb[3][ip];
+        if (m.botfr) {
+          pp = pp + hi * s_qp[0][ip];
+          up = up + hi * s_qp[1][ip];
+          vp = vp + hi * s_qp[2][ip];
+        }
+      }
     const size_t Iq = (size_t)e * Q + q;
     const double *QS = m.qstat;
-    double dp = val[0], dpp = val[1], udp = val[2], vdp = val[3];
     double wq = QS[QS_W * (size_t)npq + Iq];
     double ub = udp / dp, vb = vdp / dp;
     double tb_u = 0.0, tb_v = 0.0;
     if (m.botfr == 1) {
-      double ubot = val[5] + ub, vbot = val[6] + vb;
-      double spd = (m.cd / m.gravity) * val[4];
+      double ubot = up + ub, vbot = vp + vb;
+      double spd = (m.cd / m.gravity) * pp;
       tb_u = spd * ubot;
       tb_v = spd * vbot;
     } else if (m.botfr == 2) {
-      double ubot = val[5] + ub, vbot = val[6] + vb;
+      double ubot = up + ub, vbot = vp + vb;
       double spd = (m.cd / m.alpha[m.L - 1]) * sqrt(ubot * ubot + vbot * vbot);
       tb_u = spd * ubot;
       tb_v = spd * vbot;
@@ -199,55 +184,39 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64) btp_stage_kernel(S
       A[QA_UB * (size_t)npq + Iq] += ub;
       A[QA_VB * (size_t)npq + Iq] += vb;
     }
-    double ex = QS[QS_EX * (size_t)npq + Iq], ey = QS[QS_EY * (size_t)npq + Iq];
-    double nx = QS[QS_NX * (size_t)npq + Iq], ny = QS[QS_NY * (size_t)npq + Iq];
-    double f2x = Hq + qu, f2y = quv, f3x = quv, f3y = Hq + qv;
-    s_G[0][q] = wq * (ex * udp + ey * vdp);
-    s_G[1][q] = wq * (nx * udp + ny * vdp);
-    s_G[2][q] = wq * (ex * f2x + ey * f2y);
-    s_G[3][q] = wq * (nx * f2x + ny * f2y);
-    s_G[4][q] = wq * sc_x;
-    s_G[5][q] = wq * (ex * f3x + ey * f3y);
-    s_G[6][q] = wq * (nx * f3x + ny * f3y);
-    s_G[7][q] = wq * sc_y;
+    s_qv[0][q] = wq;
+    s_qv[1][q] = udp;
+    s_qv[2][q] = vdp;
+    s_qv[3][q] = sc_x;
+    s_qv[4][q] = sc_y;
+    s_qv[5][q] = Hq + qu;
+    s_qv[6][q] = quv;
+    s_qv[7][q] = Hq + qv;
   }
-  for (int p = (tid + BS - Q % BS) % BS; p < P; p += BS) {
-    const int i = p % NGL, j = p / NGL;
-    const size_t I = (size_t)e * P + p;
-    const double *NS = m.nstat;
-    double g4[4];
-    nodal_grad<NGL>(s_dpsi, s_uv[0], s_uv[1], i, j, NS[NS_EX * (size_t)npoin + I], NS[NS_EY * (size_t)npoin + I],
-                    NS[NS_NX * (size_t)npoin + I], NS[NS_NY * (size_t)npoin + I], g4);
-    for (int c = 0; c < 4; c++) {
-      s_grad[c][p] = g4[c];
-      if (a.accumulate) a.nacc[(NA_G1 + c) * (size_t)npoin + I] += g4[c];
-    }
+  for (int t = (tid + BS - Q % BS) % BS; t < 4 * P; t += BS) {
+    // grad(c, p) = sum_ip dpsidx_df(ip,p) * u(ip)  (mod_barotropic_terms.F90:427-441)
+    const int c = t / P, p = t % P, i = p % NGL, j = p / NGL;
+    const double *u = s_uv[c >> 1];
+    const double ex = s_nm[(c & 1) ? 1 : 0][p], nx = s_nm[(c & 1) ? 3 : 2][p];
+    double gsum = 0.0;
+    for (int mm = 0; mm < NGL; mm++)
+      for (int n = 0; n < NGL; n++) {
+        const double d = HE_DF(n, mm, i, j) * ex + HN_DF(n, mm, i, j) * nx;
+        gsum = gsum + d * u[mm * NGL + n];
+      }
+    s_grad[c][p] = gsum;
+    if (a.accumulate) a.nacc[(NA_G1 + c) * (size_t)npoin + (size_t)e * P + p] += gsum;
   }
   __syncthreads();
-  // ---------------------------------------------------------------- phase 3
-  // (a) jq-contraction of the weighted fluxes, (b) btp face fluxes at face quad points,
-  // (c) LDG fluxes at face nodes, (d) LDG volume fluxes at nodes
+  // ---------------------------------------------------------------- phase 2
+  // (a) btp face fluxes at face quad points, (b) LDG fluxes at face nodes,
+  // (c) LDG volume fluxes qq at nodes (btp_compute_laplacian, mod_laplacian_quad.F90:374-380)
   {
-    constexpr int W1 = NQ * NGL, W2 = 4 * NQ, W3 = 4 * NGL, W4 = P;
-    for (int w = tid; w < W1 + W2 + W3 + W4; w += BS) {
-      if (w < W1) {
-        const int iq = w / NGL, mm = w % NGL;
-        double ax1 = 0, ap1 = 0, ax2 = 0, ap2 = 0, ax3 = 0, ap3 = 0;
-#pragma unroll
-        for (int jq = 0; jq < NQ; jq++) {
-          double ps = s_psiq[mm * NQ + jq], dps = s_dpsiq[mm * NQ + jq];
-          int q = jq * NQ + iq;
-          ax1 += ps * s_G[0][q];
-          ap1 += dps * s_G[1][q];
-          ax2 += ps * s_G[2][q];
-          ap2 += dps * s_G[3][q] + ps * s_G[4][q];
-          ax3 += ps * s_G[5][q];
-          ap3 += dps * s_G[6][q] + ps * s_G[7][q];
-        }
-        s_A[0][w] = ax1; s_A[1][w] = ap1; s_A[2][w] = ax2; s_A[3][w] = ap2; s_A[4][w] = ax3; s_A[5][w] = ap3;
-      } else if (w < W1 + W2) {
-        // ---- creat_btp_fluxes_qdf at (face lf, quad iq) (mod_rhs_btp.F90:246-362)
-        const int t = w - W1, lf = t / NQ, iq = t % NQ;
+    constexpr int W2 = 4 * NQ, W3 = 4 * NGL, W4 = P;
+    for (int w = tid; w < W2 + W3 + W4; w += BS) {
+      if (w < W2) {
+        // ---- creat_btp_fluxes_qdf at (face lf, quad iq) (mod_rhs_btp.F90:246-337)
+        const int lf = w / NQ, iq = w % NQ;
         const int f = s_face[lf], side = s_side[lf], er = s_bc[lf];
         double ql[4] = {0, 0, 0, 0}, qr[4] = {0, 0, 0, 0}, pbl = 0.0, pbr = 0.0;
         for (int n = 0; n < NGL; n++) {
@@ -318,7 +287,6 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64) btp_stage_kernel(S
           A[FA_VL * FQ + fq] += vl;
           A[FA_VR * FQ + fq] += vr;
         }
-        double wq = FS[FS_W * FQ + fq];
         double H_kx = nxl * Hf, H_ky = nyl * Hf;
         double lamb = cmlr;
         double dispu = 0.5 * lamb * (qr[2] - ql[2]);
@@ -326,13 +294,13 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64) btp_stage_kernel(S
         double flux_x = nxl * quu + nyl * quv - dispu;
         double flux_y = nxl * qvu + nyl * qvv - dispv;
         double flux = nxl * fex + nyl * fey;
-        double sg = side == 0 ? -wq : wq;
-        s_fq[lf][iq][0] = sg * flux;
-        s_fq[lf][iq][1] = sg * (H_kx + flux_x);
-        s_fq[lf][iq][2] = sg * (H_ky + flux_y);
-      } else if (w < W1 + W2 + W3) {
+        s_fq[lf][iq][0] = FS[FS_W * FQ + fq];
+        s_fq[lf][iq][1] = flux;
+        s_fq[lf][iq][2] = H_kx + flux_x;
+        s_fq[lf][iq][3] = H_ky + flux_y;
+      } else if (w < W2 + W3) {
         // ---- create_rhs_laplacian_flux at (face lf, node n) (mod_laplacian_quad.F90:452-517)
-        const int t = w - W1 - W2, lf = t / NGL, n = t % NGL;
+        const int t = w - W2, lf = t / NGL, n = t % NGL;
         const int f = s_face[lf], side = s_side[lf], er = s_bc[lf];
         const int p = s_map[lf][n];
         const size_t fn = (size_t)f * NGL + n, FN = (size_t)F * NGL;
@@ -372,71 +340,81 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64) btp_stage_kernel(S
         double wq = m.fnstat[FN_W * FN + fn];
         double flux_qu = (qum0 - fl[0] * nxn) + (qum1 - fl[1] * nyn);
         double flux_qv = (qvm0 - fl[2] * nxn) + (qvm1 - fl[3] * nyn);
-        double sg = side == 0 ? wq : -wq;
-        s_fl[lf][n][0] = sg * flux_qu;
-        s_fl[lf][n][1] = sg * flux_qv;
+        // psi(i,iquad) is the identity: node n receives wq*1*flux (zeros add nothing)
+        double h1 = s_psi[n * NGL + n];
+        double c0 = wq * h1 * flux_qu, c1 = wq * h1 * flux_qv;
+        s_fl[lf][n][0] = side == 0 ? c0 : -c0;
+        s_fl[lf][n][1] = side == 0 ? c1 : -c1;
       } else {
-        // ---- btp_compute_laplacian volume fluxes at node p (mod_laplacian_quad.F90:372-388)
-        const int p = w - W1 - W2 - W3;
+        const int p = w - W2 - W3;
         const size_t I = (size_t)e * P + p;
-        const double *NS = m.nstat, *NC = a.ncoef;
+        const double *NC = a.ncoef;
         double pv = NC[NC_PV * (size_t)npoin + I];
-        double qq1 = pv * s_grad[0][p] + NC[NC_D1 * (size_t)npoin + I];
-        double qq2 = pv * s_grad[1][p] + NC[NC_D2 * (size_t)npoin + I];
-        double qq3 = pv * s_grad[2][p] + NC[NC_D3 * (size_t)npoin + I];
-        double qq4 = pv * s_grad[3][p] + NC[NC_D4 * (size_t)npoin + I];
-        double w_ = NS[NS_W * (size_t)npoin + I];
-        double ex = NS[NS_EX * (size_t)npoin + I], ey = NS[NS_EY * (size_t)npoin + I];
-        double nx = NS[NS_NX * (size_t)npoin + I], ny = NS[NS_NY * (size_t)npoin + I];
-        s_lg[0][p] = w_ * (ex * qq1 + ey * qq2);
-        s_lg[1][p] = w_ * (nx * qq1 + ny * qq2);
-        s_lg[2][p] = w_ * (ex * qq3 + ey * qq4);
-        s_lg[3][p] = w_ * (nx * qq3 + ny * qq4);
+        s_qq[0][p] = pv * s_grad[0][p] + NC[NC_D1 * (size_t)npoin + I];
+        s_qq[1][p] = pv * s_grad[1][p] + NC[NC_D2 * (size_t)npoin + I];
+        s_qq[2][p] = pv * s_grad[2][p] + NC[NC_D3 * (size_t)npoin + I];
+        s_qq[3][p] = pv * s_grad[3][p] + NC[NC_D4 * (size_t)npoin + I];
       }
+    }
+  }
+  __syncthreads();
+  // ---------------------------------------------------------------- phase 3
+  // weak-form accumulation, one thread per (node, output), reference order:
+  // rhs(v,p): volume over quad points (mod_rhs_btp.F90:194-206), then faces (:339-362);
+  // lap(c,p): volume over source nodes (mod_laplacian_quad.F90:382-386), then faces (:489-513)
+  for (int t = tid; t < 5 * P; t += BS) {
+    const int v = t / P, p = t % P, i = p % NGL, j = p / NGL;
+    double acc = 0.0;
+    if (v < 3) {
+      for (int q = 0; q < Q; q++) {
+        const int iq = q % NQ, jq = q / NQ;
+        const double hi = PSIH(i, j, iq, jq);
+        const double h_e = HE(i, j, iq, jq), h_n = HN(i, j, iq, jq);
+        const double dhdx = h_e * s_qm[0][q] + h_n * s_qm[2][q];
+        const double dhdy = h_e * s_qm[1][q] + h_n * s_qm[3][q];
+        const double wq = s_qv[0][q];
+        double term;
+        if (v == 0)
+          term = wq * (dhdx * s_qv[1][q] + dhdy * s_qv[2][q]);
+        else if (v == 1)
+          term = wq * (hi * s_qv[3][q] + dhdx * s_qv[5][q] + s_qv[6][q] * dhdy);
+        else
+          term = wq * (hi * s_qv[4][q] + dhdx * s_qv[6][q] + dhdy * s_qv[7][q]);
+        acc = acc + term;
+      }
+      for (int lf = 0; lf < 4; lf++)
+        for (int n = 0; n < NGL; n++) {
+          if (s_map[lf][n] != p) continue;
+          const bool left = s_side[lf] == 0;
+          for (int iq = 0; iq < NQ; iq++) {
+            const double c = s_fq[lf][iq][0] * s_psiq[n * NQ + iq] * s_fq[lf][iq][1 + v];
+            acc = left ? acc - c : acc + c;
+          }
+        }
+      s_rhs[v][p] = acc;
+    } else {
+      const int c = v - 3;
+      for (int jj = 0; jj < NGL; jj++)
+        for (int ii = 0; ii < NGL; ii++) {
+          const int s = jj * NGL + ii;  // source node Iq
+          const double dx = HE_DF(i, j, ii, jj) * s_nm[0][s] + HN_DF(i, j, ii, jj) * s_nm[2][s];
+          const double dy = HE_DF(i, j, ii, jj) * s_nm[1][s] + HN_DF(i, j, ii, jj) * s_nm[3][s];
+          acc = acc - s_nm[4][s] * (dx * s_qq[2 * c][s] + dy * s_qq[2 * c + 1][s]);
+        }
+      for (int lf = 0; lf < 4; lf++)
+        for (int n = 0; n < NGL; n++)
+          if (s_map[lf][n] == p) acc = acc + s_fl[lf][n][c];
+      s_lap[c][p] = acc;
     }
   }
   __syncthreads();
   // ---------------------------------------------------------------- phase 4: per node
   for (int p = tid; p < P; p += BS) {
-    const int i = p % NGL, j = p / NGL;
     const size_t I = (size_t)e * P + p;
-    double r[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-    for (int iq = 0; iq < NQ; iq++) {
-      double dps = s_dpsiq[i * NQ + iq], ps = s_psiq[i * NQ + iq];
-      int w = iq * NGL + j;
-      r[0] += dps * s_A[0][w] + ps * s_A[1][w];
-      r[1] += dps * s_A[2][w] + ps * s_A[3][w];
-      r[2] += dps * s_A[4][w] + ps * s_A[5][w];
-    }
-    double lap0 = 0.0, lap1 = 0.0;
-#pragma unroll
-    for (int k = 0; k < NGL; k++) {
-      lap0 -= s_dpsi[i * NGL + k] * s_lg[0][j * NGL + k] + s_dpsi[j * NGL + k] * s_lg[1][k * NGL + i];
-      lap1 -= s_dpsi[i * NGL + k] * s_lg[2][j * NGL + k] + s_dpsi[j * NGL + k] * s_lg[3][k * NGL + i];
-    }
-    for (int lf = 0; lf < 4; lf++) {
-      for (int n = 0; n < NGL; n++) {
-        if (s_map[lf][n] != p) continue;
-        double f0 = 0, f1 = 0, f2 = 0;
-#pragma unroll
-        for (int iq = 0; iq < NQ; iq++) {
-          double hi = s_psiq[n * NQ + iq];
-          f0 += hi * s_fq[lf][iq][0];
-          f1 += hi * s_fq[lf][iq][1];
-          f2 += hi * s_fq[lf][iq][2];
-        }
-        r[0] += f0;
-        r[1] += f1;
-        r[2] += f2;
-        lap0 += s_fl[lf][n][0];
-        lap1 += s_fl[lf][n][1];
-      }
-    }
     const double mi = m.nstat[NS_MINV * (size_t)npoin + I];
-    double rh0 = mi * r[0], rh1 = mi * r[1], rh2 = mi * r[2];
-    rh1 = rh1 + m.visc * mi * lap0;
-    rh2 = rh2 + m.visc * mi * lap1;
+    double rh0 = mi * s_rhs[0][p], rh1 = mi * s_rhs[1][p], rh2 = mi * s_rhs[2][p];
+    rh1 = rh1 + m.visc * mi * s_lap[0][p];
+    rh2 = rh2 + m.visc * mi * s_lap[1][p];
     if (a.rhs_only) {
       a.rhs_out[I * 3 + 0] = rh0;
       a.rhs_out[I * 3 + 1] = rh1;
@@ -485,15 +463,18 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64) btp_stage_kernel(S
       s_uv[1][p] = s_qn[3][p] / s_qn[0][p];
     }
     __syncthreads();
-    for (int t = tid; t < 4 * NGL; t += BS) {
-      const int lf = t / NGL, n = t % NGL, p = s_map[lf][n];
+    for (int t = tid; t < 4 * 4 * NGL; t += BS) {
+      const int c = t / (4 * NGL), lf = (t / NGL) % 4, n = t % NGL, p = s_map[lf][n];
       const int i = p % NGL, j = p / NGL;
-      const size_t I = (size_t)e * P + p;
-      const double *NS = m.nstat;
-      double g4[4];
-      nodal_grad<NGL>(s_dpsi, s_uv[0], s_uv[1], i, j, NS[NS_EX * (size_t)npoin + I], NS[NS_EY * (size_t)npoin + I],
-                      NS[NS_NX * (size_t)npoin + I], NS[NS_NY * (size_t)npoin + I], g4);
-      for (int c = 0; c < 4; c++) a.gtrace_out[(((size_t)e * 4 + lf) * 4 + c) * NGL + n] = g4[c];
+      const double *u = s_uv[c >> 1];
+      const double ex = s_nm[(c & 1) ? 1 : 0][p], nx = s_nm[(c & 1) ? 3 : 2][p];
+      double gsum = 0.0;
+      for (int mm = 0; mm < NGL; mm++)
+        for (int nn = 0; nn < NGL; nn++) {
+          const double d = HE_DF(nn, mm, i, j) * ex + HN_DF(nn, mm, i, j) * nx;
+          gsum = gsum + d * u[mm * NGL + nn];
+        }
+      a.gtrace_out[(((size_t)e * 4 + lf) * 4 + c) * NGL + n] = gsum;
     }
   }
 }
@@ -503,24 +484,33 @@ template <int NGL, int NQ>
 __global__ void __launch_bounds__(64) grad_trace_kernel(DevMesh m, const double *qb, double *gtrace) {
   constexpr int P = NGL * NGL;
   const int e = blockIdx.x, tid = threadIdx.x;
-  __shared__ double s_dpsi[NGL * NGL], s_u[P], s_v[P];
+  __shared__ double s_dpsi[NGL * NGL], s_psi[NGL * NGL], s_uv[2][P];
   __shared__ int s_map[4][NGL];
-  for (int t = tid; t < NGL * NGL; t += 64) s_dpsi[t] = m.basis[2 * NGL * NQ + t];
+  for (int t = tid; t < NGL * NGL; t += 64) {
+    s_dpsi[t] = m.basis[2 * NGL * NQ + t];
+    s_psi[t] = m.basis[2 * NGL * NQ + NGL * NGL + t];
+  }
   for (int t = tid; t < 4 * NGL; t += 64) s_map[t / NGL][t % NGL] = m.efmap[e * 4 * NGL + t];
   for (int p = tid; p < P; p += 64) {
     const double *q = qb + ((size_t)e * P + p) * 4;
-    s_u[p] = q[2] / q[0];
-    s_v[p] = q[3] / q[0];
+    s_uv[0][p] = q[2] / q[0];
+    s_uv[1][p] = q[3] / q[0];
   }
   __syncthreads();
-  for (int t = tid; t < 4 * NGL; t += 64) {
-    const int lf = t / NGL, n = t % NGL, p = s_map[lf][n];
+  for (int t = tid; t < 4 * 4 * NGL; t += 64) {
+    const int c = t / (4 * NGL), lf = (t / NGL) % 4, n = t % NGL, p = s_map[lf][n];
+    const int i = p % NGL, j = p / NGL;
     const size_t I = (size_t)e * P + p;
-    double g4[4];
-    nodal_grad<NGL>(s_dpsi, s_u, s_v, p % NGL, p / NGL, m.nstat[NS_EX * (size_t)m.npoin + I],
-                    m.nstat[NS_EY * (size_t)m.npoin + I], m.nstat[NS_NX * (size_t)m.npoin + I],
-                    m.nstat[NS_NY * (size_t)m.npoin + I], g4);
-    for (int c = 0; c < 4; c++) gtrace[(((size_t)e * 4 + lf) * 4 + c) * NGL + n] = g4[c];
+    const double *u = s_uv[c >> 1];
+    const double ex = m.nstat[((c & 1) ? NS_EY : NS_EX) * (size_t)m.npoin + I];
+    const double nx = m.nstat[((c & 1) ? NS_NY : NS_NX) * (size_t)m.npoin + I];
+    double gsum = 0.0;
+    for (int mm = 0; mm < NGL; mm++)
+      for (int nn = 0; nn < NGL; nn++) {
+        const double d = HE_DF(nn, mm, i, j) * ex + HN_DF(nn, mm, i, j) * nx;
+        gsum = gsum + d * u[mm * NGL + nn];
+      }
+    gtrace[(((size_t)e * 4 + lf) * 4 + c) * NGL + n] = gsum;
   }
 }
 
