@@ -44,7 +44,7 @@ struct hnumo_engine {
   std::vector<double> ssprk_a, ssprk_beta;  // host copies (kstages x 3), (kstages)
   // state and step temporaries
   double *q, *qb, *qp, *q2, *qp2, *qbp, *qf, *qf2, *dpp2;
-  double *qbuf[4], *gtrace[2];
+  double *qbuf[4], *gtrace[2];  // gtrace: [E][4][8][NGL] face traces (qb, grad u_bar) in the reader's slot
   // per-sub-cycle coefficients
   double *qcoef, *ncoef, *fcoef, *fncoef, *dpp_graduv, *dpprime_visc, *gdpp_face;
   // accumulators
@@ -57,6 +57,10 @@ struct hnumo_engine {
   hipGraphExec_t graph_exec = nullptr;
   bool resident = false, uploaded = false, alloc_failed = false;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // events recorded inside the captured step around the corrector sub-cycle's stage kernels
+  hipEvent_t evk0 = nullptr, evk1 = nullptr;
+  bool capturing = false, kernel_events = false;
+  unsigned long long *stage_prof = nullptr;  // HNUMO_STAGE_PROF=1: per-element phase clocks
 };
 
 template <typename T>
@@ -76,7 +80,7 @@ template <int NGL, int NQ>
 struct Launch {
   static constexpr int BSE = ((NQ * NQ + 63) / 64) * 64;
   static void stage(hnumo_engine *e, const StageArgs &a) {
-    hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ>), dim3(e->nelem), dim3(BSE), 0, e->stream, a);
+    hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ>), dim3(e->nelem), dim3(StageCfg<NGL, NQ>::BS), 0, e->stream, a);
   }
   static void grad_trace(hnumo_engine *e, const double *qb, double *gt) {
     hipLaunchKernelGGL((grad_trace_kernel<NGL, NQ>), dim3(e->nelem), dim3(64), 0, e->stream, e->m, qb, gt);
@@ -180,10 +184,11 @@ static void launch_bcl_coeffs(hnumo_engine *e, const double *qp, double *qf) {
 }
 
 // ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:19-151) on device state qb_state
-static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp) {
+static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp, bool timed = false) {
   zero_accumulators(e);
   launch_copy(e, e->qbuf[0], qb_state, 4 * (size_t)e->npoin);
   DISPATCH(e, grad_trace(e, e->qbuf[0], e->gtrace[0]));
+  if (timed && e->kernel_events) (void)hipEventRecord(e->evk0, e->stream);
   int cur = 0, gt = 0, qb0i = 0, qb2i = -1;
   const int K = e->K, NB = e->p.N_btp;
   for (int mstep = 0; mstep < NB; mstep++) {
@@ -202,8 +207,8 @@ static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp)
       a.ncoef = e->ncoef;
       a.fcoef = e->fcoef;
       a.fncoef = e->fncoef;
-      a.gtrace_in = e->gtrace[gt];
-      a.gtrace_out = e->gtrace[1 - gt];
+      a.trace_in = e->gtrace[gt];
+      a.trace_out = e->gtrace[1 - gt];
       a.qacc = e->qacc;
       a.facc = e->facc;
       a.nacc = e->nacc;
@@ -215,14 +220,16 @@ static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp)
       a.a3 = e->ssprk_a[ik + 2 * K];
       a.dtt = e->p.dt_btp * e->ssprk_beta[ik];
       a.rhs_only = 0;
-      a.write_grad = !(mstep == NB - 1 && ik == K - 1);
+      a.write_trace = !(mstep == NB - 1 && ik == K - 1);
       a.accumulate = 1;
+      a.prof = e->stage_prof;
       DISPATCH(e, stage(e, a));
       gt = 1 - gt;
       cur = out;
       if (K == 5 && ik == 1) qb2i = out;
     }
   }
+  if (timed && e->kernel_events) (void)hipEventRecord(e->evk1, e->stream);
   int nblk = 1024;
   hipLaunchKernelGGL(btp_finalize_kernel, dim3(nblk), dim3(256), 0, e->stream, e->qacc, e->facc, e->nacc, e->gfacc,
                      e->tau_wind_ave, e->tau_wind, e->npq, (int)e->FQ, e->npoin, (int)e->FN, NB,
@@ -248,7 +255,7 @@ static void launch_step(hnumo_engine *e) {
   launch_avg(e, e->qp2, e->qp2, e->qp, n3, 1);
   launch_avg(e, e->qf2, e->qf, e->qf2, nf, 1);
   DISPATCH(e, bcl_coeffs(e, e->qp2, e->qf2));
-  launch_subcycle(e, e->qb, e->qp2);
+  launch_subcycle(e, e->qb, e->qp2, true);
   DISPATCH(e, mass_cons(e, e->qp2, e->qf2, e->q, e->qp2, 1));
   DISPATCH(e, extract(e, e->qp2, e->qf2, 1));
   hipLaunchKernelGGL(dp_average_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp2, e->qp, e->dpp2, nl);
@@ -275,6 +282,8 @@ void hnumo_engine_destroy(hnumo_engine *eng) {
   if (eng->stream) (void)hipStreamDestroy(eng->stream);
   if (eng->ev0) (void)hipEventDestroy(eng->ev0);
   if (eng->ev1) (void)hipEventDestroy(eng->ev1);
+  if (eng->evk0) (void)hipEventDestroy(eng->evk0);
+  if (eng->evk1) (void)hipEventDestroy(eng->evk1);
   delete eng;
 }
 
@@ -385,6 +394,12 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
       hb[2 * ngl * nq + n * ngl + k] = mesh->dpsi[n + ngl * k];
       hb[2 * ngl * nq + ngl * ngl + n * ngl + k] = mesh->psi[n + ngl * k];
     }
+  // the stage kernels drop the zero terms of the nodal derivative sums: psi must be the
+  // identity at the LGL nodes (it is, exactly, for the reference's nodal basis)
+  for (int n = 0; n < ngl; n++)
+    for (int k = 0; k < ngl; k++)
+      if (mesh->psi[n + ngl * k] != (n == k ? 1.0 : 0.0))
+        return fail(eng, HNUMO_ERR_INVALID, "nodal basis psi is not the identity at the LGL nodes");
   std::vector<double> qs(QS_N * npq), ns(NS_N * npoin), fs(FS_N * FQ), fns(FN_N * FN);
   for (size_t i = 0; i < npq; i++) {
     qs[QS_W * npq + i] = mesh->jacq[i];
@@ -453,7 +468,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   eng->qf = dalloc<double>(eng, 6 * FN * L); eng->qf2 = dalloc<double>(eng, 6 * FN * L);
   eng->dpp2 = dalloc<double>(eng, npoin * L);
   for (int i = 0; i < 4; i++) eng->qbuf[i] = dalloc<double>(eng, 4 * npoin);
-  for (int i = 0; i < 2; i++) eng->gtrace[i] = dalloc<double>(eng, (size_t)E * 16 * ngl);
+  for (int i = 0; i < 2; i++) eng->gtrace[i] = dalloc<double>(eng, (size_t)E * 32 * ngl);
   eng->qcoef = dalloc<double>(eng, QC_N * npq); eng->ncoef = dalloc<double>(eng, NC_N * npoin);
   eng->fcoef = dalloc<double>(eng, FC_N * FQ); eng->fncoef = dalloc<double>(eng, 10 * FN);
   eng->dpp_graduv = dalloc<double>(eng, 4 * npoin * L); eng->dpprime_visc = dalloc<double>(eng, npoin * L);
@@ -468,6 +483,8 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   eng->lapf = dalloc<double>(eng, 2 * FN * L);
   eng->rhs = dalloc<double>(eng, 3 * npoin);
   eng->neg_flag = dalloc<int>(eng, 1);
+  if (const char *sp = getenv("HNUMO_STAGE_PROF"))
+    if (sp[0] == '1') eng->stage_prof = dalloc<unsigned long long>(eng, (size_t)eng->nelem * 12);
   if (eng->alloc_failed) return fail(eng, HNUMO_ERR_DEVICE, "hipMalloc failed (out of device memory?)");
   HIPCHK(hipHostMalloc((void **)&eng->h_neg, sizeof(int)));
   HIPCHK(hipMemcpy(eng->basis, hb.data(), hb.size() * 8, hipMemcpyHostToDevice));
@@ -510,10 +527,27 @@ static int download_state(hnumo_engine *eng, double *q, double *qb, double *qp) 
 
 static int ensure_graph(hnumo_engine *eng) {
   if (eng->graph_exec) return 0;
-  HIPCHK(hipStreamBeginCapture(eng->stream, hipStreamCaptureModeThreadLocal));
-  launch_step(eng);
-  HIPCHK(hipStreamEndCapture(eng->stream, &eng->graph));
-  HIPCHK(hipGraphInstantiate(&eng->graph_exec, eng->graph, nullptr, nullptr, 0));
+  // first try with event-record nodes around the timed stage-kernel sequence
+  for (int attempt = 0; attempt < 2; attempt++) {
+    eng->kernel_events = attempt == 0;
+    if (eng->kernel_events && !eng->evk0) {
+      HIPCHK(hipEventCreate(&eng->evk0));
+      HIPCHK(hipEventCreate(&eng->evk1));
+    }
+    HIPCHK(hipStreamBeginCapture(eng->stream, hipStreamCaptureModeThreadLocal));
+    launch_step(eng);
+    hipError_t err = hipStreamEndCapture(eng->stream, &eng->graph);
+    if (err == hipSuccess) err = hipGraphInstantiate(&eng->graph_exec, eng->graph, nullptr, nullptr, 0);
+    if (err == hipSuccess) return 0;
+    (void)hipGetLastError();
+    if (eng->graph) (void)hipGraphDestroy(eng->graph);
+    eng->graph = nullptr;
+    eng->graph_exec = nullptr;
+    if (attempt == 1) {
+      eng->err = std::string("graph capture failed: ") + hipGetErrorString(err);
+      return HNUMO_ERR_DEVICE;
+    }
+  }
   return 0;
 }
 
@@ -589,10 +623,10 @@ int hnumo_create_rhs_btp(hnumo_engine *eng, double *rhs, const double *qb_df, co
   a.m = eng->m;
   a.qb_in = eng->qb; a.qb0 = eng->qb; a.qb2 = eng->qb; a.qprime = eng->qp;
   a.qcoef = eng->qcoef; a.ncoef = eng->ncoef; a.fcoef = eng->fcoef; a.fncoef = eng->fncoef;
-  a.gtrace_in = eng->gtrace[0]; a.gtrace_out = eng->gtrace[1];
+  a.trace_in = eng->gtrace[0]; a.trace_out = eng->gtrace[1];
   a.qacc = eng->qacc; a.facc = eng->facc; a.nacc = eng->nacc; a.gfacc = eng->gfacc;
   a.qb_out = eng->qbuf[0]; a.rhs_out = eng->rhs;
-  a.rhs_only = 1; a.write_grad = 0; a.accumulate = 1;
+  a.rhs_only = 1; a.write_trace = 0; a.accumulate = 1;
   DISPATCH(eng, stage(eng, a));
   HIPCHK(hipMemcpyAsync(rhs, eng->rhs, 3 * (size_t)eng->npoin * 8, hipMemcpyDeviceToHost, eng->stream));
   HIPCHK(hipStreamSynchronize(eng->stream));
@@ -697,8 +731,52 @@ int hnumo_bench_steps(hnumo_engine *eng, int nsteps, double *ms_total, double *m
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, eng->ev0, eng->ev1));
   if (ms_total) *ms_total = ms;
-  if (ms_kernel_avg) *ms_kernel_avg = -1.0;
+  // average stage-kernel duration of the last replay's corrector sub-cycle (N_btp*K
+  // back-to-back launches of btp_stage_kernel bracketed by in-graph event nodes)
+  double kavg = -1.0;
+  if (eng->kernel_events) {
+    float mk = 0.f;
+    if (hipEventElapsedTime(&mk, eng->evk0, eng->evk1) == hipSuccess) kavg = mk / (double)(eng->p.N_btp * eng->K);
+  }
+  if (ms_kernel_avg) *ms_kernel_avg = kavg;
   if (kernel_launches) *kernel_launches = (int64_t)nsteps * 2 * eng->p.N_btp * eng->K;
+  return 0;
+}
+
+int hnumo_time_stage_kernel(hnumo_engine *eng, int nsubcycles, double *ms_kernel_avg) {
+  if (!eng || nsubcycles < 1 || !ms_kernel_avg) return HNUMO_ERR_INVALID;
+  HIPCHK(hipSetDevice(eng->device));
+  if (!eng->evk0) {
+    HIPCHK(hipEventCreate(&eng->evk0));
+    HIPCHK(hipEventCreate(&eng->evk1));
+  }
+  (void)hipGetLastError();  // clear a sticky error left by an unsupported in-graph event record
+  // the corrector sub-cycle of the current device state, on a scratch copy of qb
+  const bool ke = eng->kernel_events;
+  eng->kernel_events = true;
+  double total = 0.0;
+  for (int s = 0; s < nsubcycles; s++) {
+    launch_copy(eng, eng->qbp, eng->qb, 4 * (size_t)eng->npoin);
+    launch_subcycle(eng, eng->qbp, eng->qp, true);
+    HIPCHK(hipEventSynchronize(eng->evk1));
+    float mk = 0.f;
+    HIPCHK(hipEventElapsedTime(&mk, eng->evk0, eng->evk1));
+    total += mk;
+  }
+  eng->kernel_events = ke;
+  HIPCHK(hipStreamSynchronize(eng->stream));
+  HIPCHK(hipGetLastError());
+  *ms_kernel_avg = total / ((double)nsubcycles * eng->p.N_btp * eng->K);
+  return 0;
+}
+
+int hnumo_debug_stage_profile(hnumo_engine *eng, uint64_t *out, int64_t n) {
+  if (!eng || !out) return HNUMO_ERR_INVALID;
+  if (!eng->stage_prof) return fail(eng, HNUMO_ERR_INVALID, "engine created without HNUMO_STAGE_PROF=1");
+  if (n < (int64_t)eng->nelem * 12) return fail(eng, HNUMO_ERR_INVALID, "buffer too small");
+  HIPCHK(hipSetDevice(eng->device));
+  HIPCHK(hipStreamSynchronize(eng->stream));
+  HIPCHK(hipMemcpy(out, eng->stage_prof, (size_t)eng->nelem * 12 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return 0;
 }
 

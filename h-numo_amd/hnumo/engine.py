@@ -47,6 +47,8 @@ def lib():
         L.hnumo_sync.argtypes = [vp, dp, dp, dp]
         L.hnumo_bench_steps.argtypes = [vp, C.c_int, dp, dp, C.POINTER(C.c_int64)]
         L.hnumo_abi_version.restype = C.c_int
+        L.hnumo_time_stage_kernel.argtypes = [vp, C.c_int, dp]
+        L.hnumo_debug_stage_profile.argtypes = [vp, C.POINTER(C.c_uint64), C.c_int64]
         _lib = L
     return _lib
 
@@ -117,6 +119,18 @@ class Engine:
         n = C.c_int64()
         self._check(lib().hnumo_bench_steps(self.h, nsteps, C.byref(t), C.byref(k), C.byref(n)))
         return t.value, k.value, n.value
+
+    def time_stage_kernel(self, nsubcycles: int = 2) -> float:
+        """Average btp_stage_kernel duration (ms), HIP events on the engine stream."""
+        k = C.c_double()
+        self._check(lib().hnumo_time_stage_kernel(self.h, nsubcycles, C.byref(k)))
+        return k.value
+
+    def stage_profile(self):
+        n = self.dims["nelem"] * 12
+        out = np.zeros(n, dtype=np.uint64)
+        self._check(lib().hnumo_debug_stage_profile(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), n))
+        return out.reshape(-1, 12)
 
     def _destroy(self):
         if getattr(self, "h", None) is not None and self.h.value:

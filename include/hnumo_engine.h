@@ -165,6 +165,15 @@ int hnumo_sync(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df
 int hnumo_bench_steps(hnumo_engine *eng, int nsteps, double *ms_total,
                       double *ms_kernel_avg, int64_t *kernel_launches);
 
+/* Average duration (ms) of the fused barotropic stage kernel, from HIP events recorded
+ * on the engine stream around `nsubcycles` direct (non-graph) corrector sub-cycles of the
+ * current device state (qb is not modified).                                          */
+int hnumo_time_stage_kernel(hnumo_engine *eng, int nsubcycles, double *ms_kernel_avg);
+
+/* Diagnostics: per-element phase clocks of the last stage launch, [nelem][12] uint64
+ * (engine created with HNUMO_STAGE_PROF=1 in the environment).                        */
+int hnumo_debug_stage_profile(hnumo_engine *eng, uint64_t *out, int64_t n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -50,6 +50,7 @@ program ref_driver
     implicit none
 
     integer :: hi(16), ierr, u, nsteps, mode, istep, k
+    real(8) :: t0, t1
     real(8) :: hd(8)
     character(len=512) :: fin, fout
     integer, allocatable :: iface3(:,:,:), iface2(:,:)
@@ -176,9 +177,12 @@ program ref_driver
             call ti_barotropic_ssprk_mlswe(qb_df, qprime_df)
         end if
     case (3)
+        t0 = mpi_wtime()
         do istep = 1, nsteps
             call ti_rk_bcl(q_df, qb_df, qprime_df)
         end do
+        t1 = mpi_wtime()
+        write(*, '(A,ES24.16)') 'REF_TIME ', t1 - t0
     case default
         stop 'unknown mode'
     end select
