@@ -47,6 +47,9 @@ struct hnumo_engine {
   double *qbuf[4], *gtrace[2];  // gtrace: [E][4][8][NGL] face traces (qb, grad u_bar) in the reader's slot
   // per-sub-cycle coefficients
   double *qcoef, *ncoef, *fcoef, *fncoef, *dpp_graduv, *dpprime_visc, *gdpp_face;
+  double *ecoef, *efcoef;                   // element-major copies for the stage kernel
+  double *qstatE, *nstatE, *efstat;         // element-major statics for the stage kernel
+  std::vector<int> fslotL;                  // host copy: face -> left element slot e*4+lf
   // accumulators
   double *qacc, *facc, *nacc, *gfacc, *tau_wind_ave;
   // baroclinic scratch
@@ -92,9 +95,9 @@ struct Launch {
   }
   static void bcl_coeffs(hnumo_engine *e, const double *qp, const double *qf) {
     hipLaunchKernelGGL((bcl_coeffs_elem_kernel<NGL, NQ>), dim3(e->nelem), dim3(BSE), 0, e->stream, e->m, qp,
-                       e->qcoef, e->ncoef, e->dpp_graduv, e->dpprime_visc);
+                       e->qcoef, e->ncoef, e->dpp_graduv, e->dpprime_visc, e->ecoef);
     hipLaunchKernelGGL((bcl_coeffs_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf,
-                       e->dpp_graduv, e->dpprime_visc, e->fcoef, e->fncoef, e->gdpp_face);
+                       e->dpp_graduv, e->dpprime_visc, e->fcoef, e->fncoef, e->gdpp_face, e->efcoef);
   }
   static void mass_cons(hnumo_engine *e, const double *qp, const double *qf, double *q, double *qp_out,
                         int finalize_dp) {
@@ -173,9 +176,9 @@ static void launch_avg(hnumo_engine *e, double *out, const double *a, const doub
 
 static void zero_accumulators(hnumo_engine *e) {
   (void)hipMemsetAsync(e->qacc, 0, sizeof(double) * QA_N * e->npq, e->stream);
-  (void)hipMemsetAsync(e->facc, 0, sizeof(double) * FA_N * e->FQ, e->stream);
+  (void)hipMemsetAsync(e->facc, 0, sizeof(double) * FA_N * 4 * (size_t)e->nelem * e->nq, e->stream);
   (void)hipMemsetAsync(e->nacc, 0, sizeof(double) * NA_N * e->npoin, e->stream);
-  (void)hipMemsetAsync(e->gfacc, 0, sizeof(double) * 8 * e->FN, e->stream);
+  (void)hipMemsetAsync(e->gfacc, 0, sizeof(double) * 8 * 4 * (size_t)e->nelem * e->ngl, e->stream);
 }
 
 static void launch_bcl_coeffs(hnumo_engine *e, const double *qp, double *qf) {
@@ -203,10 +206,8 @@ static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp,
       a.qb0 = e->qbuf[qb0i];
       a.qb2 = qb2i >= 0 ? e->qbuf[qb2i] : e->qbuf[cur];
       a.qprime = qp;
-      a.qcoef = e->qcoef;
-      a.ncoef = e->ncoef;
-      a.fcoef = e->fcoef;
-      a.fncoef = e->fncoef;
+      a.ecoef = e->ecoef;
+      a.efcoef = e->efcoef;
       a.trace_in = e->gtrace[gt];
       a.trace_out = e->gtrace[1 - gt];
       a.qacc = e->qacc;
@@ -232,7 +233,7 @@ static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp,
   if (timed && e->kernel_events) (void)hipEventRecord(e->evk1, e->stream);
   int nblk = 1024;
   hipLaunchKernelGGL(btp_finalize_kernel, dim3(nblk), dim3(256), 0, e->stream, e->qacc, e->facc, e->nacc, e->gfacc,
-                     e->tau_wind_ave, e->tau_wind, e->npq, (int)e->FQ, e->npoin, (int)e->FN, NB,
+                     e->tau_wind_ave, e->tau_wind, e->npq, 4 * e->nelem * e->nq, e->npoin, 4 * e->nelem * e->ngl, NB,
                      1.0 / (double)(K * NB));
   launch_copy(e, qb_state, e->qbuf[cur], 4 * (size_t)e->npoin);
 }
@@ -369,6 +370,37 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
       if (er > 0) fnodeR[(size_t)f * ngl + n] = (er - 1) * P + lnode(mesh->imapr, f, n);
     }
   }
+  // face -> element-side slots; per-element int records for the stage kernel
+  std::vector<int> fslotL(F, -1), fslotR(F, -1);
+  for (int e = 0; e < E; e++)
+    for (int lf = 0; lf < 4; lf++) (eside[4 * e + lf] == 0 ? fslotL : fslotR)[efaces[4 * e + lf]] = 4 * e + lf;
+  const int ERS = EREC_SIZE(ngl);
+  std::vector<int> erec((size_t)E * ERS, -1);
+  for (int e = 0; e < E; e++) {
+    int *r = &erec[(size_t)e * ERS];
+    for (int lf = 0; lf < 4; lf++) {
+      r[EREC_FACE + lf] = efaces[4 * e + lf];
+      r[EREC_SIDE + lf] = eside[4 * e + lf];
+      r[EREC_BC + lf] = ebc[4 * e + lf];
+      r[EREC_NBE + lf] = enbr_e[4 * e + lf];
+      r[EREC_NBLF + lf] = enbr_lf[4 * e + lf];
+      for (int n = 0; n < ngl; n++) r[EREC_MAP + lf * ngl + n] = efmap[(4 * e + lf) * ngl + n];
+      if (ebc[4 * e + lf] > 0) {
+        // the stage kernel writes face traces into the neighbour's slot with the same face-node index
+        const int nb = enbr_e[4 * e + lf], nlf = enbr_lf[4 * e + lf];
+        for (int n = 0; n < ngl; n++)
+          if (enbr_node[(4 * e + lf) * ngl + n] != nb * P + efmap[(4 * nb + nlf) * ngl + n])
+            return fail(eng, HNUMO_ERR_INVALID, "face node orderings of neighbouring elements disagree");
+      }
+    }
+    for (int lf = 0; lf < 4; lf++)
+      for (int n = 0; n < ngl; n++) {
+        int *pf = &r[EREC_PF(ngl) + 2 * efmap[(4 * e + lf) * ngl + n]];
+        if (pf[0] < 0) pf[0] = lf * ngl + n; else if (pf[1] < 0) pf[1] = lf * ngl + n;
+        else return fail(eng, HNUMO_ERR_INVALID, "a node lies on more than two faces of its element");
+      }
+  }
+  eng->fslotL = fslotL;
   std::vector<int> conn;
   auto append = [&](const std::vector<int> &v) {
     size_t off = conn.size();
@@ -378,6 +410,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   size_t o_ef = append(efaces), o_es = append(eside), o_eb = append(ebc), o_em = append(efmap);
   size_t o_en = append(enbr_node), o_ee = append(enbr_e), o_el = append(enbr_lf), o_fl = append(fnodeL);
   size_t o_fr = append(fnodeR), o_fe = append(fel), o_fer = append(fer);
+  size_t o_sl = append(fslotL), o_sr = append(fslotR), o_er = append(erec);
   eng->iconn = dalloc<int>(eng, conn.size());
   if (!eng->iconn) return fail(eng, HNUMO_ERR_DEVICE, "hipMalloc failed");
   HIPCHK(hipMemcpy(eng->iconn, conn.data(), conn.size() * sizeof(int), hipMemcpyHostToDevice));
@@ -452,6 +485,29 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     fns[FN_PBL * FN + i] = st->pbprime_df_face[2 * i];
     fns[FN_PBR * FN + i] = st->pbprime_df_face[2 * i + 1];
   }
+  // element-major statics (engine_internal.h)
+  const int Qe = nq * nq, FBLK = EF_N * nq + EFN_N * ngl;
+  std::vector<double> qsE((size_t)E * QE_N * Qe), nsE((size_t)E * NE_N * P), efs((size_t)E * 4 * FBLK);
+  {
+    const int qmap[QE_N] = {QS_W, QS_EX, QS_EY, QS_NX, QS_NY, QS_COR, QS_TW1, QS_TW2, QS_GZ1, QS_GZ2, QS_OOP};
+    const int nmap[NE_N] = {NS_EX, NS_EY, NS_NX, NS_NY, NS_W, NS_MINV, NS_PB, NS_OOP};
+    const int fmap_[EF_N] = {FS_NX, FS_NY, FS_W, FS_CL, FS_CR, FS_CLR, FS_CML, FS_CMR, FS_CMLR, FS_OOPE};
+    const int fnmap[EFN_N] = {FN_NX, FN_NY, FN_W, FN_PBL, FN_PBR};
+    for (int e = 0; e < E; e++) {
+      for (int c = 0; c < QE_N; c++)
+        for (int q = 0; q < Qe; q++) qsE[((size_t)e * QE_N + c) * Qe + q] = qs[qmap[c] * npq + (size_t)e * Qe + q];
+      for (int c = 0; c < NE_N; c++)
+        for (int p = 0; p < P; p++) nsE[((size_t)e * NE_N + c) * P + p] = ns[nmap[c] * npoin + (size_t)e * P + p];
+      for (int lf = 0; lf < 4; lf++) {
+        const size_t f = efaces[4 * e + lf];
+        double *b = &efs[((size_t)e * 4 + lf) * FBLK];
+        for (int c = 0; c < EF_N; c++)
+          for (int iq = 0; iq < nq; iq++) b[c * nq + iq] = fs[fmap_[c] * FQ + f * nq + iq];
+        for (int c = 0; c < EFN_N; c++)
+          for (int n = 0; n < ngl; n++) b[EF_N * nq + c * ngl + n] = fns[fnmap[c] * FN + f * ngl + n];
+      }
+    }
+  }
   eng->ssprk_a.assign(st->ssprk_a, st->ssprk_a + 3 * par->kstages);
   eng->ssprk_beta.assign(st->ssprk_beta, st->ssprk_beta + par->kstages);
 
@@ -460,6 +516,11 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   eng->nstat = dalloc<double>(eng, ns.size());
   eng->fstat = dalloc<double>(eng, fs.size());
   eng->fnstat = dalloc<double>(eng, fns.size());
+  eng->qstatE = dalloc<double>(eng, qsE.size());
+  eng->nstatE = dalloc<double>(eng, nsE.size());
+  eng->efstat = dalloc<double>(eng, efs.size());
+  eng->ecoef = dalloc<double>(eng, (size_t)E * (4 * Qe + 5 * P));
+  eng->efcoef = dalloc<double>(eng, (size_t)E * 4 * (4 * nq + 10 * ngl));
   eng->alpha = dalloc<double>(eng, L);
   eng->tau_wind = dalloc<double>(eng, 2 * npq);
   const size_t n3 = 3 * npoin * L;
@@ -473,8 +534,8 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   eng->fcoef = dalloc<double>(eng, FC_N * FQ); eng->fncoef = dalloc<double>(eng, 10 * FN);
   eng->dpp_graduv = dalloc<double>(eng, 4 * npoin * L); eng->dpprime_visc = dalloc<double>(eng, npoin * L);
   eng->gdpp_face = dalloc<double>(eng, 10 * FN * L);
-  eng->qacc = dalloc<double>(eng, QA_N * npq); eng->facc = dalloc<double>(eng, FA_N * FQ);
-  eng->nacc = dalloc<double>(eng, NA_N * npoin); eng->gfacc = dalloc<double>(eng, 8 * FN);
+  eng->qacc = dalloc<double>(eng, QA_N * npq); eng->facc = dalloc<double>(eng, FA_N * 4 * (size_t)E * nq);
+  eng->nacc = dalloc<double>(eng, NA_N * npoin); eng->gfacc = dalloc<double>(eng, 8 * 4 * (size_t)E * ngl);
   eng->tau_wind_ave = dalloc<double>(eng, 2 * npq);
   eng->slmf = dalloc<double>(eng, 2 * npq); eng->slmf_face = dalloc<double>(eng, 2 * FQ);
   eng->dpp = dalloc<double>(eng, npoin * L);
@@ -484,7 +545,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   eng->rhs = dalloc<double>(eng, 3 * npoin);
   eng->neg_flag = dalloc<int>(eng, 1);
   if (const char *sp = getenv("HNUMO_STAGE_PROF"))
-    if (sp[0] == '1') eng->stage_prof = dalloc<unsigned long long>(eng, (size_t)eng->nelem * 12);
+    if (sp[0] == '1') eng->stage_prof = dalloc<unsigned long long>(eng, (size_t)eng->nelem * 32);
   if (eng->alloc_failed) return fail(eng, HNUMO_ERR_DEVICE, "hipMalloc failed (out of device memory?)");
   HIPCHK(hipHostMalloc((void **)&eng->h_neg, sizeof(int)));
   HIPCHK(hipMemcpy(eng->basis, hb.data(), hb.size() * 8, hipMemcpyHostToDevice));
@@ -492,6 +553,9 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   HIPCHK(hipMemcpy(eng->nstat, ns.data(), ns.size() * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(eng->fstat, fs.data(), fs.size() * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(eng->fnstat, fns.data(), fns.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->qstatE, qsE.data(), qsE.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->nstatE, nsE.data(), nsE.size() * 8, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(eng->efstat, efs.data(), efs.size() * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(eng->alpha, st->alpha, L * 8, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(eng->tau_wind, st->tau_wind, 2 * npq * 8, hipMemcpyHostToDevice));
 
@@ -500,6 +564,8 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   m.efaces = eng->iconn + o_ef; m.eside = eng->iconn + o_es; m.ebc = eng->iconn + o_eb; m.efmap = eng->iconn + o_em;
   m.enbr_node = eng->iconn + o_en; m.enbr_e = eng->iconn + o_ee; m.enbr_lf = eng->iconn + o_el;
   m.fnodeL = eng->iconn + o_fl; m.fnodeR = eng->iconn + o_fr; m.fel = eng->iconn + o_fe; m.fer = eng->iconn + o_fer;
+  m.fslotL = eng->iconn + o_sl; m.fslotR = eng->iconn + o_sr; m.erec = eng->iconn + o_er;
+  m.qstatE = eng->qstatE; m.nstatE = eng->nstatE; m.efstat = eng->efstat;
   m.basis = eng->basis; m.qstat = eng->qstat; m.nstat = eng->nstat; m.fstat = eng->fstat; m.fnstat = eng->fnstat;
   m.alpha = eng->alpha;
   m.gravity = par->gravity; m.cd = par->cd_mlswe; m.visc = par->visc_mlswe; m.dt = par->dt; m.dt_btp = par->dt_btp;
@@ -622,7 +688,7 @@ int hnumo_create_rhs_btp(hnumo_engine *eng, double *rhs, const double *qb_df, co
   StageArgs a{};
   a.m = eng->m;
   a.qb_in = eng->qb; a.qb0 = eng->qb; a.qb2 = eng->qb; a.qprime = eng->qp;
-  a.qcoef = eng->qcoef; a.ncoef = eng->ncoef; a.fcoef = eng->fcoef; a.fncoef = eng->fncoef;
+  a.ecoef = eng->ecoef; a.efcoef = eng->efcoef;
   a.trace_in = eng->gtrace[0]; a.trace_out = eng->gtrace[1];
   a.qacc = eng->qacc; a.facc = eng->facc; a.nacc = eng->nacc; a.gfacc = eng->gfacc;
   a.qb_out = eng->qbuf[0]; a.rhs_out = eng->rhs;
@@ -661,14 +727,56 @@ int hnumo_get_field(hnumo_engine *eng, const char *name, double *out, int64_t n)
     }
     return 0;
   };
+  // element-major accumulators -> reference (ncomp, N) layouts
+  const int E_ = eng->nelem, Q_ = nq * nq, P_ = ngl * ngl;
+  auto qacc_f = [&](std::initializer_list<int> fields) -> int {
+    size_t nc = fields.size();
+    if ((size_t)n != nc * npq) return fail(eng, HNUMO_ERR_INVALID, "field size mismatch");
+    int rc = fetch(eng->qacc, QA_N * npq, h);
+    if (rc) return rc;
+    size_t c = 0;
+    for (int k : fields) {
+      for (int e = 0; e < E_; e++)
+        for (int q = 0; q < Q_; q++) out[((size_t)e * Q_ + q) * nc + c] = h[((size_t)e * QA_N + k) * Q_ + q];
+      c++;
+    }
+    return 0;
+  };
+  auto nacc_f = [&](std::initializer_list<int> fields) -> int {
+    size_t nc = fields.size();
+    if ((size_t)n != nc * npoin) return fail(eng, HNUMO_ERR_INVALID, "field size mismatch");
+    int rc = fetch(eng->nacc, NA_N * npoin, h);
+    if (rc) return rc;
+    size_t c = 0;
+    for (int k : fields) {
+      for (int e = 0; e < E_; e++)
+        for (int p = 0; p < P_; p++) out[((size_t)e * P_ + p) * nc + c] = h[((size_t)e * NA_N + k) * P_ + p];
+      c++;
+    }
+    return 0;
+  };
+  auto facc_f = [&](std::initializer_list<int> fields) -> int {
+    size_t nc = fields.size();
+    if ((size_t)n != nc * FQ) return fail(eng, HNUMO_ERR_INVALID, "field size mismatch");
+    int rc = fetch(eng->facc, (size_t)FA_N * 4 * E_ * nq, h);
+    if (rc) return rc;
+    size_t c = 0;
+    for (int k : fields) {
+      for (size_t f = 0; f < (size_t)eng->nface; f++)
+        for (int iq = 0; iq < nq; iq++)
+          out[(f * nq + iq) * nc + c] = h[((size_t)eng->fslotL[f] * FA_N + k) * nq + iq];
+      c++;
+    }
+    return 0;
+  };
   struct QF1 { const char *nm; int fld; };
   static const QF1 qsingle[] = {{"ope_ave", QA_OPE}, {"H_ave", QA_H}, {"Qu_ave", QA_QU}, {"Qv_ave", QA_QV},
                                 {"Quv_ave", QA_QUV}, {"ope2_ave", QA_OPE2}};
   for (auto &x : qsingle)
-    if (s == x.nm) return soa(eng->qacc, npq, {x.fld});
-  if (s == "btp_mass_flux_ave") return soa(eng->qacc, npq, {QA_MFX, QA_MFY});
-  if (s == "uvb_ave") return soa(eng->qacc, npq, {QA_UB, QA_VB});
-  if (s == "tau_bot_ave") return soa(eng->qacc, npq, {QA_TBU, QA_TBV});
+    if (s == x.nm) return qacc_f({x.fld});
+  if (s == "btp_mass_flux_ave") return qacc_f({QA_MFX, QA_MFY});
+  if (s == "uvb_ave") return qacc_f({QA_UB, QA_VB});
+  if (s == "tau_bot_ave") return qacc_f({QA_TBU, QA_TBV});
   if (s == "tau_wind_ave") {  // kept in the reference layout (2,npoin_q)
     if ((size_t)n != 2 * npq) return fail(eng, HNUMO_ERR_INVALID, "field size mismatch");
     int rc = fetch(eng->tau_wind_ave, 2 * npq, h);
@@ -676,23 +784,31 @@ int hnumo_get_field(hnumo_engine *eng, const char *name, double *out, int64_t n)
     std::copy(h.begin(), h.end(), out);
     return 0;
   }
-  if (s == "ope2_ave_df") return soa(eng->nacc, npoin, {NA_OPE2});
-  if (s == "uvb_ave_df") return soa(eng->nacc, npoin, {NA_UB, NA_VB});
-  if (s == "graduvb_ave") return soa(eng->nacc, npoin, {NA_G1, NA_G2, NA_G3, NA_G4});
-  if (s == "uvb_face_ave") return soa(eng->facc, FQ, {FA_UL, FA_VL, FA_UR, FA_VR});
-  if (s == "btp_mass_flux_face_ave") return soa(eng->facc, FQ, {FA_MFX, FA_MFY});
-  if (s == "ope_face_ave") return soa(eng->facc, FQ, {FA_OPEL, FA_OPER});
-  if (s == "ope2_face_ave") return soa(eng->facc, FQ, {FA_OPE2L, FA_OPE2R});
-  if (s == "Qu_face_ave") return soa(eng->facc, FQ, {FA_QUU, FA_QUV});
-  if (s == "Qv_face_ave") return soa(eng->facc, FQ, {FA_QVU, FA_QVV});
-  if (s == "H_face_ave") return soa(eng->facc, FQ, {FA_H});
-  if (s == "one_plus_eta_edge_2_ave") return soa(eng->facc, FQ, {FA_OPEE2});
+  if (s == "ope2_ave_df") return nacc_f({NA_OPE2});
+  if (s == "uvb_ave_df") return nacc_f({NA_UB, NA_VB});
+  if (s == "graduvb_ave") return nacc_f({NA_G1, NA_G2, NA_G3, NA_G4});
+  if (s == "uvb_face_ave") return facc_f({FA_UL, FA_VL, FA_UR, FA_VR});
+  if (s == "btp_mass_flux_face_ave") return facc_f({FA_MFX, FA_MFY});
+  if (s == "ope_face_ave") return facc_f({FA_OPEL, FA_OPER});
+  if (s == "ope2_face_ave") return facc_f({FA_OPE2L, FA_OPE2R});
+  if (s == "Qu_face_ave") return facc_f({FA_QUU, FA_QUV});
+  if (s == "Qv_face_ave") return facc_f({FA_QVU, FA_QVV});
+  if (s == "H_face_ave") return facc_f({FA_H});
+  if (s == "one_plus_eta_edge_2_ave") return facc_f({FA_OPEE2});
   if (s == "Quv_face_ave") {  // never accumulated by the reference (mod_rk_mlswe.F90:114-149)
     if ((size_t)n != 2 * FQ) return fail(eng, HNUMO_ERR_INVALID, "field size mismatch");
     std::fill(out, out + n, 0.0);
     return 0;
   }
-  if (s == "graduvb_face_ave") return soa(eng->gfacc, FN, {0, 1, 2, 3, 4, 5, 6, 7});
+  if (s == "graduvb_face_ave") {
+    if ((size_t)n != 8 * FN) return fail(eng, HNUMO_ERR_INVALID, "field size mismatch");
+    int rc = fetch(eng->gfacc, (size_t)8 * 4 * E_ * ngl, h);
+    if (rc) return rc;
+    for (size_t f = 0; f < (size_t)eng->nface; f++)
+      for (int nn = 0; nn < ngl; nn++)
+        for (int c = 0; c < 8; c++) out[(f * ngl + nn) * 8 + c] = h[((size_t)eng->fslotL[f] * 8 + c) * ngl + nn];
+    return 0;
+  }
   if (s == "Q_uu_dp") return soa(eng->qcoef, npq, {QC_QUU});
   if (s == "Q_uv_dp") return soa(eng->qcoef, npq, {QC_QUV});
   if (s == "Q_vv_dp") return soa(eng->qcoef, npq, {QC_QVV});
@@ -773,10 +889,10 @@ int hnumo_time_stage_kernel(hnumo_engine *eng, int nsubcycles, double *ms_kernel
 int hnumo_debug_stage_profile(hnumo_engine *eng, uint64_t *out, int64_t n) {
   if (!eng || !out) return HNUMO_ERR_INVALID;
   if (!eng->stage_prof) return fail(eng, HNUMO_ERR_INVALID, "engine created without HNUMO_STAGE_PROF=1");
-  if (n < (int64_t)eng->nelem * 12) return fail(eng, HNUMO_ERR_INVALID, "buffer too small");
+  if (n < (int64_t)eng->nelem * 32) return fail(eng, HNUMO_ERR_INVALID, "buffer too small");
   HIPCHK(hipSetDevice(eng->device));
   HIPCHK(hipStreamSynchronize(eng->stream));
-  HIPCHK(hipMemcpy(out, eng->stage_prof, (size_t)eng->nelem * 12 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(out, eng->stage_prof, (size_t)eng->nelem * 32 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -11,8 +11,21 @@
 //   face accums      SoA [16][F*NQ]        (owned by the face's left element)
 //   element->face    efaces[e][4], eside[e][4], ebc[e][4], efmap[e][4][NGL],
 //                    enbr_node[e][4][NGL], enbr_e[e][4], enbr_lf[e][4]
-//   gradient traces  gtrace[e][4][4][NGL]  (nodal grad(u_bar) on each element face,
-//                    written by the stage that produced the state, read by the neighbour)
+//   face traces      trace[e][4][8][NGL]   (qb(4) and grad(u_bar)(4) of the neighbour at each
+//                    face node, written by the neighbour's stage into this element's slot)
+//
+// Element-major copies for the barotropic stage kernel (one contiguous record per element,
+// so a stage loads everything it needs with one round of async global->LDS copies):
+//   erec   int  [E][ERS]              faces, side, bc, nbr elem, nbr local face, face->node map,
+//                                     node->(lf*NGL+n) of the <=2 faces through each node
+//   qstatE      [E][QE_N][Q]          W, e_x, e_y, n_x, n_y, coriolis, tau_wind(2), grad_zbot(2), 1/pb
+//   nstatE      [E][NE_N][P]          e_x, e_y, n_x, n_y, w, massinv, pbprime, 1/pbprime
+//   efstat      [E][4][FBLK]          face statics at face quad points (EF_*) and face nodes (EFN_*)
+//   ecoef       [E][4Q + 5P]          per-sub-cycle Q_uu/uv/vv_dp, H_bcl | pbprime_visc, btp_dpp_graduv
+//   efcoef      [E][4][4NQ + 10NGL]   per-sub-cycle face Q_*_edge, H_bcl_edge | btp_graduv_dpp_face
+//   accumulators (element-major)      qacc [E][QA_N][Q], nacc [E][NA_N][P],
+//                                     facc [E][4][FA_N][NQ], gfacc [E][4][8][NGL]
+//                                     (face slots e*4+lf, used by the face's left element only)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -49,11 +62,38 @@ enum FCoef { FC_QUU = 0, FC_QUV, FC_QVV, FC_HBCL, FC_N };
 // face statics at face nodes: [FN_N][F*NGL]
 enum FNStat { FN_NX = 0, FN_NY, FN_W, FN_PBL, FN_PBR, FN_N };
 
+// element-major quad statics order (qstatE): the first QE_KEEP rows live for the whole stage
+enum QStatE { QE_W = 0, QE_EX, QE_EY, QE_NX, QE_NY, QE_COR, QE_TW1, QE_TW2, QE_GZ1, QE_GZ2, QE_OOP, QE_N };
+constexpr int QE_KEEP = 5;
+// element-major nodal statics order (nstatE)
+enum NStatE { NE_EX = 0, NE_EY, NE_NX, NE_NY, NE_W, NE_MINV, NE_PB, NE_OOP, NE_N };
+// element-side face statics block: FS fields at NQ face quad points, then FN fields at NGL nodes
+enum EFStat { EF_NX = 0, EF_NY, EF_W, EF_CL, EF_CR, EF_CLR, EF_CML, EF_CMR, EF_CMLR, EF_OOPE, EF_N };
+enum EFNStat { EFN_NX = 0, EFN_NY, EFN_W, EFN_PBL, EFN_PBR, EFN_N };
+// per-element int record (erec) offsets
+#define EREC_FACE 0
+#define EREC_SIDE 4
+#define EREC_BC 8
+#define EREC_NBE 12
+#define EREC_NBLF 16
+#define EREC_MAP 20
+#define EREC_PF(ngl) (20 + 4 * (ngl))
+#define EREC_SIZE(ngl) (20 + 4 * (ngl) + 2 * (ngl) * (ngl))
+
+// element-major accumulator indices
+#define QACC_I(k, e, q) ((((size_t)(e)) * QA_N + (k)) * Q + (q))
+#define NACC_I(k, e, p) ((((size_t)(e)) * NA_N + (k)) * P + (p))
+#define FACC_I(k, slot, iq) ((((size_t)(slot)) * FA_N + (k)) * NQ + (iq))
+#define GFACC_I(c, slot, n) ((((size_t)(slot)) * 8 + (c)) * NGL + (n))
+
 struct DevMesh {
   int nelem, npoin, npoin_q, nface, ngl, nq, L;
   const int *efaces, *eside, *ebc, *efmap, *enbr_node, *enbr_e, *enbr_lf;
   const int *fnodeL, *fnodeR;     // [F][NGL] global node of face node n, left/right (-1 if none)
   const int *fel, *fer;           // [F] face(7)-1, face(8) (raw: >0 element+1, <=0 code)
+  const int *fslotL, *fslotR;     // [F] element-side slot e*4+lf of the face's left / right element (-1)
+  const int *erec;                // [E][EREC_SIZE]
+  const double *qstatE, *nstatE, *efstat;
   const double *basis;            // psiq[NGL*NQ] dpsiq[NGL*NQ] dpsi[NGL*NGL]
   const double *qstat;            // [QS_N][npoin_q]
   const double *nstat;            // [NS_N][npoin]

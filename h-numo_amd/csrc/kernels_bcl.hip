@@ -147,7 +147,7 @@ __global__ void average_kernel(double *out, const double *a, const double *b, si
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     bcl_coeffs_elem_kernel(DevMesh m, const double *qp, double *qcoef, double *ncoef, double *dpp_graduv,
-                           double *dpprime_visc) {
+                           double *dpprime_visc, double *ecoef) {
   constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BS;
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q;
   __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
@@ -184,6 +184,11 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     qcoef[QC_QUV * (size_t)npq + Iq] = quv;
     qcoef[QC_QVV * (size_t)npq + Iq] = qvv;
     qcoef[QC_HBCL * (size_t)npq + Iq] = hb;
+    double *ec = ecoef + (size_t)e * (4 * Q + 5 * P);  // element-major copy for the stage kernel
+    ec[QC_QUU * Q + q] = quu;
+    ec[QC_QUV * Q + q] = quv;
+    ec[QC_QVV * Q + q] = qvv;
+    ec[QC_HBCL * Q + q] = hb;
   }
   // compute_gradient_uv of (u'_k, v'_k), reference order, one thread per (layer, comp, node)
   for (int t = tid; t < L * 4 * P; t += BS) {
@@ -211,6 +216,9 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     }
     ncoef[NC_PV * (size_t)npoin + I] = pv;
     for (int c = 0; c < 4; c++) ncoef[(NC_D1 + c) * (size_t)npoin + I] = sum[c];
+    double *ec = ecoef + (size_t)e * (4 * Q + 5 * P) + 4 * Q;
+    ec[NC_PV * P + p] = pv;
+    for (int c = 0; c < 4; c++) ec[(NC_D1 + c) * P + p] = sum[c];
   }
 }
 
@@ -220,7 +228,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(64)
     bcl_coeffs_face_kernel(DevMesh m, const double *qf, const double *dpp_graduv, const double *dpprime_visc,
-                           double *fcoef, double *fncoef, double *gdpp_face) {
+                           double *fcoef, double *fncoef, double *gdpp_face, double *efcoef) {
   const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L, npoin = m.npoin;
   __shared__ double s_psiq[NGL * NQ];
   for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
@@ -254,6 +262,14 @@ __global__ void __launch_bounds__(64)
     fcoef[FC_QUV * FQ + fq] = quv;
     fcoef[FC_QVV * FQ + fq] = qvv;
     fcoef[FC_HBCL * FQ + fq] = hb;
+    // element-side copies [slot][4*NQ + 10*NGL] for both elements of the face
+    constexpr int EFC = 4 * NQ + 10 * NGL;
+    const int sl = m.fslotL[f], sr = m.fslotR[f];
+    const double vals[4] = {quu, quv, qvv, hb};
+    for (int c = 0; c < 4; c++) {
+      efcoef[(size_t)sl * EFC + c * NQ + iq] = vals[c];
+      if (sr >= 0) efcoef[(size_t)sr * EFC + c * NQ + iq] = vals[c];
+    }
   } else if (tid >= 32 && tid < 32 + NGL) {
     const int n = tid - 32, er = m.fer[f];
     const size_t fn = (size_t)f * NGL + n;
@@ -288,6 +304,12 @@ __global__ void __launch_bounds__(64)
       }
     }
     for (int c = 0; c < 10; c++) fncoef[(size_t)c * FN + fn] = bsum[c];
+    constexpr int EFC = 4 * NQ + 10 * NGL;
+    const int sl = m.fslotL[f], sr = m.fslotR[f];
+    for (int c = 0; c < 10; c++) {
+      efcoef[(size_t)sl * EFC + 4 * NQ + c * NGL + n] = bsum[c];
+      if (sr >= 0) efcoef[(size_t)sr * EFC + 4 * NQ + c * NGL + n] = bsum[c];
+    }
   }
 }
 
@@ -307,9 +329,9 @@ __global__ void __launch_bounds__(64)
     const int iq = tid;
     const size_t fq = (size_t)f * NQ + iq;
     double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
-    double qbl0 = facc[FA_OPEL * FQ + fq], qbr0 = facc[FA_OPER * FQ + fq];
-    double qbl1 = facc[FA_UL * FQ + fq], qbr1 = facc[FA_UR * FQ + fq];
-    double qbl2 = facc[FA_VL * FQ + fq], qbr2 = facc[FA_VR * FQ + fq];
+    double qbl0 = facc[FACC_I(FA_OPEL, m.fslotL[f], iq)], qbr0 = facc[FACC_I(FA_OPER, m.fslotL[f], iq)];
+    double qbl1 = facc[FACC_I(FA_UL, m.fslotL[f], iq)], qbr1 = facc[FACC_I(FA_UR, m.fslotL[f], iq)];
+    double qbl2 = facc[FACC_I(FA_VL, m.fslotL[f], iq)], qbr2 = facc[FACC_I(FA_VR, m.fslotL[f], iq)];
     double su = 0.0, sv = 0.0;
     for (int k = 0; k < L; k++) {
       double ql[3] = {0, 0, 0}, qr[3] = {0, 0, 0};
@@ -349,8 +371,8 @@ __global__ void __launch_bounds__(64)
     const int iq = tid, er = m.fer[f];
     const size_t fq = (size_t)f * NQ + iq;
     double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
-    double d1 = facc[FA_MFX * FQ + fq] - slmf_face[0 * FQ + fq];
-    double d2 = facc[FA_MFY * FQ + fq] - slmf_face[1 * FQ + fq];
+    double d1 = facc[FACC_I(FA_MFX, m.fslotL[f], iq)] - slmf_face[0 * FQ + fq];
+    double d2 = facc[FACC_I(FA_MFY, m.fslotL[f], iq)] - slmf_face[1 * FQ + fq];
     double pbl = m.fstat[FS_PBL * FQ + fq], pbr = m.fstat[FS_PBR * FQ + fq];
     for (int k = 0; k < L; k++) {
       double ql = 0.0, qr = 0.0;
@@ -405,8 +427,8 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
   for (int q = tid; q < Q; q += BS) {
     const int iq = q % NQ, jq = q / NQ;
     const size_t Iq = (size_t)e * Q + q;
-    double qb0 = qacc[QA_OPE * (size_t)npq + Iq], qb1 = qacc[QA_UB * (size_t)npq + Iq],
-           qb2 = qacc[QA_VB * (size_t)npq + Iq];
+    double qb0 = qacc[QACC_I(QA_OPE, e, q)], qb1 = qacc[QACC_I(QA_UB, e, q)],
+           qb2 = qacc[QACC_I(QA_VB, e, q)];
     double su = 0.0, sv = 0.0;
     for (int k = 0; k < L; k++) {
       double qq[3] = {0.0, 0.0, 0.0};
@@ -482,8 +504,8 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     const int iq = q % NQ, jq = q / NQ;
     const size_t Iq = (size_t)e * Q + q;
     double pb = m.qstat[QS_PB * (size_t)npq + Iq];
-    double dx = qacc[QA_MFX * (size_t)npq + Iq] - slmf[0 * (size_t)npq + Iq];
-    double dy = qacc[QA_MFY * (size_t)npq + Iq] - slmf[1 * (size_t)npq + Iq];
+    double dx = qacc[QACC_I(QA_MFX, e, q)] - slmf[0 * (size_t)npq + Iq];
+    double dy = qacc[QACC_I(QA_MFY, e, q)] - slmf[1 * (size_t)npq + Iq];
     for (int k = 0; k < L; k++) {
       double dp = 0.0;
       for (int mm = 0; mm < NGL; mm++)
@@ -539,9 +561,9 @@ __global__ void __launch_bounds__(64)
     const size_t fq = (size_t)f * NQ + iq;
     const double *alpha = m.alpha;
     double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
-    double qbl0 = facc[FA_OPEL * FQ + fq], qbr0 = facc[FA_OPER * FQ + fq];
-    double qbl1 = facc[FA_UL * FQ + fq], qbr1 = facc[FA_UR * FQ + fq];
-    double qbl2 = facc[FA_VL * FQ + fq], qbr2 = facc[FA_VR * FQ + fq];
+    double qbl0 = facc[FACC_I(FA_OPEL, m.fslotL[f], iq)], qbr0 = facc[FACC_I(FA_OPER, m.fslotL[f], iq)];
+    double qbl1 = facc[FACC_I(FA_UL, m.fslotL[f], iq)], qbr1 = facc[FACC_I(FA_UR, m.fslotL[f], iq)];
+    double qbl2 = facc[FACC_I(FA_VL, m.fslotL[f], iq)], qbr2 = facc[FACC_I(FA_VR, m.fslotL[f], iq)];
     double ql[MAXL][3], qr[MAXL][3], udpl[MAXL], udpr[MAXL], vdpl[MAXL], vdpr[MAXL];
     double udpf[2][MAXL], vdpf[2][MAXL], Hf[2][MAXL];
     for (int k = 0; k < L; k++) {
@@ -580,8 +602,8 @@ __global__ void __launch_bounds__(64)
     for (int k = 0; k < L; k++) s2 = s2 + udpf[1][k];
     for (int k = 0; k < L; k++) s3 = s3 + vdpf[0][k];
     for (int k = 0; k < L; k++) s4 = s4 + vdpf[1][k];
-    double uu_def = facc[FA_QUU * FQ + fq] - s1, uv_def = facc[FA_QUV * FQ + fq] - s2;
-    double vu_def = facc[FA_QVU * FQ + fq] - s3, vv_def = facc[FA_QVV * FQ + fq] - s4;
+    double uu_def = facc[FACC_I(FA_QUU, m.fslotL[f], iq)] - s1, uv_def = facc[FACC_I(FA_QUV, m.fslotL[f], iq)] - s2;
+    double vu_def = facc[FACC_I(FA_QVU, m.fslotL[f], iq)] - s3, vv_def = facc[FACC_I(FA_QVV, m.fslotL[f], iq)] - s4;
     double sl = 0, sr = 0;
     for (int k = 0; k < L; k++) sl = sl + (fabs(udpl[k]) + eps1);
     for (int k = 0; k < L; k++) sr = sr + (fabs(udpr[k]) + eps1);
@@ -603,12 +625,12 @@ __global__ void __launch_bounds__(64)
     // H_r at the face (layer-overlap pressure, :627-707)
     double pf[2][MAXL + 1], zf[2][MAXL + 1], pep[MAXL + 1], pem[MAXL + 1], zep[MAXL + 1], zem[MAXL + 1];
     for (int k = 0; k <= L; k++) zf[0][k] = zf[1][k] = pf[0][k] = pf[1][k] = zep[k] = zem[k] = pep[k] = pem[k] = 0.0;
-    double ope_l = sqrt(facc[FA_OPE2L * FQ + fq]), ope_r = sqrt(facc[FA_OPE2R * FQ + fq]);
+    double ope_l = sqrt(facc[FACC_I(FA_OPE2L, m.fslotL[f], iq)]), ope_r = sqrt(facc[FACC_I(FA_OPE2R, m.fslotL[f], iq)]);
     for (int k = 1; k <= L; k++) {
       pf[0][k] = pf[0][k - 1] + ope_l * ql[k - 1][0];
       pf[1][k] = pf[1][k - 1] + ope_r * qr[k - 1][0];
     }
-    double ope_e = sqrt(facc[FA_OPEE2 * FQ + fq]);
+    double ope_e = sqrt(facc[FACC_I(FA_OPEE2, m.fslotL[f], iq)]);
     double zbl = m.fstat[FS_ZBL * FQ + fq], zbr = m.fstat[FS_ZBR * FQ + fq];
     zf[0][L] = zbl;
     zf[1][L] = zbr;
@@ -671,7 +693,7 @@ __global__ void __launch_bounds__(64)
         Hf[1][k] = Hf[1][k] + Hc2;
       }
     }
-    double hfa = facc[FA_H * FQ + fq];
+    double hfa = facc[FACC_I(FA_H, m.fslotL[f], iq)];
     for (int sd = 0; sd < 2; sd++) {
       double weight = 1.0, acc = 0.0;
       for (int k = 0; k < L; k++) acc = acc + Hf[sd][k];
@@ -696,9 +718,9 @@ __global__ void __launch_bounds__(64)
     for (int k = 0; k < L; k++) {
       double fl[4], fr[4];
       for (int iv = 0; iv < 4; iv++) {
-        fl[iv] = gdpp_face[((size_t)k * 10 + 4) * FN + fn] * gfacc[(size_t)iv * FN + fn] +
+        fl[iv] = gdpp_face[((size_t)k * 10 + 4) * FN + fn] * gfacc[GFACC_I(iv, m.fslotL[f], n)] +
                  gdpp_face[((size_t)k * 10 + iv) * FN + fn];
-        fr[iv] = gdpp_face[((size_t)k * 10 + 9) * FN + fn] * gfacc[(size_t)(4 + iv) * FN + fn] +
+        fr[iv] = gdpp_face[((size_t)k * 10 + 9) * FN + fn] * gfacc[GFACC_I(4 + iv, m.fslotL[f], n)] +
                  gdpp_face[((size_t)k * 10 + 5 + iv) * FN + fn];
       }
       double qum0 = alpha * fl[0] + beta * fr[0], qum1 = alpha * fl[1] + beta * fr[1];
@@ -762,7 +784,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
   for (int p = tid; p < P; p += BS) {
     const size_t I = (size_t)e * P + p;
     double z = m.nstat[NS_ZB * (size_t)npoin + I];
-    double so = sqrt(nacc[NA_OPE2 * (size_t)npoin + I]);
+    double so = sqrt(nacc[NACC_I(NA_OPE2, e, p)]);
     s_z[L][p] = z;
     for (int k = L - 1; k >= 0; k--) {
       z = z + (m.alpha[k] / g) * (so * s_qp[k][0][p]);
@@ -771,7 +793,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     for (int k = 0; k < L; k++) {
       double d = dpprime_visc[(size_t)k * npoin + I];
       for (int c = 0; c < 4; c++)
-        s_qq[k][c][p] = d * nacc[(NA_G1 + c) * (size_t)npoin + I] + dpp_graduv[((size_t)k * 4 + c) * npoin + I];
+        s_qq[k][c][p] = d * nacc[NACC_I((NA_G1 + c), e, p)] + dpp_graduv[((size_t)k * 4 + c) * npoin + I];
     }
   }
   __syncthreads();
@@ -782,9 +804,9 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     const size_t Iq = (size_t)e * Q + q;
     double qpv[MAXL][3], tuu[MAXL], tvv[MAXL], p_tmp[MAXL + 1], H_tmp[MAXL], u_udp[MAXL], v_vdp[MAXL];
     double u_vdp[2][MAXL], gz[2][MAXL + 1];
-    double qb0 = qacc[QA_OPE * (size_t)npq + Iq], qb1 = qacc[QA_UB * (size_t)npq + Iq],
-           qb2 = qacc[QA_VB * (size_t)npq + Iq];
-    double so2 = sqrt(qacc[QA_OPE2 * (size_t)npq + Iq]);
+    double qb0 = qacc[QACC_I(QA_OPE, e, q)], qb1 = qacc[QACC_I(QA_UB, e, q)],
+           qb2 = qacc[QACC_I(QA_VB, e, q)];
+    double so2 = sqrt(qacc[QACC_I(QA_OPE2, e, q)]);
     p_tmp[0] = 0.0;
     for (int k = 0; k < L; k++) tuu[k] = tvv[k] = 0.0;
     for (int k = 0; k < L; k++) {
@@ -828,17 +850,17 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     for (int k = 0; k < L; k++) su = su + u_udp[k];
     for (int k = 0; k < L; k++) suv = suv + u_vdp[0][k];
     for (int k = 0; k < L; k++) sv = sv + v_vdp[k];
-    double uu_def = qacc[QA_QU * (size_t)npq + Iq] - su;
-    double uv_def = qacc[QA_QUV * (size_t)npq + Iq] - suv;
-    double vv_def = qacc[QA_QV * (size_t)npq + Iq] - sv;
+    double uu_def = qacc[QACC_I(QA_QU, e, q)] - su;
+    double uv_def = qacc[QACC_I(QA_QUV, e, q)] - suv;
+    double vv_def = qacc[QACC_I(QA_QV, e, q)] - sv;
     for (int k = 0; k < L; k++) stu = stu + tuu[k];
     for (int k = 0; k < L; k++) stv = stv + tvv[k];
     for (int k = 0; k < L; k++) sH = sH + H_tmp[k];
     double oosu = 1.0 / stu, oosv = 1.0 / stv;
     double weight = 1.0;
-    if (sH > 0.0) weight = qacc[QA_H * (size_t)npq + Iq] / sH;
+    if (sH > 0.0) weight = qacc[QACC_I(QA_H, e, q)] / sH;
     double tw1 = m.qstat[QS_TW1 * (size_t)npq + Iq], tw2 = m.qstat[QS_TW2 * (size_t)npq + Iq];
-    double tb1 = qacc[QA_TBU * (size_t)npq + Iq], tb2 = qacc[QA_TBV * (size_t)npq + Iq];
+    double tb1 = qacc[QACC_I(QA_TBU, e, q)], tb2 = qacc[QACC_I(QA_TBV, e, q)];
     double pb = m.qstat[QS_PB * (size_t)npq + Iq];
     double ppt0 = 0.0;
     for (int k = 0; k < L; k++) {

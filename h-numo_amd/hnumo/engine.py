@@ -127,10 +127,10 @@ class Engine:
         return k.value
 
     def stage_profile(self):
-        n = self.dims["nelem"] * 12
+        n = self.dims["nelem"] * 32
         out = np.zeros(n, dtype=np.uint64)
         self._check(lib().hnumo_debug_stage_profile(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), n))
-        return out.reshape(-1, 12)
+        return out.reshape(-1, 32)
 
     def _destroy(self):
         if getattr(self, "h", None) is not None and self.h.value:

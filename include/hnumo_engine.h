@@ -170,7 +170,7 @@ int hnumo_bench_steps(hnumo_engine *eng, int nsteps, double *ms_total,
  * current device state (qb is not modified).                                          */
 int hnumo_time_stage_kernel(hnumo_engine *eng, int nsubcycles, double *ms_kernel_avg);
 
-/* Diagnostics: per-element phase clocks of the last stage launch, [nelem][12] uint64
+/* Diagnostics: per-element phase clocks of the last stage launch, [nelem][32] uint64
  * (engine created with HNUMO_STAGE_PROF=1 in the environment).                        */
 int hnumo_debug_stage_profile(hnumo_engine *eng, uint64_t *out, int64_t n);
 

@@ -1,4 +1,4 @@
-"""Per-phase clock breakdown of btp_stage_kernel (HNUMO_STAGE_PROF=1). GPU only."""
+"""Per-phase clock breakdown of btp_stage_kernel (HNUMO_STAGE_PROF=1). GPU only; diagnostics."""
 import os
 import sys
 
@@ -16,18 +16,33 @@ q, qb, qp = eng.state()
 eng.ti_rk_bcl(q, qb, qp)
 ms = eng.time_stage_kernel(1)
 pr = eng.stage_profile().astype(np.int64)
-d = np.diff(pr[:, :6], axis=1)
-names = ["A loads", "B quad/grad/face", "D terms+sums", "E1 update", "E2 out+traces"]
 print(f"{cfg}: stage avg {ms*1e3:.1f} us (direct events)")
-for i, n in enumerate(names):
-    print(f"  {n:14s} mean {d[:, i].mean():9.0f} clk  max {d[:, i].max():9.0f}")
-dk = np.diff(np.concatenate([pr[:, 2:3], pr[:, 6:10]], axis=1), axis=1)
-for k in range(dk.shape[1]):
-    if dk[:, k].mean() > 0:
-        print(f"    D{k:<12d} mean {dk[:, k].mean():9.0f} clk")
+for name, a, b in [("A loads", 0, 1), ("B", 1, 2), ("D all", 2, 3), ("E1 update", 3, 4), ("E2 out", 4, 5)]:
+    d = pr[:, b] - pr[:, a]
+    print(f"  {name:12s} mean {d.mean():8.0f} clk  max {d.max():8.0f}")
+prev = pr[:, 2]
+for k in range(6):
+    cur = pr[:, 6 + k]
+    if (cur > 0).all():
+        print(f"    D{k}        mean {(cur - prev).mean():8.0f} clk")
+        prev = cur
+for w in range(4):
+    print(f"    B wave{w} done mean {(pr[:, 12 + w] - pr[:, 1]).mean():8.0f} clk")
 tot = pr[:, 5] - pr[:, 0]
 print(f"  total per block mean {tot.mean():.0f} clk, max {tot.max():.0f}")
-w0, w1 = pr[:, 10], pr[:, 11]
+w0, w1 = pr[:, 30], pr[:, 31]
 t0 = w0.min()
-print(f"  wall (100MHz ticks): block start spread {np.percentile(w0 - t0, [0, 50, 90, 100])}, "
+print(f"  wall (100MHz ticks): start spread {np.percentile(w0 - t0, [0, 50, 90, 100])}, "
       f"block dur mean {(w1 - w0).mean():.0f} max {(w1 - w0).max():.0f}, span {(w1.max() - t0)}")
+hw = pr[:, 16:20]
+simd = (hw >> 4) & 3
+cu = (hw >> 8) & 15
+se = (hw >> 13) & 7
+xcc = pr[:, 20] & 15
+print("  placement (first 12 blocks): xcc, se, cu, simd of waves 0-3")
+for e in list(range(8)) + [256, 257, 512, 513]:
+    if e < len(pr):
+        print(f"    blk {e:4d}: xcc {xcc[e]} se {se[e, 0]} cu {cu[e, 0]:2d} simd {simd[e].tolist()}")
+key = xcc * 1000 + se[:, 0] * 100 + cu[:, 0]
+u, c = np.unique(key, return_counts=True)
+print(f"  distinct CUs used {len(u)}, blocks per CU: {np.bincount(c).tolist()}")
