@@ -31,6 +31,14 @@ BUNDLE_ARRAYS = [
     ("q_df", "f8", "3,npoin,nlayers"), ("qb_df", "f8", "4,npoin"), ("qprime_df", "f8", "3,npoin,nlayers"),
 ]
 
+# optional trailer (dropin_driver): the per-point metrics of mod_metrics the bridge reads
+METRIC_ARRAYS = [
+    ("ksiq_x", "f8", "nq,nq,nelem"), ("ksiq_y", "f8", "nq,nq,nelem"), ("etaq_x", "f8", "nq,nq,nelem"),
+    ("etaq_y", "f8", "nq,nq,nelem"), ("jacq", "f8", "nq,nq,nelem"),
+    ("ksi_x", "f8", "ngl,ngl,nelem"), ("ksi_y", "f8", "ngl,ngl,nelem"), ("eta_x", "f8", "ngl,ngl,nelem"),
+    ("eta_y", "f8", "ngl,ngl,nelem"), ("jac", "f8", "ngl,ngl,nelem"),
+]
+
 # engine / oracle fields copied out for parity (mod_variables), with shapes
 FIELDS = [
     ("ope_ave", "npoin_q"), ("H_ave", "npoin_q"), ("Qu_ave", "npoin_q"), ("Qv_ave", "npoin_q"),
@@ -62,7 +70,8 @@ def shape_of(expr: str, d: dict):
     return tuple(int(eval(t, {}, d)) for t in expr.split(","))
 
 
-def write_bundle(path: str, case, mode: str, nsteps: int = 1):
+def write_bundle(path: str, case, mode: str, nsteps: int = 1, metrics: bool = False):
+    """metrics=True appends METRIC_ARRAYS (read only by oracle/_ref/dropin_driver)."""
     S = case.scalars
     d = dims(case)
     hi = np.zeros(16, dtype="<i4")
@@ -73,7 +82,7 @@ def write_bundle(path: str, case, mode: str, nsteps: int = 1):
     with open(path, "wb") as fh:
         fh.write(hi.tobytes())
         fh.write(hd.tobytes())
-        for name, dt, shp in BUNDLE_ARRAYS:
+        for name, dt, shp in BUNDLE_ARRAYS + (METRIC_ARRAYS if metrics else []):
             a = np.asarray(case.arrays[name])
             want = shape_of(shp, d)
             assert a.size == int(np.prod(want)), (name, a.shape, want)

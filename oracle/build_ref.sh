@@ -40,6 +40,21 @@ if [ $left -ne 0 ]; then
   echo "reference build failed; see $OBJ/*.err" >&2; exit 1
 fi
 $FC $FLAGS -I. -c "$HERE/ref_driver.F90" -o ref_driver.o
-$FC -O2 -o "$OUT/ref_driver" ref_driver.o $(ls *.o | grep -v '^ref_driver.o$') \
+REFOBJ=$(ls *.o | grep -v -e '^ref_driver.o$' -e '^dropin_driver.o$' -e '^hnumo_')
+$FC -O2 -o "$OUT/ref_driver" ref_driver.o $REFOBJ \
     -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi -Wl,--gc-sections
 echo "built $OUT/ref_driver"
+
+# The drop-in: the same harness with ti_rk_bcl replaced by the Fortran bridge to the HIP
+# engine (include/hnumo_engine.f90 + h-numo_amd/fortran/hnumo_bridge.F90).  Runs on a GPU.
+REPO="$(cd "$HERE/.." && pwd)"
+ENGINE="$REPO/h-numo_amd/libhnumo_engine.so"
+if [ -f "$ENGINE" ]; then
+  $FC $FLAGS -I. -c "$REPO/include/hnumo_engine.f90" -o hnumo_engine_f.o
+  $FC $FLAGS -I. -c "$REPO/h-numo_amd/fortran/hnumo_bridge.F90" -o hnumo_bridge.o
+  $FC $FLAGS -DHNUMO_DROPIN -I. -c "$HERE/ref_driver.F90" -o dropin_driver.o
+  $FC -O2 -o "$OUT/dropin_driver" dropin_driver.o hnumo_bridge.o hnumo_engine_f.o $REFOBJ \
+      -L"$REPO/h-numo_amd" -Wl,-rpath,'$ORIGIN/../../h-numo_amd' -lhnumo_engine \
+      -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi -Wl,--gc-sections
+  echo "built $OUT/dropin_driver"
+fi

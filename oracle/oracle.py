@@ -103,22 +103,31 @@ class Oracle:
             self.h = C.c_void_p()
 
 
-def run_reference(case, mode: str, nsteps: int = 1, workdir: str | None = None) -> dict:
-    """Run the reference Fortran (oracle/_ref/ref_driver) on `case`; returns its outputs."""
-    if not os.path.exists(REF_DRIVER):
-        raise FileNotFoundError(REF_DRIVER)
+DROPIN_DRIVER = os.path.join(os.path.dirname(REF_DRIVER), "dropin_driver")
+
+
+def run_reference(case, mode: str, nsteps: int = 1, workdir: str | None = None, dropin: bool = False) -> dict:
+    """Run the reference Fortran (oracle/_ref/ref_driver) on `case`; returns its outputs.
+
+    dropin=True runs oracle/_ref/dropin_driver instead: the same Fortran harness with
+    ti_rk_bcl replaced by the HIP engine through the Fortran bridge (mode "step" only; GPU)."""
+    driver = DROPIN_DRIVER if dropin else REF_DRIVER
+    if not os.path.exists(driver):
+        raise FileNotFoundError(driver)
     tmp = workdir or tempfile.mkdtemp(prefix="hnumo_ref_")
     fin = os.path.join(tmp, "bundle.bin")
     fout = os.path.join(tmp, "out.bin")
-    _bundle.write_bundle(fin, case, mode, nsteps)
+    _bundle.write_bundle(fin, case, mode, nsteps, metrics=dropin)
     env = dict(os.environ)
     def _stack():
         # the reference keeps npoin-sized automatic arrays on the stack (e.g. ti_rk_bcl.F90:35-38)
         import resource
         resource.setrlimit(resource.RLIMIT_STACK, (resource.RLIM_INFINITY, resource.RLIM_INFINITY))
 
-    subprocess.run([REF_DRIVER, fin, fout], check=True, env=env, cwd=tmp, preexec_fn=_stack,
-                   stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    r = subprocess.run([driver, fin, fout], env=env, cwd=tmp, preexec_fn=_stack,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"{os.path.basename(driver)} failed ({r.returncode}): {r.stdout[-2000:]} {r.stderr[-2000:]}")
     out = _bundle.read_outputs(fout, case, mode)
     if workdir is None:
         for f in (fin, fout):

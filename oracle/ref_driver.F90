@@ -12,6 +12,12 @@
 ! halo routines run with empty neighbour lists.
 !
 ! usage: ref_driver <bundle.bin> <outputs.bin>
+!
+! Built a second time with -DHNUMO_DROPIN as oracle/_ref/dropin_driver: the same set-up,
+! but mode 3 calls hnumo_bridge_ti_rk_bcl (h-numo_amd/fortran/hnumo_bridge.F90, i.e. the
+! HIP engine through the Fortran ISO_C_BINDING module) where the reference calls
+! ti_rk_bcl -- the drop-in exactly as INTEGRATION.md describes it.  Its bundle carries the
+! per-point metrics (mod_metrics) the bridge reads.
 program ref_driver
 
     use mpi
@@ -24,6 +30,11 @@ program ref_driver
     use mod_face, only: normal_vector, normal_vector_q, jac_face, jac_faceq, imapl, imapr, &
         imapl_q, imapr_q, face_send
     use mod_metrics, only: massinv
+#ifdef HNUMO_DROPIN
+    use mod_metrics, only: ksiq_x, ksiq_y, etaq_x, etaq_y, jacq, ksi_x, ksi_y, eta_x, eta_y, jac
+    use hnumo_bridge, only: hnumo_bridge_init, hnumo_bridge_ti_rk_bcl, hnumo_bridge_fetch_averages, &
+        hnumo_bridge_finalize
+#endif
     use mod_constants, only: gravity
     use mod_initial, only: psih, dpsidx, dpsidy, indexq, wjac, psih_df, dpsidx_df, dpsidy_df, &
         index_df, wjac_df, pbprime, pbprime_df, one_over_pbprime, one_over_pbprime_df, &
@@ -144,6 +155,15 @@ program ref_driver
 
     allocate(q_df(3, npoin, nlayers), qb_df(4, npoin), qprime_df(3, npoin, nlayers), rhs(3, npoin))
     read(u) q_df; read(u) qb_df; read(u) qprime_df
+#ifdef HNUMO_DROPIN
+    ! ---- mod_metrics per-point metrics (jacq = wjac, jac = wjac_df: Tensor_product.F90:56,91)
+    allocate(ksiq_x(nq, nq, 1, nelem), ksiq_y(nq, nq, 1, nelem), etaq_x(nq, nq, 1, nelem))
+    allocate(etaq_y(nq, nq, 1, nelem), jacq(nq, nq, 1, nelem))
+    allocate(ksi_x(ngl, ngl, 1, nelem), ksi_y(ngl, ngl, 1, nelem), eta_x(ngl, ngl, 1, nelem))
+    allocate(eta_y(ngl, ngl, 1, nelem), jac(ngl, ngl, 1, nelem))
+    read(u) ksiq_x; read(u) ksiq_y; read(u) etaq_x; read(u) etaq_y; read(u) jacq
+    read(u) ksi_x; read(u) ksi_y; read(u) eta_x; read(u) eta_y; read(u) jac
+#endif
     close(u)
     rhs = 0
 
@@ -177,12 +197,24 @@ program ref_driver
             call ti_barotropic_ssprk_mlswe(qb_df, qprime_df)
         end if
     case (3)
+#ifdef HNUMO_DROPIN
+        call hnumo_bridge_init(0)
+        t0 = mpi_wtime()
+        do istep = 1, nsteps
+            call hnumo_bridge_ti_rk_bcl(q_df, qb_df, qprime_df)
+        end do
+        t1 = mpi_wtime()
+        call hnumo_bridge_fetch_averages()
+        call hnumo_bridge_finalize()
+        write(*, '(A,ES24.16)') 'DROPIN_TIME ', t1 - t0
+#else
         t0 = mpi_wtime()
         do istep = 1, nsteps
             call ti_rk_bcl(q_df, qb_df, qprime_df)
         end do
         t1 = mpi_wtime()
         write(*, '(A,ES24.16)') 'REF_TIME ', t1 - t0
+#endif
     case default
         stop 'unknown mode'
     end select
