@@ -6,6 +6,6 @@ OUT="$HERE/../libhnumo_engine.so"
 HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
 "$HIPCC" --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -Wno-unused-variable -Wno-unused-function \
   -munsafe-fp-atomics -ffp-contract=off \
-  -o "$OUT.tmp" "$HERE/engine.hip"
+  -o "$OUT.tmp" "$HERE/engine.hip" -lrccl
 mv "$OUT.tmp" "$OUT"
 echo "built $OUT"

@@ -6,11 +6,16 @@
 // ~20 baroclinic kernels) is captured once into a hipGraph and replayed.
 #include <hip/hip_runtime.h>
 
+#include <rccl/rccl.h>
+
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/hnumo_engine.h"
@@ -29,8 +34,23 @@ using namespace hnumo;
     }                                                                                      \
   } while (0)
 
+struct LocalGroup;
+
+// one neighbour rank of the ghost-layer halo (h-numo_amd/hnumo/partition.py)
+struct Neighbour {
+  int rank = -1, nsend = 0, nrecv = 0;
+  int *d_send = nullptr, *d_recv = nullptr;  // 0-based local element ids
+  double *sbuf = nullptr, *rbuf = nullptr;
+};
+
 struct hnumo_engine {
   int device = 0;
+  // multi-rank: 0 single, 1 local group (one process, shared stream), 2 RCCL
+  int comm_mode = 0, rank = 0, nranks = 1, nelem_owned = 0;
+  std::vector<Neighbour> nbh;
+  ncclComm_t comm = nullptr;
+  LocalGroup *group = nullptr;
+  bool own_stream = true;
   std::string err;
   hipStream_t stream = nullptr;
   DevMesh m{};
@@ -49,7 +69,7 @@ struct hnumo_engine {
   double *qcoef, *ncoef, *fcoef, *fncoef, *dpp_graduv, *dpprime_visc, *gdpp_face;
   double *ecoef, *efcoef;                   // element-major copies for the stage kernel
   double *qstatE, *nstatE, *efstat;         // element-major statics for the stage kernel
-  std::vector<int> fslotL;                  // host copy: face -> left element slot e*4+lf
+  std::vector<int> fslotA;                  // host copy: face -> slot holding its averages
   // accumulators
   double *qacc, *facc, *nacc, *gfacc, *tau_wind_ave;
   // baroclinic scratch
@@ -62,7 +82,7 @@ struct hnumo_engine {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // events recorded inside the captured step around the corrector sub-cycle's stage kernels
   hipEvent_t evk0 = nullptr, evk1 = nullptr;
-  bool capturing = false, kernel_events = false;
+  bool capturing = false, kernel_events = false, no_graph = false;
   unsigned long long *stage_prof = nullptr;  // HNUMO_STAGE_PROF=1: per-element phase clocks
 };
 
@@ -83,10 +103,13 @@ template <int NGL, int NQ>
 struct Launch {
   static constexpr int BSE = ((NQ * NQ + 63) / 64) * 64;
   static void stage(hnumo_engine *e, const StageArgs &a) {
-    hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ>), dim3(e->nelem), dim3(StageCfg<NGL, NQ>::BS), 0, e->stream, a);
+    hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(StageCfg<NGL, NQ>::BS), 0, e->stream,
+                       a);
   }
-  static void grad_trace(hnumo_engine *e, const double *qb, double *gt) {
-    hipLaunchKernelGGL((grad_trace_kernel<NGL, NQ>), dim3(e->nelem), dim3(64), 0, e->stream, e->m, qb, gt);
+  // face traces of elements [e0, e0+n) into their neighbours' slots
+  static void grad_trace(hnumo_engine *e, const double *qb, double *gt, int e0, int n) {
+    if (n > 0)
+      hipLaunchKernelGGL((grad_trace_kernel<NGL, NQ>), dim3(n), dim3(64), 0, e->stream, e->m, qb, gt, e0);
   }
   static void extract(hnumo_engine *e, const double *qp, double *qf, int only_dp) {
     size_t n = (size_t)e->nface * NGL;
@@ -99,22 +122,24 @@ struct Launch {
     hipLaunchKernelGGL((bcl_coeffs_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf,
                        e->dpp_graduv, e->dpprime_visc, e->fcoef, e->fncoef, e->gdpp_face, e->efcoef);
   }
-  static void mass_cons(hnumo_engine *e, const double *qp, const double *qf, double *q, double *qp_out,
-                        int finalize_dp) {
+  // layer mass update (owned elements); produces dp' (e->dpp) for the consistency step
+  static void mass(hnumo_engine *e, const double *qp, const double *qf, double *q) {
     hipLaunchKernelGGL((mass_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
                        e->fmass, e->slmf_face);
-    hipLaunchKernelGGL((mass_elem_kernel<NGL, NQ>), dim3(e->nelem), dim3(BSE), 0, e->stream, e->m, qp, e->qacc,
-                       e->fmass, q, e->slmf, e->dpp, e->neg_flag);
+    hipLaunchKernelGGL((mass_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(BSE), 0, e->stream, e->m, qp,
+                       e->qacc, e->fmass, q, e->slmf, e->dpp, e->neg_flag);
+  }
+  static void cons(hnumo_engine *e, double *q, double *qp_out, int finalize_dp) {
     hipLaunchKernelGGL((cons_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, e->dpp,
                        e->facc, e->slmf_face, e->fcons);
-    hipLaunchKernelGGL((cons_elem_kernel<NGL, NQ>), dim3(e->nelem), dim3(BSE), 0, e->stream, e->m, e->dpp, e->qacc,
-                       e->slmf, e->fcons, q, qp_out, finalize_dp);
+    hipLaunchKernelGGL((cons_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(BSE), 0, e->stream, e->m, e->dpp,
+                       e->qacc, e->slmf, e->fcons, q, qp_out, finalize_dp);
   }
   static void momentum(hnumo_engine *e, const double *qf, const double *qp_in, const double *qb, double *q,
                        double *qp_out, int mode) {
     hipLaunchKernelGGL((mom_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
                        e->gdpp_face, e->gfacc, e->momL, e->momR, e->lapf);
-    hipLaunchKernelGGL((mom_elem_kernel<NGL, NQ>), dim3(e->nelem), dim3(BSE), 0, e->stream, e->m, qp_in, e->qacc,
+    hipLaunchKernelGGL((mom_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(BSE), 0, e->stream, e->m, qp_in, e->qacc,
                        e->nacc, e->dpp_graduv, e->dpprime_visc, e->momL, e->momR, e->lapf, qb, q, qp_out, mode);
   }
 };
@@ -165,6 +190,88 @@ __global__ void qprime_final_kernel(double *qp, const double *qp2, const double 
   }
 }
 
+// ------------------------------------------------------------------ ghost exchange
+// Element block of a nodal array: for each of `nblk` blocks (layers) at `blk_stride`, the
+// element's P*ncomp contiguous doubles (qb(4,npoin): ncomp 4, 1 block; qprime(3,npoin,L):
+// ncomp 3, L blocks of stride 3*npoin; dp'(npoin,L): ncomp 1, L blocks of stride npoin).
+__global__ void ghost_pack_kernel(double *buf, const double *base, const int *elems, int nel, int per, int nblk,
+                                  size_t stride) {
+  const size_t n = (size_t)nel * nblk * per, s = (size_t)gridDim.x * blockDim.x;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += s) {
+    const int i = (int)(t / ((size_t)nblk * per)), r = (int)(t % ((size_t)nblk * per)), b = r / per, k = r % per;
+    buf[t] = base[b * stride + (size_t)elems[i] * per + k];
+  }
+}
+__global__ void ghost_unpack_kernel(double *base, const double *buf, const int *elems, int nel, int per, int nblk,
+                                    size_t stride) {
+  const size_t n = (size_t)nel * nblk * per, s = (size_t)gridDim.x * blockDim.x;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += s) {
+    const int i = (int)(t / ((size_t)nblk * per)), r = (int)(t % ((size_t)nblk * per)), b = r / per, k = r % per;
+    base[b * stride + (size_t)elems[i] * per + k] = buf[t];
+  }
+}
+
+// engines of one process joined by hnumo_local_group: a host barrier per exchange keeps
+// every engine's pack ahead of the copies and the copies ahead of the next pack (one stream)
+struct LocalGroup {
+  std::vector<hnumo_engine *> eng;
+  std::mutex mu;
+  std::condition_variable cv;
+  int count = 0, gen = 0;
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    int g = gen;
+    if (++count == (int)eng.size()) {
+      count = 0;
+      gen++;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return gen != g; });
+    }
+  }
+};
+
+// refresh the ghost elements' block of `base` from their owners
+static void exchange(hnumo_engine *e, double *base, int ncomp, int nblk, size_t stride) {
+  if (e->comm_mode == 0) return;
+  const int per = e->P * ncomp;
+  for (auto &n : e->nbh)
+    if (n.nsend) {
+      size_t tot = (size_t)n.nsend * nblk * per;
+      hipLaunchKernelGGL(ghost_pack_kernel, dim3((unsigned)std::min<size_t>((tot + 255) / 256, 1024)), dim3(256), 0,
+                         e->stream, n.sbuf, base, n.d_send, n.nsend, per, nblk, stride);
+    }
+  if (e->comm_mode == 2) {
+    (void)ncclGroupStart();
+    for (auto &n : e->nbh) {
+      if (n.nsend) (void)ncclSend(n.sbuf, (size_t)n.nsend * nblk * per, ncclDouble, n.rank, e->comm, e->stream);
+      if (n.nrecv) (void)ncclRecv(n.rbuf, (size_t)n.nrecv * nblk * per, ncclDouble, n.rank, e->comm, e->stream);
+    }
+    (void)ncclGroupEnd();
+  } else {
+    LocalGroup *g = e->group;
+    g->barrier();
+    for (auto &n : e->nbh) {
+      if (!n.nrecv) continue;
+      hnumo_engine *peer = g->eng[n.rank];
+      for (auto &pn : peer->nbh)
+        if (pn.rank == e->rank)
+          (void)hipMemcpyAsync(n.rbuf, pn.sbuf, sizeof(double) * (size_t)n.nrecv * nblk * per, hipMemcpyDeviceToDevice,
+                               e->stream);
+    }
+    g->barrier();
+  }
+  for (auto &n : e->nbh)
+    if (n.nrecv) {
+      size_t tot = (size_t)n.nrecv * nblk * per;
+      hipLaunchKernelGGL(ghost_unpack_kernel, dim3((unsigned)std::min<size_t>((tot + 255) / 256, 1024)), dim3(256), 0,
+                         e->stream, base, n.rbuf, n.d_recv, n.nrecv, per, nblk, stride);
+    }
+}
+static void exchange_qb(hnumo_engine *e, double *qb) { exchange(e, qb, 4, 1, 0); }
+static void exchange_qp(hnumo_engine *e, double *qp) { exchange(e, qp, 3, e->L, 3 * (size_t)e->npoin); }
+static void exchange_dpp(hnumo_engine *e) { exchange(e, e->dpp, 1, e->L, (size_t)e->npoin); }
+
 static void launch_copy(hnumo_engine *e, double *dst, const double *src, size_t n) {
   (void)hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, e->stream);
 }
@@ -190,7 +297,8 @@ static void launch_bcl_coeffs(hnumo_engine *e, const double *qp, double *qf) {
 static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp, bool timed = false) {
   zero_accumulators(e);
   launch_copy(e, e->qbuf[0], qb_state, 4 * (size_t)e->npoin);
-  DISPATCH(e, grad_trace(e, e->qbuf[0], e->gtrace[0]));
+  exchange_qb(e, e->qbuf[0]);
+  DISPATCH(e, grad_trace(e, e->qbuf[0], e->gtrace[0], 0, e->nelem));
   if (timed && e->kernel_events) (void)hipEventRecord(e->evk0, e->stream);
   int cur = 0, gt = 0, qb0i = 0, qb2i = -1;
   const int K = e->K, NB = e->p.N_btp;
@@ -225,6 +333,11 @@ static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp,
       a.accumulate = 1;
       a.prof = e->stage_prof;
       DISPATCH(e, stage(e, a));
+      if (a.write_trace && e->comm_mode) {
+        // ghosts take the owners' new state; their traces go into the owned elements' slots
+        exchange_qb(e, e->qbuf[out]);
+        DISPATCH(e, grad_trace(e, e->qbuf[out], e->gtrace[1 - gt], e->nelem_owned, e->nelem - e->nelem_owned));
+      }
       gt = 1 - gt;
       cur = out;
       if (K == 5 && ik == 1) qb2i = out;
@@ -249,20 +362,27 @@ static void launch_step(hnumo_engine *e) {
   launch_copy(e, e->q2, e->q, n3);
   launch_copy(e, e->qp2, e->qp, n3);
   launch_copy(e, e->qf2, e->qf, nf);
-  DISPATCH(e, mass_cons(e, e->qp2, e->qf2, e->q2, nullptr, 0));
+  DISPATCH(e, mass(e, e->qp2, e->qf2, e->q2));
+  exchange_dpp(e);
+  DISPATCH(e, cons(e, e->q2, nullptr, 0));
   DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qbp, e->q2, e->qp2, 0));
+  exchange_qp(e, e->qp2);
   DISPATCH(e, extract(e, e->qp2, e->qf2, 0));
   // correction (ti_rk_bcl.F90:62-85)
   launch_avg(e, e->qp2, e->qp2, e->qp, n3, 1);
   launch_avg(e, e->qf2, e->qf, e->qf2, nf, 1);
   DISPATCH(e, bcl_coeffs(e, e->qp2, e->qf2));
   launch_subcycle(e, e->qb, e->qp2, true);
-  DISPATCH(e, mass_cons(e, e->qp2, e->qf2, e->q, e->qp2, 1));
+  DISPATCH(e, mass(e, e->qp2, e->qf2, e->q));
+  exchange_dpp(e);
+  DISPATCH(e, cons(e, e->q, e->qp2, 1));
+  exchange_qp(e, e->qp2);
   DISPATCH(e, extract(e, e->qp2, e->qf2, 1));
   hipLaunchKernelGGL(dp_average_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp2, e->qp, e->dpp2, nl);
   launch_avg(e, e->qf2, e->qf, e->qf2, nf / 3, 3);
   DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qb, e->q, e->qp2, 1));
   hipLaunchKernelGGL(qprime_final_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp, e->qp2, e->dpp2, nl);
+  exchange_qp(e, e->qp);
   hipLaunchKernelGGL(finite_check_kernel, dim3(256), dim3(256), 0, e->stream, e->qb, 4 * (size_t)e->npoin, e->neg_flag);
 }
 
@@ -280,7 +400,8 @@ void hnumo_engine_destroy(hnumo_engine *eng) {
   if (eng->graph) (void)hipGraphDestroy(eng->graph);
   for (void *ptr : eng->allocs) (void)hipFree(ptr);
   if (eng->h_neg) (void)hipHostFree(eng->h_neg);
-  if (eng->stream) (void)hipStreamDestroy(eng->stream);
+  if (eng->stream && eng->own_stream) (void)hipStreamDestroy(eng->stream);
+  if (eng->comm) (void)ncclCommDestroy(eng->comm);
   if (eng->ev0) (void)hipEventDestroy(eng->ev0);
   if (eng->ev1) (void)hipEventDestroy(eng->ev1);
   if (eng->evk0) (void)hipEventDestroy(eng->evk0);
@@ -299,8 +420,14 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   *out = eng;
   eng->device = device;
   if (!mesh || !st || !par) return fail(eng, HNUMO_ERR_INVALID, "null descriptor");
-  if (halo && halo->nranks > 1 && halo->num_nbh > 0)
-    return fail(eng, HNUMO_ERR_INVALID, "multi-rank halo exchange not supported by this build");
+  if (halo && halo->nranks > 1) {
+    if (halo->rank < 0 || halo->rank >= halo->nranks) return fail(eng, HNUMO_ERR_INVALID, "bad rank");
+    if (halo->nelem_owned < 1 || halo->nelem_owned > mesh->nelem)
+      return fail(eng, HNUMO_ERR_INVALID, "nelem_owned must be in 1..nelem (owned elements first)");
+    for (int k = 0; k < halo->num_nbh; k++)
+      if (halo->num_send_recv && halo->num_send_recv[k] > 0)
+        return fail(eng, HNUMO_ERR_INVALID, "processor-face halos are not supported: use the ghost-element lists");
+  }
   if (par->method_visc == 1) return fail(eng, HNUMO_ERR_INVALID, "method_visc==1 (quad-point LDG) not supported");
   if (par->ad_mlswe > 0.0) return fail(eng, HNUMO_ERR_INVALID, "ad_mlswe>0 (vertical shear stress) not supported");
   if (mesh->nlayers < 1 || mesh->nlayers > MAXL)
@@ -318,6 +445,8 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   if (mesh->npoin != E * P || mesh->npoin_q != E * Q) return fail(eng, HNUMO_ERR_INVALID, "npoin/npoin_q mismatch");
   eng->nelem = E; eng->npoin = E * P; eng->npq = E * Q; eng->nface = F; eng->ngl = ngl; eng->nq = nq;
   eng->L = L; eng->P = P; eng->Q = Q; eng->K = par->kstages;
+  eng->nelem_owned = (halo && halo->nranks > 1) ? halo->nelem_owned : E;
+  const int EO = eng->nelem_owned;
   eng->FQ = (size_t)F * nq; eng->FN = (size_t)F * ngl;
   const size_t npoin = eng->npoin, npq = eng->npq, FQ = eng->FQ, FN = eng->FN;
 
@@ -371,9 +500,14 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     }
   }
   // face -> element-side slots; per-element int records for the stage kernel
-  std::vector<int> fslotL(F, -1), fslotR(F, -1);
+  std::vector<int> fslotL(F, -1), fslotR(F, -1), fslotA(F, -1);
   for (int e = 0; e < E; e++)
     for (int lf = 0; lf < 4; lf++) (eside[4 * e + lf] == 0 ? fslotL : fslotR)[efaces[4 * e + lf]] = 4 * e + lf;
+  // face averages are kept by the left element, or by the right one when the left is a ghost
+  for (int f = 0; f < F; f++) {
+    const int el = fel[f], er = fer[f];
+    fslotA[f] = (el >= EO && er > 0 && er - 1 < EO) ? fslotR[f] : fslotL[f];
+  }
   const int ERS = EREC_SIZE(ngl);
   std::vector<int> erec((size_t)E * ERS, -1);
   for (int e = 0; e < E; e++) {
@@ -384,6 +518,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
       r[EREC_BC + lf] = ebc[4 * e + lf];
       r[EREC_NBE + lf] = enbr_e[4 * e + lf];
       r[EREC_NBLF + lf] = enbr_lf[4 * e + lf];
+      r[EREC_ACC + lf] = fslotA[efaces[4 * e + lf]] == 4 * e + lf ? 1 : 0;
       for (int n = 0; n < ngl; n++) r[EREC_MAP + lf * ngl + n] = efmap[(4 * e + lf) * ngl + n];
       if (ebc[4 * e + lf] > 0) {
         // the stage kernel writes face traces into the neighbour's slot with the same face-node index
@@ -400,7 +535,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
         else return fail(eng, HNUMO_ERR_INVALID, "a node lies on more than two faces of its element");
       }
   }
-  eng->fslotL = fslotL;
+  eng->fslotA = fslotA;
   std::vector<int> conn;
   auto append = [&](const std::vector<int> &v) {
     size_t off = conn.size();
@@ -410,7 +545,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   size_t o_ef = append(efaces), o_es = append(eside), o_eb = append(ebc), o_em = append(efmap);
   size_t o_en = append(enbr_node), o_ee = append(enbr_e), o_el = append(enbr_lf), o_fl = append(fnodeL);
   size_t o_fr = append(fnodeR), o_fe = append(fel), o_fer = append(fer);
-  size_t o_sl = append(fslotL), o_sr = append(fslotR), o_er = append(erec);
+  size_t o_sl = append(fslotL), o_sr = append(fslotR), o_sa = append(fslotA), o_er = append(erec);
   eng->iconn = dalloc<int>(eng, conn.size());
   if (!eng->iconn) return fail(eng, HNUMO_ERR_DEVICE, "hipMalloc failed");
   HIPCHK(hipMemcpy(eng->iconn, conn.data(), conn.size() * sizeof(int), hipMemcpyHostToDevice));
@@ -546,6 +681,47 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   eng->neg_flag = dalloc<int>(eng, 1);
   if (const char *sp = getenv("HNUMO_STAGE_PROF"))
     if (sp[0] == '1') eng->stage_prof = dalloc<unsigned long long>(eng, (size_t)eng->nelem * 32);
+  if (halo && halo->nranks > 1) {
+    eng->rank = halo->rank;
+    eng->nranks = halo->nranks;
+    size_t os = 0, orr = 0;
+    const size_t per_max = (size_t)P * std::max(4, 3 * L);
+    for (int k = 0; k < halo->num_nbh; k++) {
+      Neighbour nb;
+      nb.rank = halo->nbh_proc[k];
+      nb.nsend = halo->num_ghost_send ? halo->num_ghost_send[k] : 0;
+      nb.nrecv = halo->num_ghost_recv ? halo->num_ghost_recv[k] : 0;
+      if (nb.rank < 0 || nb.rank >= halo->nranks || nb.rank == halo->rank)
+        return fail(eng, HNUMO_ERR_INVALID, "bad neighbour rank");
+      std::vector<int> snd(nb.nsend), rcv(nb.nrecv);
+      for (int i = 0; i < nb.nsend; i++) {
+        snd[i] = halo->ghost_send[os + i] - 1;
+        if (snd[i] < 0 || snd[i] >= eng->nelem_owned) return fail(eng, HNUMO_ERR_INVALID, "ghost_send must list owned elements");
+      }
+      for (int i = 0; i < nb.nrecv; i++) {
+        rcv[i] = halo->ghost_recv[orr + i] - 1;
+        if (rcv[i] < eng->nelem_owned || rcv[i] >= E) return fail(eng, HNUMO_ERR_INVALID, "ghost_recv must list ghost elements");
+      }
+      os += nb.nsend;
+      orr += nb.nrecv;
+      nb.d_send = dalloc<int>(eng, nb.nsend);
+      nb.d_recv = dalloc<int>(eng, nb.nrecv);
+      nb.sbuf = dalloc<double>(eng, nb.nsend * per_max);
+      nb.rbuf = dalloc<double>(eng, nb.nrecv * per_max);
+      if (eng->alloc_failed) return fail(eng, HNUMO_ERR_DEVICE, "hipMalloc failed (halo buffers)");
+      if (nb.nsend) HIPCHK(hipMemcpy(nb.d_send, snd.data(), nb.nsend * sizeof(int), hipMemcpyHostToDevice));
+      if (nb.nrecv) HIPCHK(hipMemcpy(nb.d_recv, rcv.data(), nb.nrecv * sizeof(int), hipMemcpyHostToDevice));
+      eng->nbh.push_back(nb);
+    }
+    if (halo->comm_id) {  // RCCL point-to-point over xGMI
+      ncclUniqueId id;
+      static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
+      std::memcpy(&id, halo->comm_id, sizeof(id));
+      ncclResult_t nr = ncclCommInitRank(&eng->comm, halo->nranks, id, halo->rank);
+      if (nr != ncclSuccess) return fail(eng, HNUMO_ERR_DEVICE, std::string("ncclCommInitRank: ") + ncclGetErrorString(nr));
+      eng->comm_mode = 2;
+    }
+  }
   if (eng->alloc_failed) return fail(eng, HNUMO_ERR_DEVICE, "hipMalloc failed (out of device memory?)");
   HIPCHK(hipHostMalloc((void **)&eng->h_neg, sizeof(int)));
   HIPCHK(hipMemcpy(eng->basis, hb.data(), hb.size() * 8, hipMemcpyHostToDevice));
@@ -564,7 +740,8 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   m.efaces = eng->iconn + o_ef; m.eside = eng->iconn + o_es; m.ebc = eng->iconn + o_eb; m.efmap = eng->iconn + o_em;
   m.enbr_node = eng->iconn + o_en; m.enbr_e = eng->iconn + o_ee; m.enbr_lf = eng->iconn + o_el;
   m.fnodeL = eng->iconn + o_fl; m.fnodeR = eng->iconn + o_fr; m.fel = eng->iconn + o_fe; m.fer = eng->iconn + o_fer;
-  m.fslotL = eng->iconn + o_sl; m.fslotR = eng->iconn + o_sr; m.erec = eng->iconn + o_er;
+  m.fslotL = eng->iconn + o_sl; m.fslotR = eng->iconn + o_sr; m.fslotA = eng->iconn + o_sa;
+  m.erec = eng->iconn + o_er;
   m.qstatE = eng->qstatE; m.nstatE = eng->nstatE; m.efstat = eng->efstat;
   m.basis = eng->basis; m.qstat = eng->qstat; m.nstat = eng->nstat; m.fstat = eng->fstat; m.fnstat = eng->fnstat;
   m.alpha = eng->alpha;
@@ -591,37 +768,46 @@ static int download_state(hnumo_engine *eng, double *q, double *qb, double *qp) 
   return 0;
 }
 
+// The whole step is captured once into a hipGraph (RCCL calls included) and replayed.  A
+// local exchange group (host barriers between engines) and a failed capture run the
+// same launch sequence directly.
 static int ensure_graph(hnumo_engine *eng) {
-  if (eng->graph_exec) return 0;
-  // first try with event-record nodes around the timed stage-kernel sequence
-  for (int attempt = 0; attempt < 2; attempt++) {
-    eng->kernel_events = attempt == 0;
-    if (eng->kernel_events && !eng->evk0) {
-      HIPCHK(hipEventCreate(&eng->evk0));
-      HIPCHK(hipEventCreate(&eng->evk1));
-    }
-    HIPCHK(hipStreamBeginCapture(eng->stream, hipStreamCaptureModeThreadLocal));
-    launch_step(eng);
-    hipError_t err = hipStreamEndCapture(eng->stream, &eng->graph);
-    if (err == hipSuccess) err = hipGraphInstantiate(&eng->graph_exec, eng->graph, nullptr, nullptr, 0);
-    if (err == hipSuccess) return 0;
+  if (eng->graph_exec || eng->no_graph) return 0;
+  if (eng->comm_mode == 1) {
+    eng->no_graph = true;
+    return 0;
+  }
+  eng->kernel_events = false;
+  HIPCHK(hipStreamBeginCapture(eng->stream, hipStreamCaptureModeThreadLocal));
+  launch_step(eng);
+  hipError_t err = hipStreamEndCapture(eng->stream, &eng->graph);
+  if (err == hipSuccess) err = hipGraphInstantiate(&eng->graph_exec, eng->graph, nullptr, nullptr, 0);
+  if (err != hipSuccess) {
     (void)hipGetLastError();
     if (eng->graph) (void)hipGraphDestroy(eng->graph);
     eng->graph = nullptr;
     eng->graph_exec = nullptr;
-    if (attempt == 1) {
-      eng->err = std::string("graph capture failed: ") + hipGetErrorString(err);
-      return HNUMO_ERR_DEVICE;
-    }
+    eng->no_graph = true;
+  }
+  return 0;
+}
+
+static int launch_steps(hnumo_engine *eng, int nsteps) {
+  int rc = ensure_graph(eng);
+  if (rc) return rc;
+  for (int s = 0; s < nsteps; s++) {
+    if (eng->graph_exec)
+      HIPCHK(hipGraphLaunch(eng->graph_exec, eng->stream));
+    else
+      launch_step(eng);
   }
   return 0;
 }
 
 static int run_steps(hnumo_engine *eng, int nsteps) {
-  int rc = ensure_graph(eng);
-  if (rc) return rc;
   HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
-  for (int s = 0; s < nsteps; s++) HIPCHK(hipGraphLaunch(eng->graph_exec, eng->stream));
+  int rc = launch_steps(eng, nsteps);
+  if (rc) return rc;
   HIPCHK(hipMemcpyAsync(eng->h_neg, eng->neg_flag, sizeof(int), hipMemcpyDeviceToHost, eng->stream));
   HIPCHK(hipStreamSynchronize(eng->stream));
   HIPCHK(hipGetLastError());
@@ -632,6 +818,9 @@ static int run_steps(hnumo_engine *eng, int nsteps) {
 
 int hnumo_ti_rk_bcl(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df) {
   if (!eng) return HNUMO_ERR_INVALID;
+  if (eng->comm_mode == 1) return fail(eng, HNUMO_ERR_INVALID, "engine is in a local group: use hnumo_group_ti_rk_bcl");
+  if (eng->nranks > 1 && eng->comm_mode == 0)
+    return fail(eng, HNUMO_ERR_INVALID, "multi-rank engine without transport (comm_id or hnumo_local_group)");
   HIPCHK(hipSetDevice(eng->device));
   if (!eng->resident || !eng->uploaded) {
     int rc = upload_state(eng, q_df, qb_df, qprime_df);
@@ -684,7 +873,7 @@ int hnumo_create_rhs_btp(hnumo_engine *eng, double *rhs, const double *qb_df, co
   int rc = upload_state(eng, nullptr, qb_df, qprime_df);
   if (rc) return rc;
   zero_accumulators(eng);
-  DISPATCH(eng, grad_trace(eng, eng->qb, eng->gtrace[0]));
+  DISPATCH(eng, grad_trace(eng, eng->qb, eng->gtrace[0], 0, eng->nelem));
   StageArgs a{};
   a.m = eng->m;
   a.qb_in = eng->qb; a.qb0 = eng->qb; a.qb2 = eng->qb; a.qprime = eng->qp;
@@ -764,7 +953,7 @@ int hnumo_get_field(hnumo_engine *eng, const char *name, double *out, int64_t n)
     for (int k : fields) {
       for (size_t f = 0; f < (size_t)eng->nface; f++)
         for (int iq = 0; iq < nq; iq++)
-          out[(f * nq + iq) * nc + c] = h[((size_t)eng->fslotL[f] * FA_N + k) * nq + iq];
+          out[(f * nq + iq) * nc + c] = h[((size_t)eng->fslotA[f] * FA_N + k) * nq + iq];
       c++;
     }
     return 0;
@@ -806,7 +995,7 @@ int hnumo_get_field(hnumo_engine *eng, const char *name, double *out, int64_t n)
     if (rc) return rc;
     for (size_t f = 0; f < (size_t)eng->nface; f++)
       for (int nn = 0; nn < ngl; nn++)
-        for (int c = 0; c < 8; c++) out[(f * ngl + nn) * 8 + c] = h[((size_t)eng->fslotL[f] * 8 + c) * ngl + nn];
+        for (int c = 0; c < 8; c++) out[(f * ngl + nn) * 8 + c] = h[((size_t)eng->fslotA[f] * 8 + c) * ngl + nn];
     return 0;
   }
   if (s == "Q_uu_dp") return soa(eng->qcoef, npq, {QC_QUU});
@@ -841,7 +1030,8 @@ int hnumo_bench_steps(hnumo_engine *eng, int nsteps, double *ms_total, double *m
   int rc = ensure_graph(eng);
   if (rc) return rc;
   HIPCHK(hipEventRecord(eng->ev0, eng->stream));
-  for (int s = 0; s < nsteps; s++) HIPCHK(hipGraphLaunch(eng->graph_exec, eng->stream));
+  rc = launch_steps(eng, nsteps);
+  if (rc) return rc;
   HIPCHK(hipEventRecord(eng->ev1, eng->stream));
   HIPCHK(hipEventSynchronize(eng->ev1));
   float ms = 0.f;
@@ -893,6 +1083,58 @@ int hnumo_debug_stage_profile(hnumo_engine *eng, uint64_t *out, int64_t n) {
   HIPCHK(hipSetDevice(eng->device));
   HIPCHK(hipStreamSynchronize(eng->stream));
   HIPCHK(hipMemcpy(out, eng->stage_prof, (size_t)eng->nelem * 32 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int hnumo_rccl_unique_id(unsigned char *out128) {
+  if (!out128) return HNUMO_ERR_INVALID;
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return HNUMO_ERR_DEVICE;
+  std::memcpy(out128, &id, sizeof(id));
+  return 0;
+}
+
+int hnumo_local_group(hnumo_engine **engines, int n) {
+  if (!engines || n < 1) return HNUMO_ERR_INVALID;
+  for (int i = 0; i < n; i++)
+    if (!engines[i] || engines[i]->rank != i || engines[i]->nranks != n || engines[i]->comm_mode != 0 ||
+        engines[i]->device != engines[0]->device)
+      return HNUMO_ERR_INVALID;
+  LocalGroup *g = new LocalGroup();
+  g->eng.assign(engines, engines + n);
+  for (int i = 0; i < n; i++) {
+    hnumo_engine *e = engines[i];
+    (void)hipSetDevice(e->device);
+    if (i > 0) {
+      if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+      e->stream = engines[0]->stream;
+      e->own_stream = false;
+    }
+    e->group = g;
+    e->comm_mode = 1;
+  }
+  return 0;
+}
+
+int hnumo_group_ti_rk_bcl(hnumo_engine **engines, int n, double **q_df, double **qb_df, double **qprime_df) {
+  if (!engines || n < 1 || !engines[0]->group || (int)engines[0]->group->eng.size() != n) return HNUMO_ERR_INVALID;
+  std::vector<int> rc(n, 0);
+  std::vector<std::thread> th;
+  for (int i = 0; i < n; i++)
+    th.emplace_back([&, i] {
+      hnumo_engine *eng = engines[i];
+      (void)hipSetDevice(eng->device);
+      if (!eng->resident || !eng->uploaded) {
+        rc[i] = upload_state(eng, q_df[i], qb_df[i], qprime_df[i]);
+        eng->uploaded = true;
+      }
+      int r = run_steps(eng, 1);
+      if (!rc[i]) rc[i] = r;
+      if (!rc[i] && !eng->resident) rc[i] = download_state(eng, q_df[i], qb_df[i], qprime_df[i]);
+    });
+  for (auto &t : th) t.join();
+  for (int i = 0; i < n; i++)
+    if (rc[i]) return rc[i];
   return 0;
 }
 

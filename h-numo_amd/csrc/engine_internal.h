@@ -16,7 +16,7 @@
 //
 // Element-major copies for the barotropic stage kernel (one contiguous record per element,
 // so a stage loads everything it needs with one round of async global->LDS copies):
-//   erec   int  [E][ERS]              faces, side, bc, nbr elem, nbr local face, face->node map,
+//   erec   int  [E][ERS]              faces, side, bc, nbr elem, nbr local face, keeps-averages flag, face->node map,
 //                                     node->(lf*NGL+n) of the <=2 faces through each node
 //   qstatE      [E][QE_N][Q]          W, e_x, e_y, n_x, n_y, coriolis, tau_wind(2), grad_zbot(2), 1/pb
 //   nstatE      [E][NE_N][P]          e_x, e_y, n_x, n_y, w, massinv, pbprime, 1/pbprime
@@ -25,7 +25,8 @@
 //   efcoef      [E][4][4NQ + 10NGL]   per-sub-cycle face Q_*_edge, H_bcl_edge | btp_graduv_dpp_face
 //   accumulators (element-major)      qacc [E][QA_N][Q], nacc [E][NA_N][P],
 //                                     facc [E][4][FA_N][NQ], gfacc [E][4][8][NGL]
-//                                     (face slots e*4+lf, used by the face's left element only)
+//                                     (face slots e*4+lf of the face's left element, or of its
+//                                     right element when the left one is a ghost: fslotA)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -76,9 +77,10 @@ enum EFNStat { EFN_NX = 0, EFN_NY, EFN_W, EFN_PBL, EFN_PBR, EFN_N };
 #define EREC_BC 8
 #define EREC_NBE 12
 #define EREC_NBLF 16
-#define EREC_MAP 20
-#define EREC_PF(ngl) (20 + 4 * (ngl))
-#define EREC_SIZE(ngl) (20 + 4 * (ngl) + 2 * (ngl) * (ngl))
+#define EREC_ACC 20   /* 1: this element keeps the face time averages of local face lf */
+#define EREC_MAP 24
+#define EREC_PF(ngl) (24 + 4 * (ngl))
+#define EREC_SIZE(ngl) (24 + 4 * (ngl) + 2 * (ngl) * (ngl))
 
 // element-major accumulator indices
 #define QACC_I(k, e, q) ((((size_t)(e)) * QA_N + (k)) * Q + (q))
@@ -92,6 +94,7 @@ struct DevMesh {
   const int *fnodeL, *fnodeR;     // [F][NGL] global node of face node n, left/right (-1 if none)
   const int *fel, *fer;           // [F] face(7)-1, face(8) (raw: >0 element+1, <=0 code)
   const int *fslotL, *fslotR;     // [F] element-side slot e*4+lf of the face's left / right element (-1)
+  const int *fslotA;              // [F] slot whose face accumulators hold the face's averages
   const int *erec;                // [E][EREC_SIZE]
   const double *qstatE, *nstatE, *efstat;
   const double *basis;            // psiq[NGL*NQ] dpsiq[NGL*NQ] dpsi[NGL*NGL]

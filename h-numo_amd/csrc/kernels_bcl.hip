@@ -329,9 +329,9 @@ __global__ void __launch_bounds__(64)
     const int iq = tid;
     const size_t fq = (size_t)f * NQ + iq;
     double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
-    double qbl0 = facc[FACC_I(FA_OPEL, m.fslotL[f], iq)], qbr0 = facc[FACC_I(FA_OPER, m.fslotL[f], iq)];
-    double qbl1 = facc[FACC_I(FA_UL, m.fslotL[f], iq)], qbr1 = facc[FACC_I(FA_UR, m.fslotL[f], iq)];
-    double qbl2 = facc[FACC_I(FA_VL, m.fslotL[f], iq)], qbr2 = facc[FACC_I(FA_VR, m.fslotL[f], iq)];
+    double qbl0 = facc[FACC_I(FA_OPEL, m.fslotA[f], iq)], qbr0 = facc[FACC_I(FA_OPER, m.fslotA[f], iq)];
+    double qbl1 = facc[FACC_I(FA_UL, m.fslotA[f], iq)], qbr1 = facc[FACC_I(FA_UR, m.fslotA[f], iq)];
+    double qbl2 = facc[FACC_I(FA_VL, m.fslotA[f], iq)], qbr2 = facc[FACC_I(FA_VR, m.fslotA[f], iq)];
     double su = 0.0, sv = 0.0;
     for (int k = 0; k < L; k++) {
       double ql[3] = {0, 0, 0}, qr[3] = {0, 0, 0};
@@ -371,8 +371,8 @@ __global__ void __launch_bounds__(64)
     const int iq = tid, er = m.fer[f];
     const size_t fq = (size_t)f * NQ + iq;
     double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
-    double d1 = facc[FACC_I(FA_MFX, m.fslotL[f], iq)] - slmf_face[0 * FQ + fq];
-    double d2 = facc[FACC_I(FA_MFY, m.fslotL[f], iq)] - slmf_face[1 * FQ + fq];
+    double d1 = facc[FACC_I(FA_MFX, m.fslotA[f], iq)] - slmf_face[0 * FQ + fq];
+    double d2 = facc[FACC_I(FA_MFY, m.fslotA[f], iq)] - slmf_face[1 * FQ + fq];
     double pbl = m.fstat[FS_PBL * FQ + fq], pbr = m.fstat[FS_PBR * FQ + fq];
     for (int k = 0; k < L; k++) {
       double ql = 0.0, qr = 0.0;
@@ -561,9 +561,9 @@ __global__ void __launch_bounds__(64)
     const size_t fq = (size_t)f * NQ + iq;
     const double *alpha = m.alpha;
     double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
-    double qbl0 = facc[FACC_I(FA_OPEL, m.fslotL[f], iq)], qbr0 = facc[FACC_I(FA_OPER, m.fslotL[f], iq)];
-    double qbl1 = facc[FACC_I(FA_UL, m.fslotL[f], iq)], qbr1 = facc[FACC_I(FA_UR, m.fslotL[f], iq)];
-    double qbl2 = facc[FACC_I(FA_VL, m.fslotL[f], iq)], qbr2 = facc[FACC_I(FA_VR, m.fslotL[f], iq)];
+    double qbl0 = facc[FACC_I(FA_OPEL, m.fslotA[f], iq)], qbr0 = facc[FACC_I(FA_OPER, m.fslotA[f], iq)];
+    double qbl1 = facc[FACC_I(FA_UL, m.fslotA[f], iq)], qbr1 = facc[FACC_I(FA_UR, m.fslotA[f], iq)];
+    double qbl2 = facc[FACC_I(FA_VL, m.fslotA[f], iq)], qbr2 = facc[FACC_I(FA_VR, m.fslotA[f], iq)];
     double ql[MAXL][3], qr[MAXL][3], udpl[MAXL], udpr[MAXL], vdpl[MAXL], vdpr[MAXL];
     double udpf[2][MAXL], vdpf[2][MAXL], Hf[2][MAXL];
     for (int k = 0; k < L; k++) {
@@ -602,8 +602,8 @@ __global__ void __launch_bounds__(64)
     for (int k = 0; k < L; k++) s2 = s2 + udpf[1][k];
     for (int k = 0; k < L; k++) s3 = s3 + vdpf[0][k];
     for (int k = 0; k < L; k++) s4 = s4 + vdpf[1][k];
-    double uu_def = facc[FACC_I(FA_QUU, m.fslotL[f], iq)] - s1, uv_def = facc[FACC_I(FA_QUV, m.fslotL[f], iq)] - s2;
-    double vu_def = facc[FACC_I(FA_QVU, m.fslotL[f], iq)] - s3, vv_def = facc[FACC_I(FA_QVV, m.fslotL[f], iq)] - s4;
+    double uu_def = facc[FACC_I(FA_QUU, m.fslotA[f], iq)] - s1, uv_def = facc[FACC_I(FA_QUV, m.fslotA[f], iq)] - s2;
+    double vu_def = facc[FACC_I(FA_QVU, m.fslotA[f], iq)] - s3, vv_def = facc[FACC_I(FA_QVV, m.fslotA[f], iq)] - s4;
     double sl = 0, sr = 0;
     for (int k = 0; k < L; k++) sl = sl + (fabs(udpl[k]) + eps1);
     for (int k = 0; k < L; k++) sr = sr + (fabs(udpr[k]) + eps1);
@@ -625,12 +625,12 @@ __global__ void __launch_bounds__(64)
     // H_r at the face (layer-overlap pressure, :627-707)
     double pf[2][MAXL + 1], zf[2][MAXL + 1], pep[MAXL + 1], pem[MAXL + 1], zep[MAXL + 1], zem[MAXL + 1];
     for (int k = 0; k <= L; k++) zf[0][k] = zf[1][k] = pf[0][k] = pf[1][k] = zep[k] = zem[k] = pep[k] = pem[k] = 0.0;
-    double ope_l = sqrt(facc[FACC_I(FA_OPE2L, m.fslotL[f], iq)]), ope_r = sqrt(facc[FACC_I(FA_OPE2R, m.fslotL[f], iq)]);
+    double ope_l = sqrt(facc[FACC_I(FA_OPE2L, m.fslotA[f], iq)]), ope_r = sqrt(facc[FACC_I(FA_OPE2R, m.fslotA[f], iq)]);
     for (int k = 1; k <= L; k++) {
       pf[0][k] = pf[0][k - 1] + ope_l * ql[k - 1][0];
       pf[1][k] = pf[1][k - 1] + ope_r * qr[k - 1][0];
     }
-    double ope_e = sqrt(facc[FACC_I(FA_OPEE2, m.fslotL[f], iq)]);
+    double ope_e = sqrt(facc[FACC_I(FA_OPEE2, m.fslotA[f], iq)]);
     double zbl = m.fstat[FS_ZBL * FQ + fq], zbr = m.fstat[FS_ZBR * FQ + fq];
     zf[0][L] = zbl;
     zf[1][L] = zbr;
@@ -693,7 +693,7 @@ __global__ void __launch_bounds__(64)
         Hf[1][k] = Hf[1][k] + Hc2;
       }
     }
-    double hfa = facc[FACC_I(FA_H, m.fslotL[f], iq)];
+    double hfa = facc[FACC_I(FA_H, m.fslotA[f], iq)];
     for (int sd = 0; sd < 2; sd++) {
       double weight = 1.0, acc = 0.0;
       for (int k = 0; k < L; k++) acc = acc + Hf[sd][k];
@@ -718,9 +718,9 @@ __global__ void __launch_bounds__(64)
     for (int k = 0; k < L; k++) {
       double fl[4], fr[4];
       for (int iv = 0; iv < 4; iv++) {
-        fl[iv] = gdpp_face[((size_t)k * 10 + 4) * FN + fn] * gfacc[GFACC_I(iv, m.fslotL[f], n)] +
+        fl[iv] = gdpp_face[((size_t)k * 10 + 4) * FN + fn] * gfacc[GFACC_I(iv, m.fslotA[f], n)] +
                  gdpp_face[((size_t)k * 10 + iv) * FN + fn];
-        fr[iv] = gdpp_face[((size_t)k * 10 + 9) * FN + fn] * gfacc[GFACC_I(4 + iv, m.fslotL[f], n)] +
+        fr[iv] = gdpp_face[((size_t)k * 10 + 9) * FN + fn] * gfacc[GFACC_I(4 + iv, m.fslotA[f], n)] +
                  gdpp_face[((size_t)k * 10 + 5 + iv) * FN + fn];
       }
       double qum0 = alpha * fl[0] + beta * fr[0], qum1 = alpha * fl[1] + beta * fr[1];

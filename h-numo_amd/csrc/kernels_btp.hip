@@ -186,6 +186,7 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ>::BS), (StageCfg<NGL, NQ>::M
   const int *s_er = reinterpret_cast<const int *>(S + C::O_EREC);
   const int *s_face = s_er + EREC_FACE, *s_side = s_er + EREC_SIDE, *s_bc = s_er + EREC_BC;
   const int *s_nbe = s_er + EREC_NBE, *s_nblf = s_er + EREC_NBLF, *s_map = s_er + EREC_MAP, *s_pf = s_er + EREC_PF(NGL);
+  const int *s_acc = s_er + EREC_ACC;
   double *s_qb = S + C::O_QB, *s_q0 = S + C::O_Q0, *s_q2 = S + C::O_Q2;  // [P][4]
   double *s_qk = S + C::O_QK;      // [QE_KEEP][Q]: W, e_x, e_y, n_x, n_y
   double *s_ns = S + C::O_NS;      // [NE_N][P]
@@ -407,7 +408,7 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ>::BS), (StageCfg<NGL, NQ>::M
         const double qvu = 0.5 * (ul * ql[3] + ur * qr[3]) + ope_e * ec[FC_QUV * NQ + iq];
         const double qvv = 0.5 * (vl * ql[3] + vr * qr[3]) + ope_e * ec[FC_QVV * NQ + iq];
         const double Hf = (ope_e * ope_e) * ec[FC_HBCL * NQ + iq];
-        if (a.accumulate && side == 0) {  // face time averages, kept by the face's left element
+        if (a.accumulate && s_acc[lf]) {  // face time averages, kept by one element per face
           const double opl = 1.0 + (ql[1] / pbl), opr = 1.0 + (qr[1] / pbr);
           double add[FA_N];
           add[FA_MFX] = fex; add[FA_MFY] = fey; add[FA_H] = Hf; add[FA_QUU] = quu; add[FA_QUV] = quv;
@@ -464,7 +465,7 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ>::BS), (StageCfg<NGL, NQ>::M
           gl[c] = side == 0 ? own[c] : oth[c];
           gr[c] = side == 0 ? oth[c] : own[c];
         }
-        if (a.accumulate && side == 0) {
+        if (a.accumulate && s_acc[lf]) {
           const double *old = s_ga + lf * 8 * NGL;
 #pragma unroll
           for (int c = 0; c < 4; c++) {
@@ -685,9 +686,9 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ>::BS), (StageCfg<NGL, NQ>::M
 // Face traces of a state for the first stage of a sub-cycle / a lone RHS: qb(4) and
 // grad(u_bar)(4) at the face nodes, written into the neighbours' trace slots.
 template <int NGL, int NQ>
-__global__ void __launch_bounds__(64) grad_trace_kernel(DevMesh m, const double *qb, double *trace) {
+__global__ void __launch_bounds__(64) grad_trace_kernel(DevMesh m, const double *qb, double *trace, int e0) {
   constexpr int P = NGL * NGL, ERS = EREC_SIZE(NGL);
-  const int e = blockIdx.x, tid = threadIdx.x;
+  const int e = e0 + blockIdx.x, tid = threadIdx.x;
   __shared__ double s_dpsi[NGL * NGL], s_qb[P * 4], s_nm[4 * P], s_u[P], s_v[P];
   __shared__ int s_er[ERS];
   for (int t = tid; t < NGL * NGL; t += 64) s_dpsi[t] = m.basis[2 * NGL * NQ + t];
@@ -736,6 +737,6 @@ __global__ void btp_finalize_kernel(double *qacc, double *facc, double *nacc, do
 
 #define HNUMO_INSTANTIATE_BTP(NGL, NQ)                                 \
   template __global__ void btp_stage_kernel<NGL, NQ>(StageArgs);        \
-  template __global__ void grad_trace_kernel<NGL, NQ>(DevMesh, const double *, double *);
+  template __global__ void grad_trace_kernel<NGL, NQ>(DevMesh, const double *, double *, int);
 
 }  // namespace hnumo

@@ -46,7 +46,34 @@ class HaloDesc(C.Structure):
         ("rank", C.c_int32), ("nranks", C.c_int32), ("num_nbh", C.c_int32),
         ("nbh_proc", _ip), ("num_send_recv", _ip), ("nbh_send_recv", _ip),
         ("comm_id", C.POINTER(C.c_ubyte)),
+        ("nelem_owned", C.c_int32), ("num_ghost_send", _ip), ("ghost_send", _ip),
+        ("num_ghost_recv", _ip), ("ghost_recv", _ip),
     ]
+
+
+class Halo:
+    """HaloDesc for a hnumo.partition.RankCase (keeps the index arrays alive)."""
+
+    def __init__(self, rc, comm_id: bytes | None = None):
+        nb = rc.neighbours
+        self.keep = {
+            "nbh_proc": np.array([n.rank for n in nb], dtype=np.int32),
+            "num_send_recv": np.zeros(len(nb), dtype=np.int32),
+            "num_ghost_send": np.array([len(n.send) for n in nb], dtype=np.int32),
+            "ghost_send": np.concatenate([np.asarray(n.send, dtype=np.int32) + 1 for n in nb]
+                                         or [np.zeros(0, np.int32)]).astype(np.int32),
+            "num_ghost_recv": np.array([len(n.recv) for n in nb], dtype=np.int32),
+            "ghost_recv": np.concatenate([np.asarray(n.recv, dtype=np.int32) + 1 for n in nb]
+                                         or [np.zeros(0, np.int32)]).astype(np.int32),
+        }
+        h = HaloDesc()
+        h.rank, h.nranks, h.num_nbh, h.nelem_owned = rc.rank, rc.nranks, len(nb), rc.nelem_owned
+        for k, v in self.keep.items():
+            setattr(h, k, v.ctypes.data_as(_ip) if v.size else None)
+        if comm_id is not None:
+            self.keep["comm_id"] = np.frombuffer(bytearray(comm_id), dtype=np.uint8).copy()
+            h.comm_id = self.keep["comm_id"].ctypes.data_as(C.POINTER(C.c_ubyte))
+        self.desc = h
 
 
 def ptr(a: np.ndarray | None):

@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 from . import bundle as _bundle
-from .abi import Descriptors, HaloDesc
+from .abi import Descriptors, Halo, HaloDesc
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libhnumo_engine.so")
 _lib = None
@@ -48,6 +48,9 @@ def lib():
         L.hnumo_bench_steps.argtypes = [vp, C.c_int, dp, dp, C.POINTER(C.c_int64)]
         L.hnumo_abi_version.restype = C.c_int
         L.hnumo_time_stage_kernel.argtypes = [vp, C.c_int, dp]
+        L.hnumo_rccl_unique_id.argtypes = [C.POINTER(C.c_ubyte)]
+        L.hnumo_local_group.argtypes = [C.POINTER(vp), C.c_int]
+        L.hnumo_group_ti_rk_bcl.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(dp), C.POINTER(dp), C.POINTER(dp)]
         L.hnumo_debug_stage_profile.argtypes = [vp, C.POINTER(C.c_uint64), C.c_int64]
         _lib = L
     return _lib
@@ -61,11 +64,16 @@ def _dp(a):
 class Engine:
     """One engine per GPU: device-resident ti_rk_bcl for one Case."""
 
-    def __init__(self, case, device: int = 0, halo: HaloDesc | None = None):
+    def __init__(self, case, device: int = 0, halo: HaloDesc | None = None, comm_id: bytes | None = None):
+        """case: a hnumo.case.Case, or a hnumo.partition.RankCase (multi-rank; its ghost-layer
+        halo is passed to the engine, with RCCL when comm_id is given)."""
         self.case = case
         self.desc = Descriptors(case, dense=False)
         self.dims = _bundle.dims(case)
         self.h = C.c_void_p()
+        if halo is None and getattr(case, "nranks", 1) > 1:
+            self._halo = Halo(case, comm_id)
+            halo = self._halo.desc
         self.halo = halo
         L = lib()
         rc = L.hnumo_engine_create(C.byref(self.desc.mesh), C.byref(self.desc.statics), C.byref(self.desc.params),
@@ -132,6 +140,14 @@ class Engine:
         self._check(lib().hnumo_debug_stage_profile(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), n))
         return out.reshape(-1, 32)
 
+    @staticmethod
+    def rccl_unique_id() -> bytes:
+        buf = (C.c_ubyte * 128)()
+        rc = lib().hnumo_rccl_unique_id(buf)
+        if rc:
+            raise EngineError(rc, "ncclGetUniqueId failed")
+        return bytes(buf)
+
     def _destroy(self):
         if getattr(self, "h", None) is not None and self.h.value:
             lib().hnumo_engine_destroy(self.h)
@@ -145,3 +161,24 @@ class Engine:
             self._destroy()
         except Exception:
             pass
+
+
+def local_group(engines):
+    """Join the engines of one process (ranks 0..n-1, same device) into a local exchange group."""
+    arr = (C.c_void_p * len(engines))(*[e.h.value for e in engines])
+    rc = lib().hnumo_local_group(arr, len(engines))
+    if rc:
+        raise EngineError(rc, "hnumo_local_group failed (ranks must be 0..n-1 on one device)")
+    for e in engines:
+        e._group = arr
+
+
+def group_ti_rk_bcl(engines, states):
+    """One baroclinic step of every engine of a local group; states[i] = (q, qb, qp) arrays."""
+    n = len(engines)
+    arr = engines[0]._group
+    mk = lambda j: (C.POINTER(C.c_double) * n)(*[_dp(states[i][j]) for i in range(n)])
+    rc = lib().hnumo_group_ti_rk_bcl(arr, n, mk(0), mk(1), mk(2))
+    if rc:
+        msgs = [lib().hnumo_last_error(e.h).decode() for e in engines]
+        raise EngineError(rc, "; ".join(m for m in msgs if m))

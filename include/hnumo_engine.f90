@@ -15,7 +15,7 @@ module hnumo_engine_c
 
     integer(c_int), parameter, public :: HNUMO_OK = 0, HNUMO_ERR_NEGATIVE_THICKNESS = 1, &
         HNUMO_ERR_NONFINITE = 2, HNUMO_ERR_DEVICE = 3, HNUMO_ERR_INVALID = 4
-    integer(c_int), parameter, public :: HNUMO_ABI_EXPECTED = 1   ! must equal hnumo_abi_version()
+    integer(c_int), parameter, public :: HNUMO_ABI_EXPECTED = 2   ! must equal hnumo_abi_version()
 
     ! = hnumo_mesh_desc (mod_grid, mod_face, mod_basis, mod_metrics; optional dense tables)
     type, bind(C), public :: hnumo_mesh_desc
@@ -68,6 +68,9 @@ module hnumo_engine_c
         integer(c_int32_t) :: rank = 0, nranks = 1, num_nbh = 0
         type(c_ptr) :: nbh_proc = c_null_ptr, num_send_recv = c_null_ptr, nbh_send_recv = c_null_ptr
         type(c_ptr) :: comm_id = c_null_ptr
+        integer(c_int32_t) :: nelem_owned = 0
+        type(c_ptr) :: num_ghost_send = c_null_ptr, ghost_send = c_null_ptr
+        type(c_ptr) :: num_ghost_recv = c_null_ptr, ghost_recv = c_null_ptr
     end type hnumo_halo_desc
 
     public :: hnumo_engine_create, hnumo_engine_destroy, hnumo_abi_version, hnumo_ti_rk_bcl, &

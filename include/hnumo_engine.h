@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define HNUMO_ABI_VERSION 1
+#define HNUMO_ABI_VERSION 2
 
 enum {
   HNUMO_OK = 0,
@@ -112,17 +112,32 @@ typedef struct hnumo_params {
   int32_t N_btp, kstages, method_visc, botfr;
 } hnumo_params;
 
-/* Face-halo description (mod_parallel): processor faces have face(8)=0.  Faces are
- * exchanged per neighbour in the order nbh_send_recv lists them (create_rhs_communicator
- * / send_receive_bound).  num_nbh = 0 for a single rank.  The engine moves halos with
- * RCCL point-to-point over xGMI; rank/nranks/comm_id identify the communicator.      */
+/* Multi-rank description.  The reference partitions with processor faces (face(8)=0)
+ * and exchanges face traces per neighbour (mod_parallel num_nbh / nbh_proc /
+ * num_send_recv / nbh_send_recv; create_rhs_communicator, send_receive_bound).  This
+ * engine partitions with a one-element GHOST layer instead, which keeps every owned
+ * element's arithmetic identical to the single-rank run (bit for bit): local elements
+ * 1..nelem_owned are owned, nelem_owned+1..nelem are copies of neighbours' elements
+ * whose data the engine refreshes from their owners wherever a kernel reads across an
+ * element boundary.  Per neighbour k (ranks nbh_proc[k]): ghost_send lists, in global
+ * element order, the owned elements that neighbour holds as ghosts, ghost_recv the local
+ * ghosts it owns (h-numo_amd/hnumo/partition.py builds both).  Transport: RCCL
+ * point-to-point over xGMI when comm_id (from hnumo_rccl_unique_id) is given; engines of
+ * one process on one device joined with hnumo_local_group otherwise.  The face-list
+ * fields are accepted for the reference-style partition but processor faces are
+ * rejected (code 4).  NULL halo or nranks == 1: single rank.                        */
 typedef struct hnumo_halo_desc {
   int32_t rank, nranks;
   int32_t num_nbh;
   const int32_t *nbh_proc;              /* (num_nbh) neighbour ranks                    */
   const int32_t *num_send_recv;         /* (num_nbh) shared faces per neighbour         */
   const int32_t *nbh_send_recv;         /* (sum num_send_recv) 1-based face ids         */
-  const unsigned char *comm_id;         /* 128-byte RCCL unique id (NULL if nranks==1)  */
+  const unsigned char *comm_id;         /* 128-byte RCCL unique id (NULL: local group)  */
+  int32_t nelem_owned;                  /* owned elements come first                    */
+  const int32_t *num_ghost_send;        /* (num_nbh)                                    */
+  const int32_t *ghost_send;            /* (sum num_ghost_send) 1-based local elements  */
+  const int32_t *num_ghost_recv;        /* (num_nbh)                                    */
+  const int32_t *ghost_recv;            /* (sum num_ghost_recv) 1-based local elements  */
 } hnumo_halo_desc;
 
 typedef struct hnumo_engine hnumo_engine;   /* opaque: device buffers, streams, graphs */
@@ -159,6 +174,17 @@ int hnumo_get_field(hnumo_engine *eng, const char *name, double *out, int64_t n)
  * hnumo_sync().                                                                      */
 int hnumo_set_resident(hnumo_engine *eng, int on);
 int hnumo_sync(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df);
+
+/* RCCL unique id (128 bytes) for hnumo_halo_desc.comm_id: generated by one rank and
+ * broadcast by the host (MPI / torch.distributed) before hnumo_engine_create.        */
+int hnumo_rccl_unique_id(unsigned char *out128);
+
+/* Join the n engines of one process (one per rank 0..n-1 of the same partition, on the
+ * same device) into a local exchange group: they share one stream and exchange ghost
+ * data by device copies.  hnumo_group_ti_rk_bcl then advances all of them one step
+ * (one host thread per engine).  For tests of the multi-rank path on one GPU.        */
+int hnumo_local_group(hnumo_engine **engines, int n);
+int hnumo_group_ti_rk_bcl(hnumo_engine **engines, int n, double **q_df, double **qb_df, double **qprime_df);
 
 /* Timing hook for the benchmark: run `nsteps` resident baroclinic steps and return
  * device-side event timings (ms) of the whole span and of the dominant kernel.       */
