@@ -9,9 +9,13 @@ per second, one element-update = one element advanced by one barotropic stage wi
 layers, EU/s = E * 2*N_btp*kstages / T_step.  Inputs are the analytic double-gyre initial
 condition (data: synthetic IC, no files).
 
-Multi-GPU (torch.distributed.run, one rank per GPU): this build has no inter-rank halo
-exchange yet, so every rank advances its own copy of the workload ("replicas"; weak
-scaling, no data-path collective); value = element-updates of all ranks / max time.
+Multi-GPU (torch.distributed.run, one rank per GPU; weak scaling): the double gyre is
+enlarged to px*py blocks of 25x25 elements (same element size, rank grid 2x1, 2x2, 4x2)
+and each rank owns one block plus a one-element ghost layer (hnumo/partition.py); the
+engine refreshes ghost data from the owners over RCCL point-to-point (xGMI) at every
+exchange point of the step (csrc/engine.hip `exchange`).  value = element-updates of all
+ranks / max time over ranks.  If the RCCL halo cannot be set up on every rank, the ranks
+fall back to independent replicas and say so in config.parallelism.
 """
 from __future__ import annotations
 
@@ -92,8 +96,35 @@ def main():
     from hnumo.engine import Engine
     from hnumo.roofline import HBM_PEAK_GBS, element_updates_per_step, stage_bytes
 
-    case = build_case(make_config(args.config), dense=False)
-    eng = Engine(case, device=local_rank)
+    base_cfg = make_config(args.config)
+    case = build_case(base_cfg, dense=False)         # the per-GPU block (roofline, workload name)
+    eng, parallelism = None, "single"
+    if world > 1:
+        from hnumo.partition import partition, rank_grid
+        px, py = rank_grid(world)
+        x0, x1 = base_cfg["xdims"]
+        y0, y1 = base_cfg["ydims"]
+        gcfg = make_config(args.config, nelx=base_cfg["nelx"] * px, nely=base_cfg["nely"] * py,
+                           xdims=(x0, x0 + (x1 - x0) * px), ydims=(y0, y0 + (y1 - y0) * py))
+        gcase = build_case(gcfg, dense=False)
+        obj = [Engine.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        err = None
+        try:
+            eng = Engine(partition(gcase, world, rank), device=local_rank, comm_id=obj[0])
+        except Exception as exc:  # pragma: no cover - depends on the node
+            err = f"{type(exc).__name__}: {exc}"
+        bad = torch.tensor([1 if err else 0], device="cuda")
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        if bad.item():
+            if eng is not None:
+                eng.close()
+            eng = None
+            parallelism = f"replicas{world} (RCCL halo unavailable: {err or 'on another rank'})"
+        else:
+            parallelism = f"domain decomposition {px}x{py} x ({base_cfg['nelx']}x{base_cfg['nely']}), ghost halo over RCCL"
+    if eng is None:
+        eng = Engine(case, device=local_rank)
     eng.set_resident(True)
     q, qb, qp = eng.state()
     eng.ti_rk_bcl(q, qb, qp)                       # uploads the state, builds the graph
@@ -119,12 +150,12 @@ def main():
     k_src = "graph event nodes around the corrector sub-cycle"
     if not (k_ms and k_ms > 0):
         k_ms = eng.time_stage_kernel(2)
-        k_src = "events around 2 direct corrector sub-cycles"
+        k_src = "events around 2 direct corrector sub-cycles" + (" (incl. halo exchanges)" if world > 1 else "")
     eng.sync(q, qb, qp)
     if not (abs(qb).max() < 1e30):
         raise RuntimeError("non-finite state after benchmark")
 
-    eu = element_updates_per_step(case) * args.steps * world
+    eu = element_updates_per_step(case) * args.steps * world   # every rank owns one block of E elements
     value = eu / elapsed
     ms_per_step = 1e3 * elapsed / args.steps
     sb = stage_bytes(case)
@@ -151,7 +182,7 @@ def main():
         "config": {"workload": f"{args.config}: double-gyre 25x25 elements, N=4, 3 layers, "
                                f"N_btp={case.scalars['N_btp']}, kstages=5",
                    "elements": case.scalars["nelem"], "nlayers": case.scalars["nlayers"],
-                   "nop": case.scalars["ngl"] - 1, "parallelism": f"replicas{world}" if world > 1 else "single"},
+                   "nop": case.scalars["ngl"] - 1, "parallelism": parallelism},
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
