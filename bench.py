@@ -80,6 +80,8 @@ def main():
     ap.add_argument("--config", default="dg25L3")
     ap.add_argument("--cpu-steps", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--summation", default="reference", choices=["reference", "factored"],
+                    help="stage summation order (hnumo_set_summation); only 'reference' meets the 1e-10 bar")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -111,7 +113,7 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         err = None
         try:
-            eng = Engine(partition(gcase, world, rank), device=local_rank, comm_id=obj[0])
+            eng = Engine(partition(gcase, world, rank), device=local_rank, comm_id=obj[0], summation=args.summation)
         except Exception as exc:  # pragma: no cover - depends on the node
             err = f"{type(exc).__name__}: {exc}"
         bad = torch.tensor([1 if err else 0], device="cuda")
@@ -124,7 +126,7 @@ def main():
         else:
             parallelism = f"domain decomposition {px}x{py} x ({base_cfg['nelx']}x{base_cfg['nely']}), ghost halo over RCCL"
     if eng is None:
-        eng = Engine(case, device=local_rank)
+        eng = Engine(case, device=local_rank, summation=args.summation)
     eng.set_resident(True)
     q, qb, qp = eng.state()
     eng.ti_rk_bcl(q, qb, qp)                       # uploads the state, builds the graph
@@ -182,7 +184,8 @@ def main():
         "config": {"workload": f"{args.config}: double-gyre 25x25 elements, N=4, 3 layers, "
                                f"N_btp={case.scalars['N_btp']}, kstages=5",
                    "elements": case.scalars["nelem"], "nlayers": case.scalars["nlayers"],
-                   "nop": case.scalars["ngl"] - 1, "parallelism": parallelism},
+                   "nop": case.scalars["ngl"] - 1, "parallelism": parallelism,
+                   "summation": args.summation},
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

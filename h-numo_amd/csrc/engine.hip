@@ -83,6 +83,7 @@ struct hnumo_engine {
   // events recorded inside the captured step around the corrector sub-cycle's stage kernels
   hipEvent_t evk0 = nullptr, evk1 = nullptr;
   bool capturing = false, kernel_events = false, no_graph = false;
+  int summation = HNUMO_SUM_REFERENCE;        // hnumo_set_summation
   unsigned long long *stage_prof = nullptr;  // HNUMO_STAGE_PROF=1: per-element phase clocks
 };
 
@@ -103,8 +104,12 @@ template <int NGL, int NQ>
 struct Launch {
   static constexpr int BSE = ((NQ * NQ + 63) / 64) * 64;
   static void stage(hnumo_engine *e, const StageArgs &a) {
-    hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(StageCfg<NGL, NQ>::BS), 0, e->stream,
-                       a);
+    if (e->summation == HNUMO_SUM_REFERENCE)
+      hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false>), dim3(e->nelem_owned), dim3(StageCfg<NGL, NQ, false>::BS),
+                         0, e->stream, a);
+    else
+      hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, true>), dim3(e->nelem_owned), dim3(StageCfg<NGL, NQ, true>::BS), 0,
+                         e->stream, a);
   }
   // face traces of elements [e0, e0+n) into their neighbours' slots
   static void grad_trace(hnumo_engine *e, const double *qb, double *gt, int e0, int n) {
@@ -679,6 +684,8 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   eng->lapf = dalloc<double>(eng, 2 * FN * L);
   eng->rhs = dalloc<double>(eng, 3 * npoin);
   eng->neg_flag = dalloc<int>(eng, 1);
+  if (const char *sm = getenv("HNUMO_SUMMATION"))
+    eng->summation = (sm[0] == 'r' || sm[0] == '0') ? HNUMO_SUM_REFERENCE : HNUMO_SUM_FACTORED;
   if (const char *sp = getenv("HNUMO_STAGE_PROF"))
     if (sp[0] == '1') eng->stage_prof = dalloc<unsigned long long>(eng, (size_t)eng->nelem * 32);
   if (halo && halo->nranks > 1) {
@@ -839,6 +846,24 @@ int hnumo_set_resident(hnumo_engine *eng, int on) {
   eng->uploaded = false;
   return 0;
 }
+
+int hnumo_set_summation(hnumo_engine *eng, int mode) {
+  if (!eng) return HNUMO_ERR_INVALID;
+  if (mode != HNUMO_SUM_REFERENCE && mode != HNUMO_SUM_FACTORED)
+    return fail(eng, HNUMO_ERR_INVALID, "hnumo_set_summation: mode must be HNUMO_SUM_REFERENCE or HNUMO_SUM_FACTORED");
+  if (mode != eng->summation) {
+    eng->summation = mode;
+    // the captured step holds the other kernel: capture again on the next step
+    if (eng->graph_exec) (void)hipGraphExecDestroy(eng->graph_exec);
+    if (eng->graph) (void)hipGraphDestroy(eng->graph);
+    eng->graph_exec = nullptr;
+    eng->graph = nullptr;
+    if (eng->comm_mode != 1) eng->no_graph = false;
+  }
+  return 0;
+}
+
+int hnumo_get_summation(hnumo_engine *eng) { return eng ? eng->summation : -1; }
 
 int hnumo_sync(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df) {
   if (!eng) return HNUMO_ERR_INVALID;

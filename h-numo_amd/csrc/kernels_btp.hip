@@ -68,7 +68,7 @@ __device__ __forceinline__ void glds_copy(const void *g, void *l, int ndw, int t
   rot = (rot + nch) % NW;
 }
 
-template <int NGL, int NQ>
+template <int NGL, int NQ, bool SF = false>
 struct StageCfg {
   static constexpr int P = NGL * NGL, Q = NQ * NQ;
   static constexpr int BS = (Q <= 25) ? 128 : 256;
@@ -82,10 +82,14 @@ struct StageCfg {
   static constexpr int O_BASIS = 0, O_EREC = O_BASIS + NB, O_QB = O_EREC + ERSD, O_Q0 = O_QB + 4 * P,
                        O_Q2 = O_Q0 + 4 * P, O_QK = O_Q2 + 4 * P, O_NS = O_QK + QE_KEEP * Q, O_NC = O_NS + NE_N * P,
                        O_EF = O_NC + 5 * P, O_NA = O_EF + 4 * FBLK, O_UV = O_NA + NA_N * P;
-  // working arrays
-  static constexpr int O_QV = O_UV + 2 * P, O_GR = O_QV + 7 * Q, O_QQ = O_GR + 4 * P, O_FQ = O_QQ + 4 * P,
-                       O_FL = O_FQ + 16 * NQ, O_RHS = O_FL + 8 * NGL, O_LAP = O_RHS + 3 * P, O_QN = O_LAP + 2 * P,
-                       O_B = O_QN + 4 * P;
+  // working arrays: quad-point values (exact: the 7 integrand factors; SF: the 8 weighted
+  // integrands F1,F2,G0..G2,H0..H2), B outputs, then a region written only after B that the
+  // SF variant also uses for the interpolation partials Y [NYV][NGL][NQ] read in B
+  static constexpr int NQV = SF ? 8 : 7, NYV = 7;
+  static constexpr int O_QV = O_UV + 2 * P, O_GR = O_QV + NQV * Q, O_FQ = O_GR + 4 * P, O_FL = O_FQ + 16 * NQ,
+                       O_W = O_FL + 8 * NGL, O_QQ = O_W, O_RHS = O_QQ + 4 * P, O_LAP = O_RHS + 3 * P,
+                       O_QN = O_LAP + 2 * P, O_Y = O_W, W_END = O_QN + 4 * P,
+                       O_B = (SF && O_Y + NYV * NGL * NQ > W_END) ? O_Y + NYV * NGL * NQ : W_END;
   // B-only inputs (dead after B), overlaid by the term buffers in D
   static constexpr int B_QP = 0, B_QR = B_QP + 3 * P, B_QC = B_QR + (QE_N - QE_KEEP) * Q, B_QA = B_QC + 4 * Q,
                        B_FA = B_QA + QA_N * Q, B_GA = B_FA + 4 * FA_N * NQ,
@@ -95,7 +99,10 @@ struct StageCfg {
   static constexpr int RCM = RC0 < 1 ? 1 : (RC0 > NQ ? NQ : RC0);
   static constexpr int NCH = (NQ + RCM - 1) / RCM, RC = (NQ + NCH - 1) / NCH, QC = RC * NQ;
   static constexpr int QCP = QC | 1, TSZ = 3 * P * QCP;
-  static constexpr int ARENA = O_B + (B_SIZE > 2 * TSZ ? B_SIZE : 2 * TSZ);
+  // SF: first-pass contraction partials U, W [3][2][NGL][NQ] overlay the dead B inputs
+  static constexpr int UWSZ = 3 * 2 * NGL * NQ;
+  static constexpr int DSZ = SF ? UWSZ : 2 * TSZ;
+  static constexpr int ARENA = O_B + (B_SIZE > DSZ ? B_SIZE : DSZ);
 };
 
 // The 2*NGL-1 nonzero source nodes of a nodal derivative at node (i,j), in the reference
@@ -171,9 +178,13 @@ __device__ __forceinline__ void nodal_grad4(const double *s_dpsi, int i, int j, 
 // unlike __syncthreads(), whose release fence drains every store of the wave first.
 #define LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
-template <int NGL, int NQ>
-__global__ void __launch_bounds__((StageCfg<NGL, NQ>::BS), (StageCfg<NGL, NQ>::MINW)) btp_stage_kernel(StageArgs a) {
-  using C = StageCfg<NGL, NQ>;
+// SF = false: the reference's summation order (bitwise parity, see the header);
+// SF = true: sum-factorised interpolation and volume integral (tensor-product contractions,
+// ~7x fewer flops, results within rounding of the reference order).
+template <int NGL, int NQ, bool SF>
+__global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ, SF>::MINW))
+    btp_stage_kernel(StageArgs a) {
+  using C = StageCfg<NGL, NQ, SF>;
   constexpr int P = C::P, Q = C::Q, BS = C::BS, NCH = C::NCH, QC = C::QC, QCP = C::QCP;
   const DevMesh &m = a.m;
   const int e = blockIdx.x, tid = threadIdx.x;
@@ -194,7 +205,8 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ>::BS), (StageCfg<NGL, NQ>::M
   double *s_ef = S + C::O_EF;      // [4][FBLK]
   double *s_nacc_old = S + C::O_NA;  // [NA_N][P] old nodal accumulators
   double *s_u = S + C::O_UV, *s_v = s_u + P;  // u_bar = qb(3)/qb(1), v_bar = qb(4)/qb(1) at the nodes
-  double *s_qv = S + C::O_QV;      // [7][Q]: udp, vdp, sc_x, Hq+qu, quv, sc_y, Hq+qv
+  double *s_qv = S + C::O_QV;      // [NQV][Q] (see StageCfg)
+  double *s_y = S + C::O_Y;        // SF: [NYV][NGL][NQ] interpolation partials (A2 -> B)
   double *s_grad = S + C::O_GR, *s_qq = S + C::O_QQ;  // [4][P]
   double *s_fq = S + C::O_FQ;      // [4][NQ][4]: wq, flux, H_kx+flux_x, H_ky+flux_y
   double *s_fl = S + C::O_FL;      // [4][NGL][2]
@@ -244,9 +256,52 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ>::BS), (StageCfg<NGL, NQ>::M
   }
   __syncthreads();
   // u_bar, v_bar of the stage-input state, once per node (Uk of mod_laplacian_quad.F90:48-49)
-  for (int p = tid; p < P; p += BS) {
-    s_u[p] = s_qb[p * 4 + 2] / s_qb[p * 4];
-    s_v[p] = s_qb[p * 4 + 3] / s_qb[p * 4];
+  if constexpr (!SF) {
+    for (int p = tid; p < P; p += BS) {
+      s_u[p] = s_qb[p * 4 + 2] / s_qb[p * 4];
+      s_v[p] = s_qb[p * 4 + 3] / s_qb[p * 4];
+    }
+  } else {
+    // + first pass of the nodal -> quad interpolation (mod_rhs_btp.F90:141-152):
+    // Y(var, mm, iq) = sum_n psiq(n, iq) X(var, n + mm*NGL); groups (dp, dpp) | (udp, vdp) |
+    // bottom-layer (pp, up, vp)
+    constexpr int NT1 = NQ * NGL;
+    const int ng = m.botfr ? 3 : 2;
+    for (int w = tid; w < P + ng * NT1; w += BS) {
+      asm volatile("" ::: "memory");
+      if (w < P) {
+        s_u[w] = s_qb[w * 4 + 2] / s_qb[w * 4];
+        s_v[w] = s_qb[w * 4 + 3] / s_qb[w * 4];
+        continue;
+      }
+      const int t = w - P, g = t / NT1, r = t % NT1, mm = r / NQ, iq = r % NQ;
+      double pa[NGL];
+#pragma unroll
+      for (int n = 0; n < NGL; n++) pa[n] = s_psiq[n * NQ + iq];
+      if (g < 2) {
+        double x0 = 0.0, x1 = 0.0;
+#pragma unroll
+        for (int n = 0; n < NGL; n++) {
+          const int ip = mm * NGL + n;
+          x0 = x0 + pa[n] * s_qb[ip * 4 + 2 * g];
+          x1 = x1 + pa[n] * s_qb[ip * 4 + 2 * g + 1];
+        }
+        s_y[((2 * g) * NGL + mm) * NQ + iq] = x0;
+        s_y[((2 * g + 1) * NGL + mm) * NQ + iq] = x1;
+      } else {
+        double x0 = 0.0, x1 = 0.0, x2 = 0.0;
+#pragma unroll
+        for (int n = 0; n < NGL; n++) {
+          const int ip = mm * NGL + n;
+          x0 = x0 + pa[n] * s_qp[ip * 3 + 0];
+          x1 = x1 + pa[n] * s_qp[ip * 3 + 1];
+          x2 = x2 + pa[n] * s_qp[ip * 3 + 2];
+        }
+        s_y[(4 * NGL + mm) * NQ + iq] = x0;
+        s_y[(5 * NGL + mm) * NQ + iq] = x1;
+        s_y[(6 * NGL + mm) * NQ + iq] = x2;
+      }
+    }
   }
   LDS_BARRIER();
   STAGE_MARK(1);
@@ -263,37 +318,60 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ>::BS), (StageCfg<NGL, NQ>::M
       if (w < Q) {
         // ---- quad-point physics (mod_rhs_btp.F90:136-192)
         const int q = w, iq = q % NQ, jq = q / NQ;
-        double pa[NGL], pb[NGL];
-#pragma unroll
-        for (int n = 0; n < NGL; n++) {
-          pa[n] = s_psiq[n * NQ + iq];
-          pb[n] = s_psiq[n * NQ + jq];
-        }
-        const double *gq = s_qb;  // broadcast LDS reads (every lane reads the same node)
         double dp = 0, dpp = 0, udp = 0, vdp = 0, pp = 0, up = 0, vp = 0;
-#pragma unroll 1
-        for (int mm = 0; mm < NGL; mm++)
+        if constexpr (SF) {
+          // second interpolation pass: sum_mm psiq(mm, jq) Y(var, mm, iq)
+#pragma unroll
+          for (int mm = 0; mm < NGL; mm++) {
+            const double pb = s_psiq[mm * NQ + jq];
+            const double *y = s_y + mm * NQ + iq;
+            dp = dp + pb * y[0 * NGL * NQ];
+            dpp = dpp + pb * y[1 * NGL * NQ];
+            udp = udp + pb * y[2 * NGL * NQ];
+            vdp = vdp + pb * y[3 * NGL * NQ];
+          }
+          if (m.botfr) {
+#pragma unroll
+            for (int mm = 0; mm < NGL; mm++) {
+              const double pb = s_psiq[mm * NQ + jq];
+              const double *y = s_y + mm * NQ + iq;
+              pp = pp + pb * y[4 * NGL * NQ];
+              up = up + pb * y[5 * NGL * NQ];
+              vp = vp + pb * y[6 * NGL * NQ];
+            }
+          }
+        } else {
+          double pa[NGL], pb[NGL];
 #pragma unroll
           for (int n = 0; n < NGL; n++) {
-            const int ip = mm * NGL + n;
-            const double hi = pa[n] * pb[mm];  // PSIH(n,mm,iq,jq)
-            dp = dp + hi * gq[ip * 4 + 0];
-            dpp = dpp + hi * gq[ip * 4 + 1];
-            udp = udp + hi * gq[ip * 4 + 2];
-            vdp = vdp + hi * gq[ip * 4 + 3];
+            pa[n] = s_psiq[n * NQ + iq];
+            pb[n] = s_psiq[n * NQ + jq];
           }
-        if (m.botfr) {
-          const double *gp = s_qp;
+          const double *gq = s_qb;  // broadcast LDS reads (every lane reads the same node)
 #pragma unroll 1
           for (int mm = 0; mm < NGL; mm++)
 #pragma unroll
             for (int n = 0; n < NGL; n++) {
               const int ip = mm * NGL + n;
-              const double hi = pa[n] * pb[mm];
-              pp = pp + hi * gp[ip * 3 + 0];
-              up = up + hi * gp[ip * 3 + 1];
-              vp = vp + hi * gp[ip * 3 + 2];
+              const double hi = pa[n] * pb[mm];  // PSIH(n,mm,iq,jq)
+              dp = dp + hi * gq[ip * 4 + 0];
+              dpp = dpp + hi * gq[ip * 4 + 1];
+              udp = udp + hi * gq[ip * 4 + 2];
+              vdp = vdp + hi * gq[ip * 4 + 3];
             }
+          if (m.botfr) {
+            const double *gp = s_qp;
+#pragma unroll 1
+            for (int mm = 0; mm < NGL; mm++)
+#pragma unroll
+              for (int n = 0; n < NGL; n++) {
+                const int ip = mm * NGL + n;
+                const double hi = pa[n] * pb[mm];
+                pp = pp + hi * gp[ip * 3 + 0];
+                up = up + hi * gp[ip * 3 + 1];
+                vp = vp + hi * gp[ip * 3 + 2];
+              }
+          }
         }
         const double cor = s_qr[(QE_COR - QE_KEEP) * Q + q];
         const double tw1 = s_qr[(QE_TW1 - QE_KEEP) * Q + q], tw2 = s_qr[(QE_TW2 - QE_KEEP) * Q + q];
@@ -328,13 +406,30 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ>::BS), (StageCfg<NGL, NQ>::M
 #pragma unroll
           for (int k = 0; k < QA_N; k++) a.qacc[QACC_I(k, e, q)] = s_qa[k * Q + q] + add[k];
         }
-        s_qv[0 * Q + q] = udp;
-        s_qv[1 * Q + q] = vdp;
-        s_qv[2 * Q + q] = sc_x;
-        s_qv[3 * Q + q] = Hq + qu;
-        s_qv[4 * Q + q] = quv;
-        s_qv[5 * Q + q] = sc_y;
-        s_qv[6 * Q + q] = Hq + qv;
+        if constexpr (SF) {
+          // weighted integrands of T(v) = wq*(hi*S_v + dhdx*X_v + dhdy*Y_v) split by basis
+          // factor: psi*psi -> F_v = wq*S_v, dpsi*psi -> G_v = wq*(e_x X_v + e_y Y_v),
+          // psi*dpsi -> H_v = wq*(n_x X_v + n_y Y_v)  (create_rhs_btp_volume_qdf, :194-206)
+          const double wq = s_qk[QE_W * Q + q], ex = s_qk[QE_EX * Q + q], ey = s_qk[QE_EY * Q + q];
+          const double nx = s_qk[QE_NX * Q + q], ny = s_qk[QE_NY * Q + q];
+          const double A = Hq + qu, B = Hq + qv;
+          s_qv[0 * Q + q] = wq * sc_x;
+          s_qv[1 * Q + q] = wq * sc_y;
+          s_qv[2 * Q + q] = wq * (ex * udp + ey * vdp);
+          s_qv[3 * Q + q] = wq * (ex * A + ey * quv);
+          s_qv[4 * Q + q] = wq * (ex * quv + ey * B);
+          s_qv[5 * Q + q] = wq * (nx * udp + ny * vdp);
+          s_qv[6 * Q + q] = wq * (nx * A + ny * quv);
+          s_qv[7 * Q + q] = wq * (nx * quv + ny * B);
+        } else {
+          s_qv[0 * Q + q] = udp;
+          s_qv[1 * Q + q] = vdp;
+          s_qv[2 * Q + q] = sc_x;
+          s_qv[3 * Q + q] = Hq + qu;
+          s_qv[4 * Q + q] = quv;
+          s_qv[5 * Q + q] = sc_y;
+          s_qv[6 * Q + q] = Hq + qv;
+        }
       } else if (w >= OG && w < OG + P) {
         // ---- nodal grad(u_bar) (compute_gradient_uv) + stage-start nodal averages
         const int p = w - OG, i = p % NGL, j = p / NGL;
@@ -519,6 +614,55 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ>::BS), (StageCfg<NGL, NQ>::M
       T[(2 * P + p) * QCP + qi] = wq * (hi * scy + dhdx * quv + dhdy * B);
     }
   };
+  // creat_btp_fluxes_qdf projection onto node p (mod_rhs_btp.F90:339-362): left -, right +
+  auto face_proj = [&](int v, int p, double acc) {
+#pragma unroll
+    for (int kf = 0; kf < 2; kf++) {
+      const int r = s_pf[2 * p + kf];
+      if (r < 0) continue;
+      const int lf = r / NGL, n = r % NGL;
+      const bool left = s_side[lf] == 0;
+      const double *fq = s_fq + lf * NQ * 4;
+#pragma unroll
+      for (int iq = 0; iq < NQ; iq++) {
+        const double c = fq[iq * 4] * s_psiq[n * NQ + iq] * fq[iq * 4 + 1 + v];
+        acc = left ? acc - c : acc + c;
+      }
+    }
+    return acc;
+  };
+  // LDG volume fluxes qq (btp_compute_laplacian, mod_laplacian_quad.F90:374-380)
+  auto qq_task = [&](int p) {
+    const double pv = s_nc[NC_PV * P + p];
+#pragma unroll
+    for (int c = 0; c < 4; c++) s_qq[c * P + p] = pv * s_grad[c * P + p] + s_nc[(NC_D1 + c) * P + p];
+  };
+  // lap(c,p): volume over source nodes s=(ii,jj) (mod_laplacian_quad.F90:382-386), nonzero
+  // terms only (jj==j or ii==i), then faces (:489-513)
+  auto lap_task = [&](int c, int p) {
+    const int i = p % NGL, j = p / NGL;
+    double acc = 0.0;
+    const int qa = (2 * c) * P, qb_ = (2 * c + 1) * P;
+#pragma unroll
+    for (int r = 0; r < 2 * NGL - 1; r++) {
+      const bool mid = (r >= j) && (r < j + NGL);
+      const int jj = mid ? j : (r < j ? r : r - NGL + 1);
+      const int ii = mid ? r - j : i;
+      const int s = jj * NGL + ii;
+      // HE_DF(i,j,ii,jj) = dpsi(i,ii) [jj==j], HN_DF(i,j,ii,jj) = dpsi(j,jj) [ii==i]
+      const double he = s_dpsi[i * NGL + ii], hn = s_dpsi[j * NGL + jj];
+      const double ex_ = he * s_ns[NE_EX * P + s], ey_ = he * s_ns[NE_EY * P + s];
+      const double nx_ = hn * s_ns[NE_NX * P + s], ny_ = hn * s_ns[NE_NY * P + s];
+      const bool both = mid && ii == i;
+      const double dx = both ? ex_ + nx_ : (mid ? ex_ : nx_);
+      const double dy = both ? ey_ + ny_ : (mid ? ey_ : ny_);
+      acc = acc - s_ns[NE_W * P + s] * (dx * s_qq[qa + s] + dy * s_qq[qb_ + s]);
+    }
+    const int r0 = s_pf[2 * p], r1 = s_pf[2 * p + 1];
+    if (r0 >= 0) acc = acc + s_fl[r0 * 2 + c];
+    if (r1 >= 0) acc = acc + s_fl[r1 * 2 + c];
+    s_lap[c * P + p] = acc;
+  };
   // sum task (v, p): rhs(v,p) += T over the chunk in quad order; faces after the last chunk
   auto sum_task = [&](int k, int t) {
     const int v = t / P, p = t % P;
@@ -528,25 +672,57 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ>::BS), (StageCfg<NGL, NQ>::M
 #pragma unroll
     for (int qi = 0; qi < QC; qi++)
       if (qi < nq_k) acc = acc + T[qi];
-    if (k == NCH - 1) {
-      // creat_btp_fluxes_qdf projection (mod_rhs_btp.F90:339-362): left -, right +
-#pragma unroll
-      for (int kf = 0; kf < 2; kf++) {
-        const int r = s_pf[2 * p + kf];
-        if (r < 0) continue;
-        const int lf = r / NGL, n = r % NGL;
-        const bool left = s_side[lf] == 0;
-        const double *fq = s_fq + lf * NQ * 4;
-#pragma unroll
-        for (int iq = 0; iq < NQ; iq++) {
-          const double c = fq[iq * 4] * s_psiq[n * NQ + iq] * fq[iq * 4 + 1 + v];
-          acc = left ? acc - c : acc + c;
-        }
-      }
-    }
+    if (k == NCH - 1) acc = face_proj(v, p, acc);
     s_rhs[v * P + p] = acc;
   };
 
+  if constexpr (SF) {
+    // C1: first contraction pass over iq, per (v, i, jq):
+    //   U_v(i,jq) = sum_iq psiq(i,iq) F_v + dpsiq(i,iq) G_v,  W_v(i,jq) = sum_iq psiq(i,iq) H_v
+    // (F_0 = 0), with the LDG volume fluxes qq alongside
+    double *s_uw = SB;  // [3][2][NGL][NQ]
+    constexpr int NT1 = 3 * NGL * NQ;
+    for (int w = tid; w < NT1 + P; w += BS) {
+      asm volatile("" ::: "memory");
+      if (w < NT1) {
+        const int v = w / (NGL * NQ), r = w % (NGL * NQ), i = r / NQ, jq = r % NQ;
+        const double *F = s_qv + (v > 0 ? v - 1 : 0) * Q + jq * NQ, *G = s_qv + (2 + v) * Q + jq * NQ;
+        const double *H = s_qv + (5 + v) * Q + jq * NQ;
+        double u = 0.0, wv = 0.0;
+#pragma unroll
+        for (int iq = 0; iq < NQ; iq++) {
+          const double pi = s_psiq[i * NQ + iq], dpi = s_dpsiq[i * NQ + iq];
+          if (v > 0) u = u + pi * F[iq];
+          u = u + dpi * G[iq];
+          wv = wv + pi * H[iq];
+        }
+        s_uw[((2 * v) * NGL + i) * NQ + jq] = u;
+        s_uw[((2 * v + 1) * NGL + i) * NQ + jq] = wv;
+      } else {
+        qq_task(w - NT1);
+      }
+    }
+    LDS_BARRIER();
+    STAGE_MARK(6);
+    // C2: second pass over jq per (v, p=(i,j)): rhs = sum_jq psiq(j,jq) U + dpsiq(j,jq) W,
+    // then the face projections; the Laplacian alongside
+    for (int w = tid; w < 3 * P + 2 * P; w += BS) {
+      asm volatile("" ::: "memory");
+      if (w < 3 * P) {
+        const int v = w / P, p = w % P, i = p % NGL, j = p / NGL;
+        const double *U = s_uw + ((2 * v) * NGL + i) * NQ, *W = s_uw + ((2 * v + 1) * NGL + i) * NQ;
+        double acc = 0.0;
+#pragma unroll
+        for (int jq = 0; jq < NQ; jq++) acc = acc + (s_psiq[j * NQ + jq] * U[jq] + s_dpsiq[j * NQ + jq] * W[jq]);
+        s_rhs[v * P + p] = face_proj(v, p, acc);
+      } else {
+        const int t = w - 3 * P;
+        lap_task(t / P, t % P);
+      }
+    }
+    LDS_BARRIER();
+    STAGE_MARK(7);
+  } else
   for (int k = 0; k <= NCH; k++) {
     asm volatile("" ::: "memory");  // keep LDS reads inside their phase (no hoisting)
     const int WT = (k < NCH) ? ((k == NCH - 1) ? (Q - k * QC) : QC) * NGL : 0;  // term tasks
@@ -562,38 +738,10 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ>::BS), (StageCfg<NGL, NQ>::M
       } else if (w < WT + WS) {
         sum_task(k - 1, w - WT);
       } else if (w < WT + WS + WG + WX) {
-        // ---- LDG volume fluxes qq (btp_compute_laplacian, mod_laplacian_quad.F90:374-380)
-        const int p = w - WT - WS - WG;
-        const double pv = s_nc[NC_PV * P + p];
-#pragma unroll
-        for (int c = 0; c < 4; c++) s_qq[c * P + p] = pv * s_grad[c * P + p] + s_nc[(NC_D1 + c) * P + p];
+        qq_task(w - WT - WS - WG);
       } else {
-        // ---- lap(c,p): volume over source nodes s=(ii,jj) (mod_laplacian_quad.F90:382-386),
-        //      nonzero terms only (jj==j or ii==i), then faces (:489-513)
-        const int t = w - WT - WS - WG - WX, c = t / P, p = t % P, i = p % NGL, j = p / NGL;
-        double acc = 0.0;
-        const int qa = (2 * c) * P, qb_ = (2 * c + 1) * P;
-#pragma unroll
-        for (int r = 0; r < 2 * NGL - 1; r++) {
-          const bool mid = (r >= j) && (r < j + NGL);
-          const int jj = mid ? j : (r < j ? r : r - NGL + 1);
-          const int ii = mid ? r - j : i;
-          const int s = jj * NGL + ii;
-          // HE_DF(i,j,ii,jj) = dpsi(i,ii) [jj==j], HN_DF(i,j,ii,jj) = dpsi(j,jj) [ii==i]
-          const double he = s_dpsi[i * NGL + ii], hn = s_dpsi[j * NGL + jj];
-          const double ex_ = he * s_ns[NE_EX * P + s], ey_ = he * s_ns[NE_EY * P + s];
-          const double nx_ = hn * s_ns[NE_NX * P + s], ny_ = hn * s_ns[NE_NY * P + s];
-          const bool both = mid && ii == i;
-          const double dx = both ? ex_ + nx_ : (mid ? ex_ : nx_);
-          const double dy = both ? ey_ + ny_ : (mid ? ey_ : ny_);
-          acc = acc - s_ns[NE_W * P + s] * (dx * s_qq[qa + s] + dy * s_qq[qb_ + s]);
-        }
-        {
-          const int r0 = s_pf[2 * p], r1 = s_pf[2 * p + 1];
-          if (r0 >= 0) acc = acc + s_fl[r0 * 2 + c];
-          if (r1 >= 0) acc = acc + s_fl[r1 * 2 + c];
-        }
-        s_lap[c * P + p] = acc;
+        const int t = w - WT - WS - WG - WX;
+        lap_task(t / P, t % P);
       }
     }
     LDS_BARRIER();
@@ -736,7 +884,8 @@ __global__ void btp_finalize_kernel(double *qacc, double *facc, double *nacc, do
 }
 
 #define HNUMO_INSTANTIATE_BTP(NGL, NQ)                                 \
-  template __global__ void btp_stage_kernel<NGL, NQ>(StageArgs);        \
+  template __global__ void btp_stage_kernel<NGL, NQ, false>(StageArgs); \
+  template __global__ void btp_stage_kernel<NGL, NQ, true>(StageArgs);  \
   template __global__ void grad_trace_kernel<NGL, NQ>(DevMesh, const double *, double *, int);
 
 }  // namespace hnumo

@@ -16,6 +16,7 @@ module hnumo_engine_c
     integer(c_int), parameter, public :: HNUMO_OK = 0, HNUMO_ERR_NEGATIVE_THICKNESS = 1, &
         HNUMO_ERR_NONFINITE = 2, HNUMO_ERR_DEVICE = 3, HNUMO_ERR_INVALID = 4
     integer(c_int), parameter, public :: HNUMO_ABI_EXPECTED = 2   ! must equal hnumo_abi_version()
+    integer(c_int), parameter, public :: HNUMO_SUM_REFERENCE = 0, HNUMO_SUM_FACTORED = 1
 
     ! = hnumo_mesh_desc (mod_grid, mod_face, mod_basis, mod_metrics; optional dense tables)
     type, bind(C), public :: hnumo_mesh_desc
@@ -75,7 +76,8 @@ module hnumo_engine_c
 
     public :: hnumo_engine_create, hnumo_engine_destroy, hnumo_abi_version, hnumo_ti_rk_bcl, &
         hnumo_ti_barotropic_ssprk, hnumo_btp_bcl_coeffs, hnumo_create_rhs_btp, hnumo_get_field_c, &
-        hnumo_set_resident, hnumo_sync, hnumo_last_error_c, hnumo_last_error, hnumo_get_field
+        hnumo_set_resident, hnumo_sync, hnumo_last_error_c, hnumo_last_error, hnumo_get_field, &
+        hnumo_set_summation, hnumo_get_summation
 
     interface
         integer(c_int) function hnumo_engine_create(mesh, statics, params, halo, device, eng) &
@@ -147,6 +149,19 @@ module hnumo_engine_c
             type(c_ptr), value :: eng
             integer(c_int), value :: on
         end function hnumo_set_resident
+
+        ! summation order of the barotropic stage: HNUMO_SUM_REFERENCE (default, bitwise) or
+        ! HNUMO_SUM_FACTORED (sum-factorised, opt-in; see include/hnumo_engine.h)
+        integer(c_int) function hnumo_set_summation(eng, mode) bind(C, name='hnumo_set_summation')
+            import :: c_int, c_ptr
+            type(c_ptr), value :: eng
+            integer(c_int), value :: mode
+        end function hnumo_set_summation
+
+        integer(c_int) function hnumo_get_summation(eng) bind(C, name='hnumo_get_summation')
+            import :: c_int, c_ptr
+            type(c_ptr), value :: eng
+        end function hnumo_get_summation
 
         integer(c_int) function hnumo_sync(eng, q_df, qb_df, qprime_df) bind(C, name='hnumo_sync')
             import :: c_int, c_ptr, c_double

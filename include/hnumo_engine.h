@@ -175,6 +175,20 @@ int hnumo_get_field(hnumo_engine *eng, const char *name, double *out, int64_t n)
 int hnumo_set_resident(hnumo_engine *eng, int on);
 int hnumo_sync(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df);
 
+/* Summation order of the barotropic stage (no reference counterpart: the reference has
+ * one order).  HNUMO_SUM_REFERENCE (the default) evaluates the volume integral and the
+ * nodal -> quad interpolation as the reference's dense psih/dpsidx sums in its order:
+ * results bit-identical to the reference Fortran.  HNUMO_SUM_FACTORED uses tensor-product
+ * sum factorisation (~7x fewer flops, ~1.4x faster stage).  It is exact up to rounding,
+ * but the momentum RHS is a difference of terms ~1e7 times larger, so reordering moves
+ * it by up to ~1e-6 relative and the state by ~1e-7 relative after a few steps: outside
+ * the 1e-10 parity bar, hence opt-in.  Environment override at create:
+ * HNUMO_SUMMATION=reference|factored.  hnumo_get_summation returns the mode.          */
+#define HNUMO_SUM_REFERENCE 0
+#define HNUMO_SUM_FACTORED 1
+int hnumo_set_summation(hnumo_engine *eng, int mode);
+int hnumo_get_summation(hnumo_engine *eng);
+
 /* RCCL unique id (128 bytes) for hnumo_halo_desc.comm_id: generated by one rank and
  * broadcast by the host (MPI / torch.distributed) before hnumo_engine_create.        */
 int hnumo_rccl_unique_id(unsigned char *out128);

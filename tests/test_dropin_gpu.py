@@ -4,7 +4,8 @@ ISO_C_BINDING bridge (oracle/_ref/dropin_driver; include/hnumo_engine.f90 +
 h-numo_amd/fortran/hnumo_bridge.F90).  Both binaries are built in the build container from
 /root/reference sources (oracle/build_ref.sh) and travel to the GPU box with the repo.
 
-Parity bar: bit-identical state and time averages (same as test_engine_gpu.test_bitwise_step).
+Parity bar: bit-identical state and time averages (same as test_engine_gpu.test_bitwise_step;
+default summation order).
 """
 import os
 
