@@ -72,37 +72,50 @@ template <int NGL, int NQ, bool SF = false>
 struct StageCfg {
   static constexpr int P = NGL * NGL, Q = NQ * NQ;
   static constexpr int BS = (Q <= 25) ? 128 : 256;
-  static constexpr int MINW = (BS == 256) ? 3 : 4;          // waves/SIMD wanted (3 blocks/CU)
+  static constexpr int MINW = (BS == 256) ? 3 : 4;          // waves/SIMD wanted
+  static constexpr int NBLK_CU = (MINW * 4 * 64) / BS;      // resident blocks per CU wanted
+  static constexpr int BUDGET = (163840 / NBLK_CU - 512) / 8;  // LDS doubles per block
   static constexpr int ERS = EREC_SIZE(NGL), ERSD = (ERS + 1) / 2;
   static constexpr int FBLK = EF_N * NQ + EFN_N * NGL;      // efstat block per element side
   static constexpr int EFC = 4 * NQ + 10 * NGL;             // efcoef block per element side
   static constexpr int ECO = 4 * Q + 5 * P;                 // ecoef record per element
   static constexpr int NB = 2 * NGL * NQ + NGL * NGL;       // psiq, dpsiq, dpsi
-  // LDS arena (doubles). Persistent (A..E):
+  static_assert(Q <= BS, "one quad-point task per thread");
+  // LDS arena (doubles).  Persistent (A..E); the wall normals of the face nodes are copied
+  // out of the face statics (which live in the B region) for E1:
   static constexpr int O_BASIS = 0, O_EREC = O_BASIS + NB, O_QB = O_EREC + ERSD, O_Q0 = O_QB + 4 * P,
                        O_Q2 = O_Q0 + 4 * P, O_QK = O_Q2 + 4 * P, O_NS = O_QK + QE_KEEP * Q, O_NC = O_NS + NE_N * P,
-                       O_EF = O_NC + 5 * P, O_NA = O_EF + 4 * FBLK, O_UV = O_NA + NA_N * P;
+                       O_UV = O_NC + 5 * P, O_WN = O_UV + 2 * P;
   // working arrays: quad-point values (exact: the 7 integrand factors; SF: the 8 weighted
   // integrands F1,F2,G0..G2,H0..H2), B outputs, then a region written only after B that the
-  // SF variant also uses for the interpolation partials Y [NYV][NGL][NQ] read in B
+  // SF variant also uses for the interpolation partials Y [NYV][NGL][NQ] (A2 -> B)
   static constexpr int NQV = SF ? 8 : 7, NYV = 7;
-  static constexpr int O_QV = O_UV + 2 * P, O_GR = O_QV + NQV * Q, O_FQ = O_GR + 4 * P, O_FL = O_FQ + 16 * NQ,
+  static constexpr int O_QV = O_WN + 8 * NGL, O_GR = O_QV + NQV * Q, O_FQ = O_GR + 4 * P, O_FL = O_FQ + 16 * NQ,
                        O_W = O_FL + 8 * NGL, O_QQ = O_W, O_RHS = O_QQ + 4 * P, O_LAP = O_RHS + 3 * P,
                        O_QN = O_LAP + 2 * P, O_Y = O_W, W_END = O_QN + 4 * P,
                        O_B = (SF && O_Y + NYV * NGL * NQ > W_END) ? O_Y + NYV * NGL * NQ : W_END;
-  // B-only inputs (dead after B), overlaid by the term buffers in D
-  static constexpr int B_QP = 0, B_QR = B_QP + 3 * P, B_QC = B_QR + (QE_N - QE_KEEP) * Q, B_QA = B_QC + 4 * Q,
-                       B_FA = B_QA + QA_N * Q, B_GA = B_FA + 4 * FA_N * NQ,
-                       B_EC = B_GA + 4 * 8 * NGL, B_TR = B_EC + 4 * EFC, B_SIZE = B_TR + 32 * NGL;
-  // term chunks: RC quad rows, two buffers of [3P][QCP] (odd row pitch against bank conflicts)
-  static constexpr int RC0 = B_SIZE / (2 * 3 * P * (NQ + 1));
+  // B region: inputs read up to B (bottom-layer qprime, face statics, neighbour traces, face
+  // coefficients), then the term buffers (exact) / contraction partials (SF)
+  static constexpr int B_QP = 0, B_EF = B_QP + 3 * P, B_TR = B_EF + 4 * FBLK, B_EC = B_TR + 32 * NGL,
+                       B_SIZE = B_EC + 4 * EFC;
+  // exact: term chunks of RC quad rows, two buffers of [3P][QCP] (odd pitch against bank
+  // conflicts), as many rows as the LDS budget allows.  Buffer 0 (D0, D2, ..) lies past the
+  // B inputs, which the LDG face fluxes still read in D0; buffer 1 overlays them.
+  static constexpr int TAV = (BUDGET - O_B) / 2;
+  static constexpr int RC0 = (TAV / (3 * P) - 1) / NQ;  // largest RC with 3P*((RC*NQ)|1) <= TAV
   static constexpr int RCM = RC0 < 1 ? 1 : (RC0 > NQ ? NQ : RC0);
   static constexpr int NCH = (NQ + RCM - 1) / RCM, RC = (NQ + NCH - 1) / NCH, QC = RC * NQ;
   static constexpr int QCP = QC | 1, TSZ = 3 * P * QCP;
-  // SF: first-pass contraction partials U, W [3][2][NGL][NQ] overlay the dead B inputs
-  static constexpr int UWSZ = 3 * 2 * NGL * NQ;
-  static constexpr int DSZ = SF ? UWSZ : 2 * TSZ;
-  static constexpr int ARENA = O_B + (B_SIZE > DSZ ? B_SIZE : DSZ);
+  static constexpr int TB0 = TSZ > B_SIZE ? TSZ : B_SIZE, TB1 = 0;
+  // SF: first-pass contraction partials U, W [3][2][NGL][NQ], past the B inputs (C1 runs
+  // the LDG face fluxes)
+  static constexpr int UWSZ = 3 * 2 * NGL * NQ, B_UW = B_SIZE;
+  static constexpr int ARENA = O_B + (SF ? B_SIZE + UWSZ : TB0 + TSZ);
+  // B task ranges: quad points [0,Q) | face points [OF,OF+4NQ) | nodal grad [OG,OG+P) |
+  // LDG face nodes [OL,OL+4NGL), the face and nodal ranges on their own waves when they fit
+  static constexpr int RU = 64, OFa = ((Q + RU - 1) / RU) * RU, OGa = ((OFa + 4 * NQ + RU - 1) / RU) * RU;
+  static constexpr bool WIDE = OGa + P + 4 * NGL <= BS;
+  static constexpr int OF = WIDE ? OFa : Q, OG = WIDE ? OGa : OF + 4 * NQ, OL = OG + P, WEND = OL + 4 * NGL;
 };
 
 // The 2*NGL-1 nonzero source nodes of a nodal derivative at node (i,j), in the reference
@@ -170,6 +183,17 @@ __device__ __forceinline__ void nodal_grad4(const double *s_dpsi, int i, int j, 
   }
 }
 
+// Task range [0,n) laid out from virtual slot o on: task t runs on thread (o+t) % BS, in
+// the first pass iff o+t < BS (tasks of a first pass may use registers preloaded by role).
+template <int BS, class F>
+__device__ __forceinline__ void for_tasks(int tid, int o, int n, F &&f) {
+  static_assert((BS & (BS - 1)) == 0, "BS must be a power of two");
+  for (int t = (tid - o) & (BS - 1); t < n; t += BS) {
+    asm volatile("" ::: "memory");
+    f(t, o + t < BS);
+  }
+}
+
 #define STAGE_MARK(k) \
   if (a.prof && tid == 0) s_prof[k] = clock64();
 
@@ -180,7 +204,7 @@ __device__ __forceinline__ void nodal_grad4(const double *s_dpsi, int i, int j, 
 
 // SF = false: the reference's summation order (bitwise parity, see the header);
 // SF = true: sum-factorised interpolation and volume integral (tensor-product contractions,
-// ~7x fewer flops, results within rounding of the reference order).
+// ~7x fewer flops, equal to the reference up to rounding -- hnumo_set_summation).
 template <int NGL, int NQ, bool SF>
 __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ, SF>::MINW))
     btp_stage_kernel(StageArgs a) {
@@ -195,32 +219,27 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
   double *const S = s_arena;
   const double *s_psiq = S + C::O_BASIS, *s_dpsiq = s_psiq + NGL * NQ, *s_dpsi = s_dpsiq + NGL * NQ;
   const int *s_er = reinterpret_cast<const int *>(S + C::O_EREC);
-  const int *s_face = s_er + EREC_FACE, *s_side = s_er + EREC_SIDE, *s_bc = s_er + EREC_BC;
+  const int *s_side = s_er + EREC_SIDE, *s_bc = s_er + EREC_BC;
   const int *s_nbe = s_er + EREC_NBE, *s_nblf = s_er + EREC_NBLF, *s_map = s_er + EREC_MAP, *s_pf = s_er + EREC_PF(NGL);
   const int *s_acc = s_er + EREC_ACC;
   double *s_qb = S + C::O_QB, *s_q0 = S + C::O_Q0, *s_q2 = S + C::O_Q2;  // [P][4]
   double *s_qk = S + C::O_QK;      // [QE_KEEP][Q]: W, e_x, e_y, n_x, n_y
   double *s_ns = S + C::O_NS;      // [NE_N][P]
   double *s_nc = S + C::O_NC;      // [5][P] pbprime_visc, btp_dpp_graduv(4)
-  double *s_ef = S + C::O_EF;      // [4][FBLK]
-  double *s_nacc_old = S + C::O_NA;  // [NA_N][P] old nodal accumulators
   double *s_u = S + C::O_UV, *s_v = s_u + P;  // u_bar = qb(3)/qb(1), v_bar = qb(4)/qb(1) at the nodes
+  double *s_wn = S + C::O_WN;      // [4][2][NGL] face-node normals (wall fix)
   double *s_qv = S + C::O_QV;      // [NQV][Q] (see StageCfg)
-  double *s_y = S + C::O_Y;        // SF: [NYV][NGL][NQ] interpolation partials (A2 -> B)
+  double *s_y = S + C::O_Y;        // SF: [NYV][NGL][NQ] interpolation partials
   double *s_grad = S + C::O_GR, *s_qq = S + C::O_QQ;  // [4][P]
   double *s_fq = S + C::O_FQ;      // [4][NQ][4]: wq, flux, H_kx+flux_x, H_ky+flux_y
   double *s_fl = S + C::O_FL;      // [4][NGL][2]
   double *s_rhs = S + C::O_RHS, *s_lap = S + C::O_LAP;  // [3][P], [2][P]
   double *s_qn = S + C::O_QN;      // [P][4]
-  double *SB = S + C::O_B;         // B-only inputs, then the term buffers
+  double *SB = S + C::O_B;         // B-region inputs, then the term buffers / partials
   double *s_qp = SB + C::B_QP;     // [P][3] qprime of the bottom layer
-  double *s_qr = SB + C::B_QR;     // [QE_N-QE_KEEP][Q]: coriolis, tau_wind(2), grad_zbot(2), 1/pb
-  double *s_qc = SB + C::B_QC;     // [4][Q] Q_uu_dp, Q_uv_dp, Q_vv_dp, H_bcl (QC_* order)
-  double *s_qa = SB + C::B_QA;     // [QA_N][Q] old quad accumulators
-  double *s_fa = SB + C::B_FA;     // [4][FA_N][NQ]
-  double *s_ga = SB + C::B_GA;     // [4][8][NGL]
-  double *s_ec = SB + C::B_EC;     // [4][EFC]
+  double *s_ef = SB + C::B_EF;     // [4][FBLK]
   double *s_tr = SB + C::B_TR;     // [4][8][NGL]
+  double *s_ec = SB + C::B_EC;     // [4][EFC]
 
   // ------------------------------------------------------------- A: async loads
   if (a.prof && tid == 0) s_prof[30] = wall_clock64();
@@ -237,69 +256,121 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
     if (m.botfr) glds_copy<BS>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
     if (!a.rhs_only && a.a1 != 0.0) glds_copy<BS>(a.qb0 + (size_t)e * 4 * P, s_q0, 8 * P, tid, rot);
     if (!a.rhs_only && a.a3 != 0.0) glds_copy<BS>(a.qb2 + (size_t)e * 4 * P, s_q2, 8 * P, tid, rot);
-    const double *qse = m.qstatE + (size_t)e * QE_N * Q;
-    glds_copy<BS>(qse, s_qk, 2 * QE_KEEP * Q, tid, rot);
-    glds_copy<BS>(qse + QE_KEEP * Q, s_qr, 2 * (QE_N - QE_KEEP) * Q, tid, rot);
-    const double *eco = a.ecoef + (size_t)e * C::ECO;
-    glds_copy<BS>(eco, s_qc, 2 * 4 * Q, tid, rot);
-    glds_copy<BS>(eco + 4 * Q, s_nc, 2 * 5 * P, tid, rot);
+    glds_copy<BS>(m.qstatE + (size_t)e * QE_N * Q, s_qk, 2 * QE_KEEP * Q, tid, rot);
+    glds_copy<BS>(a.ecoef + (size_t)e * C::ECO + 4 * Q, s_nc, 2 * 5 * P, tid, rot);
     glds_copy<BS>(m.nstatE + (size_t)e * NE_N * P, s_ns, 2 * NE_N * P, tid, rot);
     glds_copy<BS>(m.efstat + (size_t)e * 4 * C::FBLK, s_ef, 2 * 4 * C::FBLK, tid, rot);
-    glds_copy<BS>(a.efcoef + (size_t)e * 4 * C::EFC, s_ec, 2 * 4 * C::EFC, tid, rot);
     glds_copy<BS>(a.trace_in + (size_t)e * 32 * NGL, s_tr, 2 * 32 * NGL, tid, rot);
-    if (a.accumulate) {
-      glds_copy<BS>(a.qacc + (size_t)e * QA_N * Q, s_qa, 2 * QA_N * Q, tid, rot);
-      glds_copy<BS>(a.nacc + (size_t)e * NA_N * P, s_nacc_old, 2 * NA_N * P, tid, rot);
-      glds_copy<BS>(a.facc + (size_t)e * 4 * FA_N * NQ, s_fa, 2 * 4 * FA_N * NQ, tid, rot);
-      glds_copy<BS>(a.gfacc + (size_t)e * 4 * 8 * NGL, s_ga, 2 * 4 * 8 * NGL, tid, rot);
-    }
+    glds_copy<BS>(a.efcoef + (size_t)e * 4 * C::EFC, s_ec, 2 * 4 * C::EFC, tid, rot);
+  }
+  // Register loads for this thread's quad-point task in B (quad point tid), issued before
+  // the wait so they overlap the LDS copies and the interpolation: the remaining quad
+  // statics (coriolis, tau_wind, grad_zbot, 1/pb) and the baroclinic coefficients.
+  // (The time averages are never read here: every stage adds its values with a global
+  // float64 atomic add, which rounds exactly as acc = acc + x and, one stage per launch,
+  // keeps the reference's summation order.)
+  constexpr int NST = QE_N - QE_KEEP, NPRE = NST + 4;
+  double pre[NPRE];
+  if (tid < Q) {
+    const double *qse = m.qstatE + (size_t)e * QE_N * Q + tid;
+#pragma unroll
+    for (int k = 0; k < NST; k++) pre[k] = qse[(QE_KEEP + k) * Q];
+    const double *eco = a.ecoef + (size_t)e * C::ECO + tid;
+#pragma unroll
+    for (int k = 0; k < 4; k++) pre[NST + k] = eco[k * Q];
   }
   __syncthreads();
-  // u_bar, v_bar of the stage-input state, once per node (Uk of mod_laplacian_quad.F90:48-49)
-  if constexpr (!SF) {
-    for (int p = tid; p < P; p += BS) {
-      s_u[p] = s_qb[p * 4 + 2] / s_qb[p * 4];
-      s_v[p] = s_qb[p * 4 + 3] / s_qb[p * 4];
-    }
-  } else {
-    // + first pass of the nodal -> quad interpolation (mod_rhs_btp.F90:141-152):
-    // Y(var, mm, iq) = sum_n psiq(n, iq) X(var, n + mm*NGL); groups (dp, dpp) | (udp, vdp) |
-    // bottom-layer (pp, up, vp)
-    constexpr int NT1 = NQ * NGL;
+  STAGE_MARK(21);
+
+  // ------------------------------------------------------------- A2
+  // u_bar, v_bar of the stage-input state once per node (Uk of mod_laplacian_quad.F90:48-49);
+  // the face-node wall normals; and the nodal -> quad interpolations of mod_rhs_btp.F90:
+  // 141-152, split over threads by variable group: (dp, dpp) | (udp, vdp) | bottom-layer
+  // (pp, up, vp).  exact: one thread per (group, quad point), the reference's ordered
+  // 25-term sum with PSIH = psiq(n,iq)*psiq(mm,jq); SF: first pass of the factorised sum,
+  // Y(var, mm, iq) = sum_n psiq(n, iq) X(var, n + mm*NGL), one thread per (group, mm, iq).
+  {
     const int ng = m.botfr ? 3 : 2;
-    for (int w = tid; w < P + ng * NT1; w += BS) {
+    constexpr int TPG = SF ? NQ * NGL : Q;  // tasks per group
+    const int nint = ng * TPG;
+    for (int w = tid; w < nint + 8 * NGL + P; w += BS) {
       asm volatile("" ::: "memory");
-      if (w < P) {
-        s_u[w] = s_qb[w * 4 + 2] / s_qb[w * 4];
-        s_v[w] = s_qb[w * 4 + 3] / s_qb[w * 4];
-        continue;
-      }
-      const int t = w - P, g = t / NT1, r = t % NT1, mm = r / NQ, iq = r % NQ;
-      double pa[NGL];
+      if (w < nint) {
+        const int g = w / TPG, r = w % TPG;
+        if constexpr (SF) {
+          const int mm = r / NQ, iq = r % NQ;
+          double pa[NGL];
 #pragma unroll
-      for (int n = 0; n < NGL; n++) pa[n] = s_psiq[n * NQ + iq];
-      if (g < 2) {
-        double x0 = 0.0, x1 = 0.0;
+          for (int n = 0; n < NGL; n++) pa[n] = s_psiq[n * NQ + iq];
+          if (g < 2) {
+            double x0 = 0.0, x1 = 0.0;
 #pragma unroll
-        for (int n = 0; n < NGL; n++) {
-          const int ip = mm * NGL + n;
-          x0 = x0 + pa[n] * s_qb[ip * 4 + 2 * g];
-          x1 = x1 + pa[n] * s_qb[ip * 4 + 2 * g + 1];
+            for (int n = 0; n < NGL; n++) {
+              const int ip = mm * NGL + n;
+              x0 = x0 + pa[n] * s_qb[ip * 4 + 2 * g];
+              x1 = x1 + pa[n] * s_qb[ip * 4 + 2 * g + 1];
+            }
+            s_y[((2 * g) * NGL + mm) * NQ + iq] = x0;
+            s_y[((2 * g + 1) * NGL + mm) * NQ + iq] = x1;
+          } else {
+            double x0 = 0.0, x1 = 0.0, x2 = 0.0;
+#pragma unroll
+            for (int n = 0; n < NGL; n++) {
+              const int ip = mm * NGL + n;
+              x0 = x0 + pa[n] * s_qp[ip * 3 + 0];
+              x1 = x1 + pa[n] * s_qp[ip * 3 + 1];
+              x2 = x2 + pa[n] * s_qp[ip * 3 + 2];
+            }
+            s_y[(4 * NGL + mm) * NQ + iq] = x0;
+            s_y[(5 * NGL + mm) * NQ + iq] = x1;
+            s_y[(6 * NGL + mm) * NQ + iq] = x2;
+          }
+        } else {
+          const int q = r, iq = q % NQ, jq = q / NQ;
+          double pa[NGL], pb[NGL];
+#pragma unroll
+          for (int n = 0; n < NGL; n++) {
+            pa[n] = s_psiq[n * NQ + iq];
+            pb[n] = s_psiq[n * NQ + jq];
+          }
+          if (g < 2) {
+            // broadcast LDS reads (every lane of the group reads the same node)
+            double x0 = 0.0, x1 = 0.0;
+#pragma unroll 1
+            for (int mm = 0; mm < NGL; mm++)
+#pragma unroll
+              for (int n = 0; n < NGL; n++) {
+                const int ip = mm * NGL + n;
+                const double hi = pa[n] * pb[mm];  // PSIH(n,mm,iq,jq)
+                x0 = x0 + hi * s_qb[ip * 4 + 2 * g];
+                x1 = x1 + hi * s_qb[ip * 4 + 2 * g + 1];
+              }
+            s_qv[(2 * g) * Q + q] = x0;
+            s_qv[(2 * g + 1) * Q + q] = x1;
+          } else {
+            double x0 = 0.0, x1 = 0.0, x2 = 0.0;
+#pragma unroll 1
+            for (int mm = 0; mm < NGL; mm++)
+#pragma unroll
+              for (int n = 0; n < NGL; n++) {
+                const int ip = mm * NGL + n;
+                const double hi = pa[n] * pb[mm];
+                x0 = x0 + hi * s_qp[ip * 3 + 0];
+                x1 = x1 + hi * s_qp[ip * 3 + 1];
+                x2 = x2 + hi * s_qp[ip * 3 + 2];
+              }
+            s_qv[4 * Q + q] = x0;
+            s_qv[5 * Q + q] = x1;
+            s_qv[6 * Q + q] = x2;
+          }
         }
-        s_y[((2 * g) * NGL + mm) * NQ + iq] = x0;
-        s_y[((2 * g + 1) * NGL + mm) * NQ + iq] = x1;
+      } else if (w < nint + 8 * NGL) {
+        const int t = w - nint, lf = t / (2 * NGL), c = (t / NGL) & 1, n = t % NGL;
+        s_wn[t] = s_ef[lf * C::FBLK + EF_N * NQ + (c ? EFN_NY : EFN_NX) * NGL + n];
       } else {
-        double x0 = 0.0, x1 = 0.0, x2 = 0.0;
-#pragma unroll
-        for (int n = 0; n < NGL; n++) {
-          const int ip = mm * NGL + n;
-          x0 = x0 + pa[n] * s_qp[ip * 3 + 0];
-          x1 = x1 + pa[n] * s_qp[ip * 3 + 1];
-          x2 = x2 + pa[n] * s_qp[ip * 3 + 2];
-        }
-        s_y[(4 * NGL + mm) * NQ + iq] = x0;
-        s_y[(5 * NGL + mm) * NQ + iq] = x1;
-        s_y[(6 * NGL + mm) * NQ + iq] = x2;
+        const int p = w - nint - 8 * NGL;
+        s_u[p] = s_qb[p * 4 + 2] / s_qb[p * 4];
+        s_v[p] = s_qb[p * 4 + 3] / s_qb[p * 4];
       }
     }
   }
@@ -307,282 +378,196 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
   STAGE_MARK(1);
 
   // ------------------------------------------------------------- B
-  {
-    // task ranges [0,Q) quad | [OG,OG+P) grad | [OF,OF+4NQ) face | [OL,OL+4NGL) LDG, the
-    // face ranges starting on their own wave when the block is wide enough
-    constexpr int RU = 64, OG = Q, OFa = ((Q + P + RU - 1) / RU) * RU, OLa = ((OFa + 4 * NQ + RU - 1) / RU) * RU;
-    constexpr bool WIDE = OLa + 4 * NGL <= BS;
-    constexpr int OF = WIDE ? OFa : Q + P, OL = WIDE ? OLa : OF + 4 * NQ, WEND = OL + 4 * NGL;
-    for (int w = tid; w < WEND; w += BS) {
-      asm volatile("" ::: "memory");
-      if (w < Q) {
-        // ---- quad-point physics (mod_rhs_btp.F90:136-192)
-        const int q = w, iq = q % NQ, jq = q / NQ;
-        double dp = 0, dpp = 0, udp = 0, vdp = 0, pp = 0, up = 0, vp = 0;
-        if constexpr (SF) {
-          // second interpolation pass: sum_mm psiq(mm, jq) Y(var, mm, iq)
+  for (int w = tid; w < C::OL; w += BS) {
+    asm volatile("" ::: "memory");
+    if (w < Q) {
+      // ---- quad-point physics (mod_rhs_btp.F90:136-192)
+      const int q = w, iq = q % NQ, jq = q / NQ;
+      double dp = 0, dpp = 0, udp = 0, vdp = 0, pp = 0, up = 0, vp = 0;
+      if constexpr (SF) {
+        // second interpolation pass: sum_mm psiq(mm, jq) Y(var, mm, iq)
+#pragma unroll
+        for (int mm = 0; mm < NGL; mm++) {
+          const double pb = s_psiq[mm * NQ + jq];
+          const double *y = s_y + mm * NQ + iq;
+          dp = dp + pb * y[0 * NGL * NQ];
+          dpp = dpp + pb * y[1 * NGL * NQ];
+          udp = udp + pb * y[2 * NGL * NQ];
+          vdp = vdp + pb * y[3 * NGL * NQ];
+        }
+        if (m.botfr) {
 #pragma unroll
           for (int mm = 0; mm < NGL; mm++) {
             const double pb = s_psiq[mm * NQ + jq];
             const double *y = s_y + mm * NQ + iq;
-            dp = dp + pb * y[0 * NGL * NQ];
-            dpp = dpp + pb * y[1 * NGL * NQ];
-            udp = udp + pb * y[2 * NGL * NQ];
-            vdp = vdp + pb * y[3 * NGL * NQ];
-          }
-          if (m.botfr) {
-#pragma unroll
-            for (int mm = 0; mm < NGL; mm++) {
-              const double pb = s_psiq[mm * NQ + jq];
-              const double *y = s_y + mm * NQ + iq;
-              pp = pp + pb * y[4 * NGL * NQ];
-              up = up + pb * y[5 * NGL * NQ];
-              vp = vp + pb * y[6 * NGL * NQ];
-            }
-          }
-        } else {
-          double pa[NGL], pb[NGL];
-#pragma unroll
-          for (int n = 0; n < NGL; n++) {
-            pa[n] = s_psiq[n * NQ + iq];
-            pb[n] = s_psiq[n * NQ + jq];
-          }
-          const double *gq = s_qb;  // broadcast LDS reads (every lane reads the same node)
-#pragma unroll 1
-          for (int mm = 0; mm < NGL; mm++)
-#pragma unroll
-            for (int n = 0; n < NGL; n++) {
-              const int ip = mm * NGL + n;
-              const double hi = pa[n] * pb[mm];  // PSIH(n,mm,iq,jq)
-              dp = dp + hi * gq[ip * 4 + 0];
-              dpp = dpp + hi * gq[ip * 4 + 1];
-              udp = udp + hi * gq[ip * 4 + 2];
-              vdp = vdp + hi * gq[ip * 4 + 3];
-            }
-          if (m.botfr) {
-            const double *gp = s_qp;
-#pragma unroll 1
-            for (int mm = 0; mm < NGL; mm++)
-#pragma unroll
-              for (int n = 0; n < NGL; n++) {
-                const int ip = mm * NGL + n;
-                const double hi = pa[n] * pb[mm];
-                pp = pp + hi * gp[ip * 3 + 0];
-                up = up + hi * gp[ip * 3 + 1];
-                vp = vp + hi * gp[ip * 3 + 2];
-              }
+            pp = pp + pb * y[4 * NGL * NQ];
+            up = up + pb * y[5 * NGL * NQ];
+            vp = vp + pb * y[6 * NGL * NQ];
           }
         }
-        const double cor = s_qr[(QE_COR - QE_KEEP) * Q + q];
-        const double tw1 = s_qr[(QE_TW1 - QE_KEEP) * Q + q], tw2 = s_qr[(QE_TW2 - QE_KEEP) * Q + q];
-        const double gz1 = s_qr[(QE_GZ1 - QE_KEEP) * Q + q], gz2 = s_qr[(QE_GZ2 - QE_KEEP) * Q + q];
-        const double oop = s_qr[(QE_OOP - QE_KEEP) * Q + q];
-        const double ub = udp / dp, vb = vdp / dp;
-        double tb_u = 0.0, tb_v = 0.0;
-        if (m.botfr == 1) {
-          const double ubot = up + ub, vbot = vp + vb;
-          const double spd = (m.cd / m.gravity) * pp;
-          tb_u = spd * ubot;
-          tb_v = spd * vbot;
-        } else if (m.botfr == 2) {
-          const double ubot = up + ub, vbot = vp + vb;
-          const double spd = (m.cd / m.alpha[m.L - 1]) * sqrt(ubot * ubot + vbot * vbot);
-          tb_u = spd * ubot;
-          tb_v = spd * vbot;
+      } else {
+        dp = s_qv[0 * Q + q];
+        dpp = s_qv[1 * Q + q];
+        udp = s_qv[2 * Q + q];
+        vdp = s_qv[3 * Q + q];
+        if (m.botfr) {
+          pp = s_qv[4 * Q + q];
+          up = s_qv[5 * Q + q];
+          vp = s_qv[6 * Q + q];
         }
-        const double g = m.gravity;
-        const double sc_x = cor * vdp + g * (tw1 - tb_u) - g * dp * gz1;
-        const double sc_y = -cor * udp + g * (tw2 - tb_v) - g * dp * gz2;
-        const double ope = 1.0 + dpp * oop;
-        const double Hq = (ope * ope) * s_qc[QC_HBCL * Q + q];
-        const double qu = ub * udp + ope * s_qc[QC_QUU * Q + q];
-        const double quv = ub * vdp + ope * s_qc[QC_QUV * Q + q];
-        const double qv = vb * vdp + ope * s_qc[QC_QVV * Q + q];
-        if (a.accumulate) {  // time averages (mod_rk_mlswe.F90:107-113)
-          double add[QA_N];
-          add[QA_H] = Hq; add[QA_QU] = qu; add[QA_QV] = qv; add[QA_QUV] = quv;
-          add[QA_TBU] = tb_u; add[QA_TBV] = tb_v; add[QA_OPE] = ope; add[QA_OPE2] = ope * ope;
-          add[QA_MFX] = udp; add[QA_MFY] = vdp; add[QA_UB] = ub; add[QA_VB] = vb;
+      }
+      const double cor = pre[QE_COR - QE_KEEP];
+      const double tw1 = pre[QE_TW1 - QE_KEEP], tw2 = pre[QE_TW2 - QE_KEEP];
+      const double gz1 = pre[QE_GZ1 - QE_KEEP], gz2 = pre[QE_GZ2 - QE_KEEP];
+      const double oop = pre[QE_OOP - QE_KEEP];
+      const double ub = udp / dp, vb = vdp / dp;
+      double tb_u = 0.0, tb_v = 0.0;
+      if (m.botfr == 1) {
+        const double ubot = up + ub, vbot = vp + vb;
+        const double spd = (m.cd / m.gravity) * pp;
+        tb_u = spd * ubot;
+        tb_v = spd * vbot;
+      } else if (m.botfr == 2) {
+        const double ubot = up + ub, vbot = vp + vb;
+        const double spd = (m.cd / m.alpha[m.L - 1]) * sqrt(ubot * ubot + vbot * vbot);
+        tb_u = spd * ubot;
+        tb_v = spd * vbot;
+      }
+      const double g = m.gravity;
+      const double sc_x = cor * vdp + g * (tw1 - tb_u) - g * dp * gz1;
+      const double sc_y = -cor * udp + g * (tw2 - tb_v) - g * dp * gz2;
+      const double ope = 1.0 + dpp * oop;
+      const double Hq = (ope * ope) * pre[NST + QC_HBCL];
+      const double qu = ub * udp + ope * pre[NST + QC_QUU];
+      const double quv = ub * vdp + ope * pre[NST + QC_QUV];
+      const double qv = vb * vdp + ope * pre[NST + QC_QVV];
+      if (a.accumulate) {  // time averages (mod_rk_mlswe.F90:107-113)
+        double add[QA_N];
+        add[QA_H] = Hq; add[QA_QU] = qu; add[QA_QV] = qv; add[QA_QUV] = quv;
+        add[QA_TBU] = tb_u; add[QA_TBV] = tb_v; add[QA_OPE] = ope; add[QA_OPE2] = ope * ope;
+        add[QA_MFX] = udp; add[QA_MFY] = vdp; add[QA_UB] = ub; add[QA_VB] = vb;
 #pragma unroll
-          for (int k = 0; k < QA_N; k++) a.qacc[QACC_I(k, e, q)] = s_qa[k * Q + q] + add[k];
-        }
-        if constexpr (SF) {
-          // weighted integrands of T(v) = wq*(hi*S_v + dhdx*X_v + dhdy*Y_v) split by basis
-          // factor: psi*psi -> F_v = wq*S_v, dpsi*psi -> G_v = wq*(e_x X_v + e_y Y_v),
-          // psi*dpsi -> H_v = wq*(n_x X_v + n_y Y_v)  (create_rhs_btp_volume_qdf, :194-206)
-          const double wq = s_qk[QE_W * Q + q], ex = s_qk[QE_EX * Q + q], ey = s_qk[QE_EY * Q + q];
-          const double nx = s_qk[QE_NX * Q + q], ny = s_qk[QE_NY * Q + q];
-          const double A = Hq + qu, B = Hq + qv;
-          s_qv[0 * Q + q] = wq * sc_x;
-          s_qv[1 * Q + q] = wq * sc_y;
-          s_qv[2 * Q + q] = wq * (ex * udp + ey * vdp);
-          s_qv[3 * Q + q] = wq * (ex * A + ey * quv);
-          s_qv[4 * Q + q] = wq * (ex * quv + ey * B);
-          s_qv[5 * Q + q] = wq * (nx * udp + ny * vdp);
-          s_qv[6 * Q + q] = wq * (nx * A + ny * quv);
-          s_qv[7 * Q + q] = wq * (nx * quv + ny * B);
-        } else {
-          s_qv[0 * Q + q] = udp;
-          s_qv[1 * Q + q] = vdp;
-          s_qv[2 * Q + q] = sc_x;
-          s_qv[3 * Q + q] = Hq + qu;
-          s_qv[4 * Q + q] = quv;
-          s_qv[5 * Q + q] = sc_y;
-          s_qv[6 * Q + q] = Hq + qv;
-        }
-      } else if (w >= OG && w < OG + P) {
-        // ---- nodal grad(u_bar) (compute_gradient_uv) + stage-start nodal averages
-        const int p = w - OG, i = p % NGL, j = p / NGL;
-        double g[4];
-        nodal_grad4<NGL>(s_dpsi, i, j, s_ns[NE_EX * P + p], s_ns[NE_EY * P + p], s_ns[NE_NX * P + p],
-                         s_ns[NE_NY * P + p], s_u, s_v, g);
+        for (int k = 0; k < QA_N; k++) atomicAdd(&a.qacc[QACC_I(k, e, q)], add[k]);
+      }
+      if constexpr (SF) {
+        // weighted integrands of T(v) = wq*(hi*S_v + dhdx*X_v + dhdy*Y_v) split by basis
+        // factor: psi*psi -> F_v = wq*S_v, dpsi*psi -> G_v = wq*(e_x X_v + e_y Y_v),
+        // psi*dpsi -> H_v = wq*(n_x X_v + n_y Y_v)  (create_rhs_btp_volume_qdf, :194-206)
+        const double wq = s_qk[QE_W * Q + q], ex = s_qk[QE_EX * Q + q], ey = s_qk[QE_EY * Q + q];
+        const double nx = s_qk[QE_NX * Q + q], ny = s_qk[QE_NY * Q + q];
+        const double A = Hq + qu, B = Hq + qv;
+        s_qv[0 * Q + q] = wq * sc_x;
+        s_qv[1 * Q + q] = wq * sc_y;
+        s_qv[2 * Q + q] = wq * (ex * udp + ey * vdp);
+        s_qv[3 * Q + q] = wq * (ex * A + ey * quv);
+        s_qv[4 * Q + q] = wq * (ex * quv + ey * B);
+        s_qv[5 * Q + q] = wq * (nx * udp + ny * vdp);
+        s_qv[6 * Q + q] = wq * (nx * A + ny * quv);
+        s_qv[7 * Q + q] = wq * (nx * quv + ny * B);
+      } else {
+        s_qv[0 * Q + q] = udp;
+        s_qv[1 * Q + q] = vdp;
+        s_qv[2 * Q + q] = sc_x;
+        s_qv[3 * Q + q] = Hq + qu;
+        s_qv[4 * Q + q] = quv;
+        s_qv[5 * Q + q] = sc_y;
+        s_qv[6 * Q + q] = Hq + qv;
+      }
+    } else if (w >= C::OF && w < C::OF + 4 * NQ) {
+      // ---- creat_btp_fluxes_qdf at (face lf, quad iq) (mod_rhs_btp.F90:246-337)
+      const int t = w - C::OF, lf = t / NQ, iq = t % NQ;
+      const int side = s_side[lf], er = s_bc[lf];
+      const bool keep = a.accumulate && s_acc[lf];
+      const double *ef = s_ef + lf * C::FBLK, *efn = ef + EF_N * NQ;
+      const double *ec = s_ec + lf * C::EFC;
+      const double *tr = s_tr + lf * 8 * NGL;
+      double ql[4] = {0, 0, 0, 0}, qr[4] = {0, 0, 0, 0}, pbl = 0.0, pbr = 0.0;
 #pragma unroll
-        for (int c = 0; c < 4; c++) s_grad[c * P + p] = g[c];
-        if (a.accumulate) {
-#pragma unroll
-          for (int c = 0; c < 4; c++) a.nacc[NACC_I(NA_G1 + c, e, p)] = s_nacc_old[(NA_G1 + c) * P + p] + g[c];
-          // mod_rk_mlswe.F90:90-92
-          const double t1 = 1.0 + s_qb[p * 4 + 1] * s_ns[NE_OOP * P + p];
-          a.nacc[NACC_I(NA_OPE2, e, p)] = s_nacc_old[NA_OPE2 * P + p] + t1 * t1;
-          a.nacc[NACC_I(NA_UB, e, p)] = s_nacc_old[NA_UB * P + p] + s_u[p];
-          a.nacc[NACC_I(NA_VB, e, p)] = s_nacc_old[NA_VB * P + p] + s_v[p];
-        }
-      } else if (w >= OF && w < OF + 4 * NQ) {
-        // ---- creat_btp_fluxes_qdf at (face lf, quad iq) (mod_rhs_btp.F90:246-337)
-        const int t = w - OF, lf = t / NQ, iq = t % NQ;
-        const int side = s_side[lf], er = s_bc[lf];
-        const double *ef = s_ef + lf * C::FBLK, *efn = ef + EF_N * NQ;
-        const double *ec = s_ec + lf * C::EFC;
-        const double *tr = s_tr + lf * 8 * NGL;
-        double ql[4] = {0, 0, 0, 0}, qr[4] = {0, 0, 0, 0}, pbl = 0.0, pbr = 0.0;
-#pragma unroll
-        for (int n = 0; n < NGL; n++) {
-          const double hi = s_psiq[n * NQ + iq];
-          const int p = s_map[lf * NGL + n];
-          double own[4] = {s_qb[p * 4], s_qb[p * 4 + 1], s_qb[p * 4 + 2], s_qb[p * 4 + 3]};
-          double oth[4];
-          if (er > 0) {
-#pragma unroll
-            for (int c = 0; c < 4; c++) oth[c] = tr[c * NGL + n];
-          } else {
-            // ghost state of btp_extract_df (mod_barotropic_terms.F90:75-91)
-#pragma unroll
-            for (int c = 0; c < 4; c++) oth[c] = own[c];
-            if (er == -4) {
-              const double nxn = efn[EFN_NX * NGL + n], nyn = efn[EFN_NY * NGL + n];
-              const double un = nxn * own[2] + nyn * own[3];
-              oth[2] = own[2] - 2.0 * un * nxn;
-              oth[3] = own[3] - 2.0 * un * nyn;
-            } else if (er == -2) {
-              oth[2] = -own[2];
-              oth[3] = -own[3];
-            }
-          }
-#pragma unroll
-          for (int c = 0; c < 4; c++) {
-            const double l = side == 0 ? own[c] : oth[c], r = side == 0 ? oth[c] : own[c];
-            ql[c] = ql[c] + hi * l;
-            qr[c] = qr[c] + hi * r;
-          }
-          pbl = pbl + hi * efn[EFN_PBL * NGL + n];
-          pbr = pbr + hi * efn[EFN_PBR * NGL + n];
-        }
-        const double nxl = ef[EF_NX * NQ + iq], nyl = ef[EF_NY * NQ + iq];
-        const double nxr = -nxl, nyr = -nyl;
-        const double pU_L = nxl * ql[2] + nyl * ql[3];
-        const double pU_R = nxr * qr[2] + nyr * qr[3];
-        const double pbpert_edge =
-            ef[EF_CL * NQ + iq] * ql[1] + ef[EF_CR * NQ + iq] * qr[1] + ef[EF_CLR * NQ + iq] * (pU_L + pU_R);
-        const double ope_e = 1.0 + pbpert_edge * ef[EF_OOPE * NQ + iq];
-        const double cml = ef[EF_CML * NQ + iq], cmr = ef[EF_CMR * NQ + iq], cmlr = ef[EF_CMLR * NQ + iq];
-        const double fex = cml * ql[2] + cmr * qr[2] + cmlr * (nxl * ql[1] + nxr * qr[1]);
-        const double fey = cml * ql[3] + cmr * qr[3] + cmlr * (nyl * ql[1] + nyr * qr[1]);
-        const double ul = ql[2] / ql[0], ur = qr[2] / qr[0], vl = ql[3] / ql[0], vr = qr[3] / qr[0];
-        const double quu = 0.5 * (ul * ql[2] + ur * qr[2]) + ope_e * ec[FC_QUU * NQ + iq];
-        const double quv = 0.5 * (vl * ql[2] + vr * qr[2]) + ope_e * ec[FC_QUV * NQ + iq];
-        const double qvu = 0.5 * (ul * ql[3] + ur * qr[3]) + ope_e * ec[FC_QUV * NQ + iq];
-        const double qvv = 0.5 * (vl * ql[3] + vr * qr[3]) + ope_e * ec[FC_QVV * NQ + iq];
-        const double Hf = (ope_e * ope_e) * ec[FC_HBCL * NQ + iq];
-        if (a.accumulate && s_acc[lf]) {  // face time averages, kept by one element per face
-          const double opl = 1.0 + (ql[1] / pbl), opr = 1.0 + (qr[1] / pbr);
-          double add[FA_N];
-          add[FA_MFX] = fex; add[FA_MFY] = fey; add[FA_H] = Hf; add[FA_QUU] = quu; add[FA_QUV] = quv;
-          add[FA_QVU] = qvu; add[FA_QVV] = qvv; add[FA_OPEL] = opl; add[FA_OPER] = opr;
-          add[FA_OPE2L] = opl * opl; add[FA_OPE2R] = opr * opr; add[FA_OPEE2] = ope_e * ope_e;
-          add[FA_UL] = ul; add[FA_UR] = ur; add[FA_VL] = vl; add[FA_VR] = vr;
-          const double *old = s_fa + lf * FA_N * NQ;
-#pragma unroll
-          for (int k = 0; k < FA_N; k++) a.facc[FACC_I(k, e * 4 + lf, iq)] = old[k * NQ + iq] + add[k];
-        }
-        const double H_kx = nxl * Hf, H_ky = nyl * Hf;
-        const double lamb = cmlr;
-        const double dispu = 0.5 * lamb * (qr[2] - ql[2]);
-        const double dispv = 0.5 * lamb * (qr[3] - ql[3]);
-        const double flux_x = nxl * quu + nyl * quv - dispu;
-        const double flux_y = nxl * qvu + nyl * qvv - dispv;
-        const double flux = nxl * fex + nyl * fey;
-        double *fq = s_fq + (lf * NQ + iq) * 4;
-        fq[0] = ef[EF_W * NQ + iq];
-        fq[1] = flux;
-        fq[2] = H_kx + flux_x;
-        fq[3] = H_ky + flux_y;
-      } else if (w >= OL) {
-        // ---- create_rhs_laplacian_flux at (face lf, node n) (mod_laplacian_quad.F90:452-517)
-        const int t = w - OL, lf = t / NGL, n = t % NGL;
-        const int side = s_side[lf], er = s_bc[lf];
-        const int p = s_map[lf * NGL + n], i = p % NGL, j = p / NGL;
-        const double *efn = s_ef + lf * C::FBLK + EF_N * NQ;
-        const double *B = s_ec + lf * C::EFC + 4 * NQ;  // btp_graduv_dpp_face(c) at [c][NGL]
-        const double *tr = s_tr + lf * 8 * NGL;
-        const double nxn = efn[EFN_NX * NGL + n], nyn = efn[EFN_NY * NGL + n], wq = efn[EFN_W * NGL + n];
-        double own[4];
-        nodal_grad4<NGL>(s_dpsi, i, j, s_ns[NE_EX * P + p], s_ns[NE_EY * P + p], s_ns[NE_NX * P + p],
-                         s_ns[NE_NY * P + p], s_u, s_v, own);
+      for (int n = 0; n < NGL; n++) {
+        const double hi = s_psiq[n * NQ + iq];
+        const int p = s_map[lf * NGL + n];
+        double own[4] = {s_qb[p * 4], s_qb[p * 4 + 1], s_qb[p * 4 + 2], s_qb[p * 4 + 3]};
         double oth[4];
         if (er > 0) {
 #pragma unroll
-          for (int c = 0; c < 4; c++) oth[c] = tr[(4 + c) * NGL + n];
+          for (int c = 0; c < 4; c++) oth[c] = tr[c * NGL + n];
         } else {
+          // ghost state of btp_extract_df (mod_barotropic_terms.F90:75-91)
 #pragma unroll
           for (int c = 0; c < 4; c++) oth[c] = own[c];
-          if (er == -4) {  // mod_laplacian_quad.F90:85-98
-            double un = own[0] * nxn + own[1] * nyn;
-            oth[0] = own[0] - 2.0 * un * nxn;
-            oth[1] = own[1] - 2.0 * un * nyn;
-            un = own[2] * nxn + own[3] * nyn;
+          if (er == -4) {
+            const double nxn = efn[EFN_NX * NGL + n], nyn = efn[EFN_NY * NGL + n];
+            const double un = nxn * own[2] + nyn * own[3];
             oth[2] = own[2] - 2.0 * un * nxn;
             oth[3] = own[3] - 2.0 * un * nyn;
+          } else if (er == -2) {
+            oth[2] = -own[2];
+            oth[3] = -own[3];
           }
         }
-        double gl[4], gr[4];
 #pragma unroll
         for (int c = 0; c < 4; c++) {
-          gl[c] = side == 0 ? own[c] : oth[c];
-          gr[c] = side == 0 ? oth[c] : own[c];
+          const double l = side == 0 ? own[c] : oth[c], r = side == 0 ? oth[c] : own[c];
+          ql[c] = ql[c] + hi * l;
+          qr[c] = qr[c] + hi * r;
         }
-        if (a.accumulate && s_acc[lf]) {
-          const double *old = s_ga + lf * 8 * NGL;
+        pbl = pbl + hi * efn[EFN_PBL * NGL + n];
+        pbr = pbr + hi * efn[EFN_PBR * NGL + n];
+      }
+      const double nxl = ef[EF_NX * NQ + iq], nyl = ef[EF_NY * NQ + iq];
+      const double nxr = -nxl, nyr = -nyl;
+      const double pU_L = nxl * ql[2] + nyl * ql[3];
+      const double pU_R = nxr * qr[2] + nyr * qr[3];
+      const double pbpert_edge =
+          ef[EF_CL * NQ + iq] * ql[1] + ef[EF_CR * NQ + iq] * qr[1] + ef[EF_CLR * NQ + iq] * (pU_L + pU_R);
+      const double ope_e = 1.0 + pbpert_edge * ef[EF_OOPE * NQ + iq];
+      const double cml = ef[EF_CML * NQ + iq], cmr = ef[EF_CMR * NQ + iq], cmlr = ef[EF_CMLR * NQ + iq];
+      const double fex = cml * ql[2] + cmr * qr[2] + cmlr * (nxl * ql[1] + nxr * qr[1]);
+      const double fey = cml * ql[3] + cmr * qr[3] + cmlr * (nyl * ql[1] + nyr * qr[1]);
+      const double ul = ql[2] / ql[0], ur = qr[2] / qr[0], vl = ql[3] / ql[0], vr = qr[3] / qr[0];
+      const double quu = 0.5 * (ul * ql[2] + ur * qr[2]) + ope_e * ec[FC_QUU * NQ + iq];
+      const double quv = 0.5 * (vl * ql[2] + vr * qr[2]) + ope_e * ec[FC_QUV * NQ + iq];
+      const double qvu = 0.5 * (ul * ql[3] + ur * qr[3]) + ope_e * ec[FC_QUV * NQ + iq];
+      const double qvv = 0.5 * (vl * ql[3] + vr * qr[3]) + ope_e * ec[FC_QVV * NQ + iq];
+      const double Hf = (ope_e * ope_e) * ec[FC_HBCL * NQ + iq];
+      if (keep) {  // face time averages, kept by one element per face
+        const double opl = 1.0 + (ql[1] / pbl), opr = 1.0 + (qr[1] / pbr);
+        double add[FA_N];
+        add[FA_MFX] = fex; add[FA_MFY] = fey; add[FA_H] = Hf; add[FA_QUU] = quu; add[FA_QUV] = quv;
+        add[FA_QVU] = qvu; add[FA_QVV] = qvv; add[FA_OPEL] = opl; add[FA_OPER] = opr;
+        add[FA_OPE2L] = opl * opl; add[FA_OPE2R] = opr * opr; add[FA_OPEE2] = ope_e * ope_e;
+        add[FA_UL] = ul; add[FA_UR] = ur; add[FA_VL] = vl; add[FA_VR] = vr;
 #pragma unroll
-          for (int c = 0; c < 4; c++) {
-            a.gfacc[GFACC_I(c, e * 4 + lf, n)] = old[c * NGL + n] + gl[c];
-            a.gfacc[GFACC_I(4 + c, e * 4 + lf, n)] = old[(4 + c) * NGL + n] + gr[c];
-          }
-        }
-        double fl[4], fr[4];
+        for (int k = 0; k < FA_N; k++) atomicAdd(&a.facc[FACC_I(k, e * 4 + lf, iq)], add[k]);
+      }
+      const double H_kx = nxl * Hf, H_ky = nyl * Hf;
+      const double lamb = cmlr;
+      const double dispu = 0.5 * lamb * (qr[2] - ql[2]);
+      const double dispv = 0.5 * lamb * (qr[3] - ql[3]);
+      const double flux_x = nxl * quu + nyl * quv - dispu;
+      const double flux_y = nxl * qvu + nyl * qvv - dispv;
+      const double flux = nxl * fex + nyl * fey;
+      double *fq = s_fq + (lf * NQ + iq) * 4;
+      fq[0] = ef[EF_W * NQ + iq];
+      fq[1] = flux;
+      fq[2] = H_kx + flux_x;
+      fq[3] = H_ky + flux_y;
+    } else if (w >= C::OG && w < C::OL) {
+      // ---- nodal grad(u_bar) (compute_gradient_uv) + stage-start nodal averages
+      const int p = w - C::OG, i = p % NGL, j = p / NGL;
+      double g[4];
+      nodal_grad4<NGL>(s_dpsi, i, j, s_ns[NE_EX * P + p], s_ns[NE_EY * P + p], s_ns[NE_NX * P + p],
+                       s_ns[NE_NY * P + p], s_u, s_v, g);
 #pragma unroll
-        for (int iv = 0; iv < 4; iv++) {
-          fl[iv] = B[4 * NGL + n] * gl[iv] + B[iv * NGL + n];
-          fr[iv] = B[9 * NGL + n] * gr[iv] + B[(5 + iv) * NGL + n];
-        }
-        const double beta = 0.5, alpha = 1.0 - beta;
-        const double qum0 = alpha * fl[0] + beta * fr[0], qum1 = alpha * fl[1] + beta * fr[1];
-        const double qvm0 = alpha * fl[2] + beta * fr[2], qvm1 = alpha * fl[3] + beta * fr[3];
-        const double flux_qu = (qum0 - fl[0] * nxn) + (qum1 - fl[1] * nyn);
-        const double flux_qv = (qvm0 - fl[2] * nxn) + (qvm1 - fl[3] * nyn);
-        // psi(n,n) == 1: node n receives wq*1*flux
-        const double c0 = wq * 1.0 * flux_qu, c1 = wq * 1.0 * flux_qv;
-        s_fl[(lf * NGL + n) * 2 + 0] = side == 0 ? c0 : -c0;
-        s_fl[(lf * NGL + n) * 2 + 1] = side == 0 ? c1 : -c1;
+      for (int c = 0; c < 4; c++) s_grad[c * P + p] = g[c];
+      if (a.accumulate) {
+#pragma unroll
+        for (int c = 0; c < 4; c++) atomicAdd(&a.nacc[NACC_I(NA_G1 + c, e, p)], g[c]);
+        // mod_rk_mlswe.F90:90-92
+        const double t1 = 1.0 + s_qb[p * 4 + 1] * s_ns[NE_OOP * P + p];
+        atomicAdd(&a.nacc[NACC_I(NA_OPE2, e, p)], t1 * t1);
+        atomicAdd(&a.nacc[NACC_I(NA_UB, e, p)], s_u[p]);
+        atomicAdd(&a.nacc[NACC_I(NA_VB, e, p)], s_v[p]);
       }
     }
   }
@@ -590,30 +575,7 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
   LDS_BARRIER();
   STAGE_MARK(2);
 
-  // ------------------------------------------------------------- D0 .. D_NCH
-  // term task (q in chunk k, i): T(v, p=(i,j), q) for j = 0..NGL-1
-  // (create_rhs_btp_volume_qdf, mod_rhs_btp.F90:194-206: rhs(v,I) += wq*(...))
-  auto term_task = [&](int k, int t) {
-    double *T = SB + (k & 1) * C::TSZ;
-    const int qi = t / NGL, i = t % NGL;
-    const int q = k * QC + qi, iq = q % NQ, jq = q / NQ;
-    const double wq = s_qk[QE_W * Q + q], ex = s_qk[QE_EX * Q + q], ey = s_qk[QE_EY * Q + q];
-    const double nx = s_qk[QE_NX * Q + q], ny = s_qk[QE_NY * Q + q];
-    const double udp = s_qv[0 * Q + q], vdp = s_qv[1 * Q + q], scx = s_qv[2 * Q + q], A = s_qv[3 * Q + q];
-    const double quv = s_qv[4 * Q + q], scy = s_qv[5 * Q + q], B = s_qv[6 * Q + q];
-    const double pi = s_psiq[i * NQ + iq], dpi = s_dpsiq[i * NQ + iq];
-#pragma unroll
-    for (int j = 0; j < NGL; j++) {
-      const double pj = s_psiq[j * NQ + jq], dpj = s_dpsiq[j * NQ + jq];
-      const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
-      const double dhdx = h_e * ex + h_n * nx;
-      const double dhdy = h_e * ey + h_n * ny;
-      const int p = j * NGL + i;
-      T[p * QCP + qi] = wq * (dhdx * udp + dhdy * vdp);
-      T[(P + p) * QCP + qi] = wq * (hi * scx + dhdx * A + quv * dhdy);
-      T[(2 * P + p) * QCP + qi] = wq * (hi * scy + dhdx * quv + dhdy * B);
-    }
-  };
+  // ------------------------------------------------------------- D: volume integral + LDG
   // creat_btp_fluxes_qdf projection onto node p (mod_rhs_btp.F90:339-362): left -, right +
   auto face_proj = [&](int v, int p, double acc) {
 #pragma unroll
@@ -630,6 +592,63 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
       }
     }
     return acc;
+  };
+  // create_rhs_laplacian_flux at (face lf, node n) (mod_laplacian_quad.F90:452-517), with the
+  // element's own grad(u_bar) from B
+  auto ldg_task = [&](int t, bool first) {
+    const int lf = t / NGL, n = t % NGL;
+    const int side = s_side[lf], er = s_bc[lf];
+    const bool keep = a.accumulate && s_acc[lf];
+    const int p = s_map[lf * NGL + n];
+    const double *efn = s_ef + lf * C::FBLK + EF_N * NQ;
+    const double *B = s_ec + lf * C::EFC + 4 * NQ;  // btp_graduv_dpp_face(c) at [c][NGL]
+    const double *tr = s_tr + lf * 8 * NGL;
+    const double nxn = efn[EFN_NX * NGL + n], nyn = efn[EFN_NY * NGL + n], wq = efn[EFN_W * NGL + n];
+    double own[4] = {s_grad[0 * P + p], s_grad[1 * P + p], s_grad[2 * P + p], s_grad[3 * P + p]};
+    double oth[4];
+    if (er > 0) {
+#pragma unroll
+      for (int c = 0; c < 4; c++) oth[c] = tr[(4 + c) * NGL + n];
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; c++) oth[c] = own[c];
+      if (er == -4) {  // mod_laplacian_quad.F90:85-98
+        double un = own[0] * nxn + own[1] * nyn;
+        oth[0] = own[0] - 2.0 * un * nxn;
+        oth[1] = own[1] - 2.0 * un * nyn;
+        un = own[2] * nxn + own[3] * nyn;
+        oth[2] = own[2] - 2.0 * un * nxn;
+        oth[3] = own[3] - 2.0 * un * nyn;
+      }
+    }
+    double gl[4], gr[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      gl[c] = side == 0 ? own[c] : oth[c];
+      gr[c] = side == 0 ? oth[c] : own[c];
+    }
+    if (keep) {
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        atomicAdd(&a.gfacc[GFACC_I(c, e * 4 + lf, n)], gl[c]);
+        atomicAdd(&a.gfacc[GFACC_I(4 + c, e * 4 + lf, n)], gr[c]);
+      }
+    }
+    double fl[4], fr[4];
+#pragma unroll
+    for (int iv = 0; iv < 4; iv++) {
+      fl[iv] = B[4 * NGL + n] * gl[iv] + B[iv * NGL + n];
+      fr[iv] = B[9 * NGL + n] * gr[iv] + B[(5 + iv) * NGL + n];
+    }
+    const double beta = 0.5, alpha = 1.0 - beta;
+    const double qum0 = alpha * fl[0] + beta * fr[0], qum1 = alpha * fl[1] + beta * fr[1];
+    const double qvm0 = alpha * fl[2] + beta * fr[2], qvm1 = alpha * fl[3] + beta * fr[3];
+    const double flux_qu = (qum0 - fl[0] * nxn) + (qum1 - fl[1] * nyn);
+    const double flux_qv = (qvm0 - fl[2] * nxn) + (qvm1 - fl[3] * nyn);
+    // psi(n,n) == 1: node n receives wq*1*flux
+    const double c0 = wq * 1.0 * flux_qu, c1 = wq * 1.0 * flux_qv;
+    s_fl[(lf * NGL + n) * 2 + 0] = side == 0 ? c0 : -c0;
+    s_fl[(lf * NGL + n) * 2 + 1] = side == 0 ? c1 : -c1;
   };
   // LDG volume fluxes qq (btp_compute_laplacian, mod_laplacian_quad.F90:374-380)
   auto qq_task = [&](int p) {
@@ -663,25 +682,14 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
     if (r1 >= 0) acc = acc + s_fl[r1 * 2 + c];
     s_lap[c * P + p] = acc;
   };
-  // sum task (v, p): rhs(v,p) += T over the chunk in quad order; faces after the last chunk
-  auto sum_task = [&](int k, int t) {
-    const int v = t / P, p = t % P;
-    const int nq_k = (k == NCH - 1) ? Q - k * QC : QC;
-    double acc = k == 0 ? 0.0 : s_rhs[v * P + p];
-    const double *T = SB + (k & 1) * C::TSZ + t * QCP;
-#pragma unroll
-    for (int qi = 0; qi < QC; qi++)
-      if (qi < nq_k) acc = acc + T[qi];
-    if (k == NCH - 1) acc = face_proj(v, p, acc);
-    s_rhs[v * P + p] = acc;
-  };
 
   if constexpr (SF) {
     // C1: first contraction pass over iq, per (v, i, jq):
     //   U_v(i,jq) = sum_iq psiq(i,iq) F_v + dpsiq(i,iq) G_v,  W_v(i,jq) = sum_iq psiq(i,iq) H_v
     // (F_0 = 0), with the LDG volume fluxes qq alongside
-    double *s_uw = SB;  // [3][2][NGL][NQ]
+    double *s_uw = SB + C::B_UW;  // [3][2][NGL][NQ]
     constexpr int NT1 = 3 * NGL * NQ;
+    for_tasks<BS>(tid, C::OL, 4 * NGL, ldg_task);
     for (int w = tid; w < NT1 + P; w += BS) {
       asm volatile("" ::: "memory");
       if (w < NT1) {
@@ -722,30 +730,97 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
     }
     LDS_BARRIER();
     STAGE_MARK(7);
-  } else
-  for (int k = 0; k <= NCH; k++) {
-    asm volatile("" ::: "memory");  // keep LDS reads inside their phase (no hoisting)
-    const int WT = (k < NCH) ? ((k == NCH - 1) ? (Q - k * QC) : QC) * NGL : 0;  // term tasks
-    const int WS = (k >= 1) ? 3 * P : 0;                                          // sums of chunk k-1
-    // qq in D0, Laplacian sums in D1
-    const int WG = 0;
-    const int WX = (k == 0) ? P : 0;                                              // qq
-    const int WP = (k == 1) ? 2 * P : 0;                                          // Laplacian sums
-    for (int w = tid; w < WT + WS + WG + WX + WP; w += BS) {
-      asm volatile("" ::: "memory");
-      if (w < WT) {
-        term_task(k, w);
-      } else if (w < WT + WS) {
-        sum_task(k - 1, w - WT);
-      } else if (w < WT + WS + WG + WX) {
-        qq_task(w - WT - WS - WG);
-      } else {
-        const int t = w - WT - WS - WG - WX;
-        lap_task(t / P, t % P);
+  } else {
+    // D0 .. D_NCH: weak-form terms T(v,p,q) of quad-row chunk k computed in parallel into
+    // term buffer k&1 (create_rhs_btp_volume_qdf, mod_rhs_btp.F90:194-206: rhs(v,I) +=
+    // wq*(...)) while chunk k-1 is summed in quad order by one thread per (v,p); qq rides in
+    // D0, the Laplacian in the last phase.
+    // term task (q in chunk k, i): T(v, p=(i,j), q) for j = 0..NGL-1
+    auto tbuf = [&](int k) { return SB + ((k & 1) ? C::TB1 : C::TB0); };
+    auto term_task = [&](int k, int t) {
+      double *T = tbuf(k);
+      const int qi = t / NGL, i = t % NGL;
+      const int q = k * QC + qi, iq = q % NQ, jq = q / NQ;
+      const double wq = s_qk[QE_W * Q + q], ex = s_qk[QE_EX * Q + q], ey = s_qk[QE_EY * Q + q];
+      const double nx = s_qk[QE_NX * Q + q], ny = s_qk[QE_NY * Q + q];
+      const double udp = s_qv[0 * Q + q], vdp = s_qv[1 * Q + q], scx = s_qv[2 * Q + q], A = s_qv[3 * Q + q];
+      const double quv = s_qv[4 * Q + q], scy = s_qv[5 * Q + q], B = s_qv[6 * Q + q];
+      const double pi = s_psiq[i * NQ + iq], dpi = s_dpsiq[i * NQ + iq];
+#pragma unroll
+      for (int j = 0; j < NGL; j++) {
+        const double pj = s_psiq[j * NQ + jq], dpj = s_dpsiq[j * NQ + jq];
+        const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
+        const double dhdx = h_e * ex + h_n * nx;
+        const double dhdy = h_e * ey + h_n * ny;
+        const int p = j * NGL + i;
+        T[p * QCP + qi] = wq * (dhdx * udp + dhdy * vdp);
+        T[(P + p) * QCP + qi] = wq * (hi * scx + dhdx * A + quv * dhdy);
+        T[(2 * P + p) * QCP + qi] = wq * (hi * scy + dhdx * quv + dhdy * B);
       }
+    };
+    // sum task (p): rhs(v,p) += T(v,p,q) over chunk k in quad order for v = 0..2 (three
+    // independent ordered chains); the face projections after the last chunk
+    auto sum_task = [&](int k, int p) {
+      const int nq_k = (k == NCH - 1) ? Q - k * QC : QC;
+      double acc[3];
+#pragma unroll
+      for (int v = 0; v < 3; v++) acc[v] = k == 0 ? 0.0 : s_rhs[v * P + p];
+      const double *T = tbuf(k) + p * QCP;
+      // blocks of SBK quad points: their loads are issued together (bounded VGPRs)
+      constexpr int SBK = 9;
+#pragma unroll
+      for (int q0 = 0; q0 < QC; q0 += SBK) {
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int qi = q0; qi < q0 + SBK && qi < QC; qi++)
+          if (qi < nq_k) {
+#pragma unroll
+            for (int v = 0; v < 3; v++) acc[v] = acc[v] + T[v * P * QCP + qi];
+          }
+      }
+      if (k == NCH - 1) {
+        // face projections of the three components, each in the reference order
+#pragma unroll
+        for (int kf = 0; kf < 2; kf++) {
+          const int r = s_pf[2 * p + kf];
+          if (r < 0) continue;
+          const int lf = r / NGL, n = r % NGL;
+          const bool left = s_side[lf] == 0;
+          const double *fq = s_fq + lf * NQ * 4;
+#pragma unroll
+          for (int iq = 0; iq < NQ; iq++) {
+            if (iq % 3 == 0) asm volatile("" ::: "memory");  // loads issued 3 points at a time
+            const double wp = fq[iq * 4] * s_psiq[n * NQ + iq];
+#pragma unroll
+            for (int v = 0; v < 3; v++) {
+              const double c = wp * fq[iq * 4 + 1 + v];
+              acc[v] = left ? acc[v] - c : acc[v] + c;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < 3; v++) s_rhs[v * P + p] = acc[v];
+    };
+    // lanes: terms from 0, the sums on the last wave when they fit beside the terms, qq
+    // after the terms (D0), the LDG fluxes on their preload threads (D0), the Laplacian
+    // from 0 in the last phase (no terms there)
+    constexpr int WTMAX = QC * NGL;
+    constexpr int OSUM = (P <= 64 && WTMAX <= BS - 64) ? BS - 64 : WTMAX;
+#pragma unroll
+    for (int k = 0; k <= NCH; k++) {
+      asm volatile("" ::: "memory");  // keep LDS reads inside their phase (no hoisting)
+      const int WT = (k < NCH) ? ((k == NCH - 1) ? (Q - k * QC) : QC) * NGL : 0;  // term tasks
+      for_tasks<BS>(tid, 0, WT, [&](int t, bool) { term_task(k, t); });
+      if (k >= 1) for_tasks<BS>(tid, OSUM, P, [&](int t, bool) { sum_task(k - 1, t); });
+      if (k == 0) {
+        for_tasks<BS>(tid, WT, P, [&](int t, bool) { qq_task(t); });
+        for_tasks<BS>(tid, C::OL, 4 * NGL, ldg_task);
+      }
+      if (k == NCH) for_tasks<BS>(tid, 0, 2 * P, [&](int t, bool) { lap_task(t / P, t % P); });
+      LDS_BARRIER();
+      if (k < 6) STAGE_MARK(6 + k);
     }
-    LDS_BARRIER();
-    if (k < 6) STAGE_MARK(6 + k);
   }
   STAGE_MARK(3);
 
@@ -781,8 +856,7 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
       if (r < 0) continue;
       const int lf = r / NGL, n = r % NGL, er = s_bc[lf];
       if (er == -4) {
-        const double *efn = s_ef + lf * C::FBLK + EF_N * NQ;
-        const double nx = efn[EFN_NX * NGL + n], ny = efn[EFN_NY * NGL + n];
+        const double nx = s_wn[(lf * 2 + 0) * NGL + n], ny = s_wn[(lf * 2 + 1) * NGL + n];
         const double unl = qn[2] * nx + qn[3] * ny;
         qn[2] = qn[2] - unl * nx;
         qn[3] = qn[3] - unl * ny;

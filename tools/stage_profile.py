@@ -17,7 +17,7 @@ eng.ti_rk_bcl(q, qb, qp)
 ms = eng.time_stage_kernel(1)
 pr = eng.stage_profile().astype(np.int64)
 print(f"{cfg}: stage avg {ms*1e3:.1f} us (direct events)")
-for name, a, b in [("A loads", 0, 1), ("B", 1, 2), ("D all", 2, 3), ("E1 update", 3, 4), ("E2 out", 4, 5)]:
+for name, a, b in [("A loads", 0, 21), ("A2", 21, 1), ("B", 1, 2), ("D all", 2, 3), ("E1 update", 3, 4), ("E2 out", 4, 5)]:
     d = pr[:, b] - pr[:, a]
     print(f"  {name:12s} mean {d.mean():8.0f} clk  max {d.max():8.0f}")
 prev = pr[:, 2]
