@@ -144,7 +144,7 @@ struct Launch {
                        double *qp_out, int mode) {
     hipLaunchKernelGGL((mom_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
                        e->gdpp_face, e->gfacc, e->momL, e->momR, e->lapf);
-    hipLaunchKernelGGL((mom_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(BSE), 0, e->stream, e->m, qp_in, e->qacc,
+    hipLaunchKernelGGL((mom_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(MomCfg<NGL, NQ>::BS), 0, e->stream, e->m, qp_in, e->qacc,
                        e->nacc, e->dpp_graduv, e->dpprime_visc, e->momL, e->momR, e->lapf, qb, q, qp_out, mode);
   }
 };

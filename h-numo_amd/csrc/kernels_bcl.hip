@@ -742,22 +742,41 @@ __global__ void __launch_bounds__(64)
 // (mod_layer_terms.F90:529-584) and evaluate_bcl (mode 0, :198-238) / evaluate_bcl_v1
 // (mode 1, :240-270).
 template <int NGL, int NQ>
-__global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
+struct MomCfg {
+  static constexpr int P = NGL * NGL, Q = NQ * NQ;
+  static constexpr int BS = 256;
+};
+
+template <int NGL, int NQ>
+__global__ void __launch_bounds__(256, 2)
     mom_elem_kernel(DevMesh m, const double *qp_in, const double *qacc, const double *nacc, const double *dpp_graduv,
                     const double *dpprime_visc, const double *momL, const double *momR, const double *lapf,
                     const double *qb, double *q, double *qp_out, int mode) {
-  constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BS;
+  constexpr int P = MomCfg<NGL, NQ>::P, Q = MomCfg<NGL, NQ>::Q, BS = MomCfg<NGL, NQ>::BS;
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
   const double g = m.gravity, eps1 = 1.0e-20;
   __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
   __shared__ double s_qp[MAXL][3][P], s_qm2[MAXL][2][P], s_z[MAXL + 1][P];
   __shared__ double s_qm[5][Q];            // e_x, e_y, n_x, n_y, w at quad points
   __shared__ double s_nm[5][P];            // e_x, e_y, n_x, n_y, w at nodes
+  __shared__ double s_iv[MAXL][5][Q];      // interpolated dp', u', v', u*dp, v*dp per layer
   __shared__ double s_G[MAXL][6][Q];       // source_x, Hq+uu, uv, source_y, vu, Hq+vv
   __shared__ double s_qq[MAXL][4][P];      // LDG volume fluxes per layer
   __shared__ double s_r[MAXL][4][P];       // rhs_mom(2) and lap(2) per layer
-  __shared__ double s_new[MAXL][3][P];
   __shared__ int s_map[4 * NGL], s_face[4], s_side[4], s_bc[4];
+
+  // quad-point scalars for the layer-coupling task of quad point tid, in flight during
+  // the loads and the interpolation
+  double r_qa[10], r_qs[3];
+  if (tid < Q) {
+    const int kk[10] = {QA_OPE, QA_UB, QA_VB, QA_OPE2, QA_QU, QA_QUV, QA_QV, QA_H, QA_TBU, QA_TBV};
+#pragma unroll
+    for (int c = 0; c < 10; c++) r_qa[c] = qacc[QACC_I(kk[c], e, tid)];
+    const size_t Iq = (size_t)e * Q + tid;
+    r_qs[0] = m.qstat[QS_TW1 * (size_t)npq + Iq];
+    r_qs[1] = m.qstat[QS_TW2 * (size_t)npq + Iq];
+    r_qs[2] = m.qstat[QS_PB * (size_t)npq + Iq];
+  }
   load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
   if (tid < 4) {
     s_face[tid] = m.efaces[e * 4 + tid];
@@ -779,247 +798,331 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     s_nm[c][t % P] = m.nstat[(c < 4 ? NS_EX + c : NS_W) * (size_t)npoin + (size_t)e * P + t % P];
   }
   __syncthreads();
-  // layer interfaces at nodes (mod_create_rhs_mlswe.F90:320-325) and LDG volume fluxes
-  // qq = dpprime_visc*graduvb_ave + dpp_graduv (mod_laplacian_quad.F90:409-413)
-  for (int p = tid; p < P; p += BS) {
-    const size_t I = (size_t)e * P + p;
-    double z = m.nstat[NS_ZB * (size_t)npoin + I];
-    double so = sqrt(nacc[NACC_I(NA_OPE2, e, p)]);
-    s_z[L][p] = z;
-    for (int k = L - 1; k >= 0; k--) {
-      z = z + (m.alpha[k] / g) * (so * s_qp[k][0][p]);
-      s_z[k][p] = z;
-    }
-    for (int k = 0; k < L; k++) {
-      double d = dpprime_visc[(size_t)k * npoin + I];
-      for (int c = 0; c < 4; c++)
-        s_qq[k][c][p] = d * nacc[NACC_I((NA_G1 + c), e, p)] + dpp_graduv[((size_t)k * 4 + c) * npoin + I];
-    }
-  }
-  __syncthreads();
-  const double Pstress = (g / m.alpha[0]) * 50.0;
-  const double Pbstress = (g / m.alpha[L - 1]) * 10.0;
-  for (int q = tid; q < Q; q += BS) {
-    const int iq = q % NQ, jq = q / NQ;
-    const size_t Iq = (size_t)e * Q + q;
-    double qpv[MAXL][3], tuu[MAXL], tvv[MAXL], p_tmp[MAXL + 1], H_tmp[MAXL], u_udp[MAXL], v_vdp[MAXL];
-    double u_vdp[2][MAXL], gz[2][MAXL + 1];
-    double qb0 = qacc[QACC_I(QA_OPE, e, q)], qb1 = qacc[QACC_I(QA_UB, e, q)],
-           qb2 = qacc[QACC_I(QA_VB, e, q)];
-    double so2 = sqrt(qacc[QACC_I(QA_OPE2, e, q)]);
-    p_tmp[0] = 0.0;
-    for (int k = 0; k < L; k++) tuu[k] = tvv[k] = 0.0;
-    for (int k = 0; k < L; k++) {
-      double v0 = 0.0, v1 = 0.0, v2 = 0.0;
+
+  // ---- 1: per (layer, quad point) interpolations of dp', u', v', u*dp, v*dp (reference
+  //      order: PSIH(n,mm,iq,jq) over mm outer, n inner); per node the layer interfaces
+  //      (mod_create_rhs_mlswe.F90:320-325) and the LDG volume fluxes
+  //      qq = dpprime_visc*graduvb_ave + dpp_graduv (mod_laplacian_quad.F90:409-413)
+  for (int w = tid; w < L * Q + P; w += BS) {
+    if (w < L * Q) {
+      const int k = w / Q, qd = w % Q, iq = qd % NQ, jq = qd / NQ;
+      double pa[NGL], pb[NGL];
+#pragma unroll
+      for (int n = 0; n < NGL; n++) {
+        pa[n] = s_psiq[n * NQ + iq];
+        pb[n] = s_psiq[n * NQ + jq];
+      }
+      double v0 = 0.0, v1 = 0.0, v2 = 0.0, t0 = 0.0, t1 = 0.0;
+#pragma unroll 1
       for (int mm = 0; mm < NGL; mm++)
+#pragma unroll
         for (int n = 0; n < NGL; n++) {
           const int ip = mm * NGL + n;
-          const double hi = PSIH(n, mm, iq, jq);
+          const double hi = pa[n] * pb[mm];
           v0 = v0 + hi * s_qp[k][0][ip];
           v1 = v1 + hi * s_qp[k][1][ip];
           v2 = v2 + hi * s_qp[k][2][ip];
-          tuu[k] = tuu[k] + hi * s_qm2[k][0][ip];
-          tvv[k] = tvv[k] + hi * s_qm2[k][1][ip];
+          t0 = t0 + hi * s_qm2[k][0][ip];
+          t1 = t1 + hi * s_qm2[k][1][ip];
         }
-      qpv[k][0] = v0;
-      qpv[k][1] = v1;
-      qpv[k][2] = v2;
-      p_tmp[k + 1] = p_tmp[k] + so2 * v0;
-      H_tmp[k] = 0.5 * m.alpha[k] * (p_tmp[k + 1] * p_tmp[k + 1] - p_tmp[k] * p_tmp[k]);
-      double dp = v0 * qb0, u = v1 + qb1, v = v2 + qb2;
-      u_udp[k] = dp * u * u;
-      v_vdp[k] = dp * v * v;
-      u_vdp[0][k] = u * v * dp;
-      u_vdp[1][k] = v * u * dp;
-      tuu[k] = fabs(tuu[k]) + eps1;
-      tvv[k] = fabs(tvv[k]) + eps1;
-    }
-    for (int k = 0; k <= L; k++) gz[0][k] = gz[1][k] = 0.0;
-    for (int mm = 0; mm < NGL; mm++)
-      for (int n = 0; n < NGL; n++) {
-        const int ip = mm * NGL + n;
-        const double h_e = HE(n, mm, iq, jq), h_n = HN(n, mm, iq, jq);
-        const double dx = h_e * s_qm[0][q] + h_n * s_qm[2][q];
-        const double dy = h_e * s_qm[1][q] + h_n * s_qm[3][q];
-        for (int k = 0; k <= L; k++) {
-          gz[0][k] = gz[0][k] + dx * s_z[k][ip];
-          gz[1][k] = gz[1][k] + dy * s_z[k][ip];
-        }
+      s_iv[k][0][qd] = v0;
+      s_iv[k][1][qd] = v1;
+      s_iv[k][2][qd] = v2;
+      s_iv[k][3][qd] = t0;
+      s_iv[k][4][qd] = t1;
+    } else {
+      const int p = w - L * Q;
+      const size_t I = (size_t)e * P + p;
+      double z = m.nstat[NS_ZB * (size_t)npoin + I];
+      const double so = sqrt(nacc[NACC_I(NA_OPE2, e, p)]);
+      double gsum[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) gsum[c] = nacc[NACC_I((NA_G1 + c), e, p)];
+      s_z[L][p] = z;
+      for (int k = L - 1; k >= 0; k--) {
+        z = z + (m.alpha[k] / g) * (so * s_qp[k][0][p]);
+        s_z[k][p] = z;
       }
-    double su = 0, suv = 0, sv = 0, stu = 0, stv = 0, sH = 0;
-    for (int k = 0; k < L; k++) su = su + u_udp[k];
-    for (int k = 0; k < L; k++) suv = suv + u_vdp[0][k];
-    for (int k = 0; k < L; k++) sv = sv + v_vdp[k];
-    double uu_def = qacc[QACC_I(QA_QU, e, q)] - su;
-    double uv_def = qacc[QACC_I(QA_QUV, e, q)] - suv;
-    double vv_def = qacc[QACC_I(QA_QV, e, q)] - sv;
-    for (int k = 0; k < L; k++) stu = stu + tuu[k];
-    for (int k = 0; k < L; k++) stv = stv + tvv[k];
-    for (int k = 0; k < L; k++) sH = sH + H_tmp[k];
-    double oosu = 1.0 / stu, oosv = 1.0 / stv;
-    double weight = 1.0;
-    if (sH > 0.0) weight = qacc[QACC_I(QA_H, e, q)] / sH;
-    double tw1 = m.qstat[QS_TW1 * (size_t)npq + Iq], tw2 = m.qstat[QS_TW2 * (size_t)npq + Iq];
-    double tb1 = qacc[QACC_I(QA_TBU, e, q)], tb2 = qacc[QACC_I(QA_TBV, e, q)];
-    double pb = m.qstat[QS_PB * (size_t)npq + Iq];
-    double ppt0 = 0.0;
-    for (int k = 0; k < L; k++) {
-      // QUIRK (mod_create_rhs_mlswe.F90:382): qp(k) = the LAST layer's (dp',u',v') indexed by k
-      double ppt1 = ppt0 + qpv[L - 1][k];
-      double wgt = tuu[k] * oosu;
-      u_udp[k] = u_udp[k] + wgt * uu_def;
-      u_vdp[0][k] = u_vdp[0][k] + wgt * uv_def;
-      wgt = tvv[k] * oosv;
-      u_vdp[1][k] = u_vdp[1][k] + wgt * uv_def;
-      v_vdp[k] = v_vdp[k] + wgt * vv_def;
-      double Hq = H_tmp[k] * weight;
-      double temp1 = (dmin(ppt1, Pstress) - dmin(ppt0, Pstress)) / Pstress;
-      double tempbot = dmin(Pbstress, pb - ppt1) - dmin(Pbstress, pb - ppt0);
-      tempbot = tempbot / Pbstress;
-      double sx = g * (temp1 * tw1 - tempbot * tb1 + p_tmp[k] * gz[0][k] - p_tmp[k + 1] * gz[0][k + 1]);
-      double sy = g * (temp1 * tw2 - tempbot * tb2 + p_tmp[k] * gz[1][k] - p_tmp[k + 1] * gz[1][k + 1]);
-      s_G[k][0][q] = sx;
-      s_G[k][1][q] = Hq + u_udp[k];
-      s_G[k][2][q] = u_vdp[0][k];
-      s_G[k][3][q] = sy;
-      s_G[k][4][q] = u_vdp[1][k];
-      s_G[k][5][q] = Hq + v_vdp[k];
-      ppt0 = ppt1;
+#pragma unroll
+      for (int k = 0; k < MAXL; k++) {
+        if (k >= L) break;
+        const double d = dpprime_visc[(size_t)k * npoin + I];
+#pragma unroll
+        for (int c = 0; c < 4; c++) s_qq[k][c][p] = d * gsum[c] + dpp_graduv[((size_t)k * 4 + c) * npoin + I];
+      }
     }
   }
   __syncthreads();
-  // weak forms, one thread per (layer, output, node), reference accumulation order
-  for (int t = tid; t < L * 4 * P; t += BS) {
-    const int k = t / (4 * P), o = (t / P) % 4, p = t % P, i = p % NGL, j = p / NGL;
-    double acc = 0.0;
-    if (o < 2) {
-      const double *G = s_G[k][3 * o];
-      for (int q = 0; q < Q; q++) {
-        const int iq = q % NQ, jq = q / NQ;
-        const double hi = PSIH(i, j, iq, jq);
-        const double h_e = HE(i, j, iq, jq), h_n = HN(i, j, iq, jq);
-        const double dhdx = h_e * s_qm[0][q] + h_n * s_qm[2][q];
-        const double dhdy = h_e * s_qm[1][q] + h_n * s_qm[3][q];
-        double term;
-        if (o == 0)
-          term = s_qm[4][q] * (hi * G[q] + dhdx * s_G[k][1][q] + s_G[k][2][q] * dhdy);
-        else
-          term = s_qm[4][q] * (hi * G[q] + s_G[k][4][q] * dhdx + dhdy * s_G[k][5][q]);
-        acc = acc + term;
+
+  // ---- 2: per quad point the layer coupling (mod_create_rhs_mlswe.F90:326-400);
+  //      alongside, per (layer, component, node) the LDG Laplacian (mod_laplacian_quad.F90:
+  //      392-425, nonzero terms only, then the face terms :521-611)
+  const double Pstress = (g / m.alpha[0]) * 50.0;
+  const double Pbstress = (g / m.alpha[L - 1]) * 10.0;
+  for (int w = tid; w < Q + L * 2 * P; w += BS) {
+    if (w < Q) {
+      const int qd = w, iq = qd % NQ, jq = qd / NQ;
+      const double qb0 = r_qa[0], qb1 = r_qa[1], qb2 = r_qa[2];
+      const double so2 = sqrt(r_qa[3]);
+      double tuu[MAXL], tvv[MAXL], p_tmp[MAXL + 1], H_tmp[MAXL], u_udp[MAXL], v_vdp[MAXL];
+      double u_vdp0[MAXL], u_vdp1[MAXL], gz0[MAXL + 1], gz1[MAXL + 1];
+      p_tmp[0] = 0.0;
+#pragma unroll
+      for (int k = 0; k < MAXL; k++) {
+        if (k >= L) break;
+        const double v0 = s_iv[k][0][qd], v1 = s_iv[k][1][qd], v2 = s_iv[k][2][qd];
+        p_tmp[k + 1] = p_tmp[k] + so2 * v0;
+        H_tmp[k] = 0.5 * m.alpha[k] * (p_tmp[k + 1] * p_tmp[k + 1] - p_tmp[k] * p_tmp[k]);
+        const double dp = v0 * qb0, u = v1 + qb1, v = v2 + qb2;
+        u_udp[k] = dp * u * u;
+        v_vdp[k] = dp * v * v;
+        u_vdp0[k] = u * v * dp;
+        u_vdp1[k] = v * u * dp;
+        tuu[k] = fabs(s_iv[k][3][qd]) + eps1;
+        tvv[k] = fabs(s_iv[k][4][qd]) + eps1;
       }
-      const double *fw = m.fstat + FS_W * (size_t)F * NQ;
-      for (int lf = 0; lf < 4; lf++)
+#pragma unroll
+      for (int k = 0; k <= MAXL; k++) gz0[k] = gz1[k] = 0.0;
+      double pa[NGL], da[NGL], pb[NGL], db[NGL];
+#pragma unroll
+      for (int n = 0; n < NGL; n++) {
+        pa[n] = s_psiq[n * NQ + iq];
+        da[n] = s_dpsiq[n * NQ + iq];
+        pb[n] = s_psiq[n * NQ + jq];
+        db[n] = s_dpsiq[n * NQ + jq];
+      }
+      const double e0 = s_qm[0][qd], e1 = s_qm[1][qd], e2 = s_qm[2][qd], e3 = s_qm[3][qd];
+#pragma unroll 1
+      for (int mm = 0; mm < NGL; mm++)
+#pragma unroll
         for (int n = 0; n < NGL; n++) {
-          if (s_map[lf * NGL + n] != p) continue;
-          const size_t b = (size_t)s_face[lf] * NQ;
-          const bool left = s_side[lf] == 0;
-          const double *src = (left ? momL : momR) + ((size_t)k * 2 + o) * F * NQ;
-          for (int iq = 0; iq < NQ; iq++) {
-            const double c = fw[b + iq] * s_psiq[n * NQ + iq] * src[b + iq];
-            acc = left ? acc - c : acc + c;
+          const int ip = mm * NGL + n;
+          const double h_e = da[n] * pb[mm], h_n = pa[n] * db[mm];
+          const double dx = h_e * e0 + h_n * e2;
+          const double dy = h_e * e1 + h_n * e3;
+#pragma unroll
+          for (int k = 0; k <= MAXL; k++) {
+            if (k > L) break;
+            gz0[k] = gz0[k] + dx * s_z[k][ip];
+            gz1[k] = gz1[k] + dy * s_z[k][ip];
           }
         }
+      double su = 0, suv = 0, sv = 0, stu = 0, stv = 0, sH = 0;
+#pragma unroll
+      for (int k = 0; k < MAXL; k++)
+        if (k < L) su = su + u_udp[k];
+#pragma unroll
+      for (int k = 0; k < MAXL; k++)
+        if (k < L) suv = suv + u_vdp0[k];
+#pragma unroll
+      for (int k = 0; k < MAXL; k++)
+        if (k < L) sv = sv + v_vdp[k];
+      const double uu_def = r_qa[4] - su;
+      const double uv_def = r_qa[5] - suv;
+      const double vv_def = r_qa[6] - sv;
+#pragma unroll
+      for (int k = 0; k < MAXL; k++)
+        if (k < L) stu = stu + tuu[k];
+#pragma unroll
+      for (int k = 0; k < MAXL; k++)
+        if (k < L) stv = stv + tvv[k];
+#pragma unroll
+      for (int k = 0; k < MAXL; k++)
+        if (k < L) sH = sH + H_tmp[k];
+      const double oosu = 1.0 / stu, oosv = 1.0 / stv;
+      double weight = 1.0;
+      if (sH > 0.0) weight = r_qa[7] / sH;
+      const double tw1 = r_qs[0], tw2 = r_qs[1], tb1 = r_qa[8], tb2 = r_qa[9], pb_ = r_qs[2];
+      double ppt0 = 0.0;
+#pragma unroll
+      for (int k = 0; k < MAXL; k++) {
+        if (k >= L) break;
+        // QUIRK (mod_create_rhs_mlswe.F90:382): qp(k) = the LAST layer's (dp',u',v') indexed by k
+        const double ppt1 = ppt0 + s_iv[L - 1][k][qd];
+        double wgt = tuu[k] * oosu;
+        const double uu = u_udp[k] + wgt * uu_def;
+        const double uv0 = u_vdp0[k] + wgt * uv_def;
+        wgt = tvv[k] * oosv;
+        const double uv1 = u_vdp1[k] + wgt * uv_def;
+        const double vv = v_vdp[k] + wgt * vv_def;
+        const double Hq = H_tmp[k] * weight;
+        const double temp1 = (dmin(ppt1, Pstress) - dmin(ppt0, Pstress)) / Pstress;
+        double tempbot = dmin(Pbstress, pb_ - ppt1) - dmin(Pbstress, pb_ - ppt0);
+        tempbot = tempbot / Pbstress;
+        const double sx = g * (temp1 * tw1 - tempbot * tb1 + p_tmp[k] * gz0[k] - p_tmp[k + 1] * gz0[k + 1]);
+        const double sy = g * (temp1 * tw2 - tempbot * tb2 + p_tmp[k] * gz1[k] - p_tmp[k + 1] * gz1[k + 1]);
+        s_G[k][0][qd] = sx;
+        s_G[k][1][qd] = Hq + uu;
+        s_G[k][2][qd] = uv0;
+        s_G[k][3][qd] = sy;
+        s_G[k][4][qd] = uv1;
+        s_G[k][5][qd] = Hq + vv;
+        ppt0 = ppt1;
+      }
     } else {
-      const int c = o - 2;
-      for (int jj = 0; jj < NGL; jj++)
-        for (int ii = 0; ii < NGL; ii++) {
-          const int sn = jj * NGL + ii;
-          const double dx = HE_DF(i, j, ii, jj) * s_nm[0][sn] + HN_DF(i, j, ii, jj) * s_nm[2][sn];
-          const double dy = HE_DF(i, j, ii, jj) * s_nm[1][sn] + HN_DF(i, j, ii, jj) * s_nm[3][sn];
-          acc = acc - s_nm[4][sn] * (dx * s_qq[k][2 * c][sn] + dy * s_qq[k][2 * c + 1][sn]);
-        }
+      const int t = w - Q, k = t / (2 * P), c = (t / P) % 2, p = t % P, i = p % NGL, j = p / NGL;
+      double acc = 0.0;
+#pragma unroll
+      for (int r = 0; r < 2 * NGL - 1; r++) {
+        const bool mid = (r >= j) && (r < j + NGL);
+        const int jj = mid ? j : (r < j ? r : r - NGL + 1);
+        const int ii = mid ? r - j : i;
+        const int sn = jj * NGL + ii;
+        // HE_DF(i,j,ii,jj) = dpsi(i,ii) [jj==j], HN_DF(i,j,ii,jj) = dpsi(j,jj) [ii==i]
+        const double he = s_dpsi[i * NGL + ii], hn = s_dpsi[j * NGL + jj];
+        const double ex_ = he * s_nm[0][sn], ey_ = he * s_nm[1][sn];
+        const double nx_ = hn * s_nm[2][sn], ny_ = hn * s_nm[3][sn];
+        const bool both = mid && ii == i;
+        const double dx = both ? ex_ + nx_ : (mid ? ex_ : nx_);
+        const double dy = both ? ey_ + ny_ : (mid ? ey_ : ny_);
+        acc = acc - s_nm[4][sn] * (dx * s_qq[k][2 * c][sn] + dy * s_qq[k][2 * c + 1][sn]);
+      }
       for (int lf = 0; lf < 4; lf++)
         for (int n = 0; n < NGL; n++)
           if (s_map[lf * NGL + n] == p) {
             const double v = lapf[((size_t)k * 2 + c) * F * NGL + (size_t)s_face[lf] * NGL + n];
             acc = s_side[lf] == 0 ? acc + v : acc - v;
           }
+      s_r[k][2 + c][p] = acc;
     }
+  }
+  __syncthreads();
+
+  // ---- 3: weak forms, one thread per (layer, output, node), reference accumulation order
+  //      (create_rhs_dynamics_volume_layers :401-456, then Apply_layers_fluxes :778-817)
+  for (int t = tid; t < L * 2 * P; t += BS) {
+    const int k = t / (2 * P), o = (t / P) % 2, p = t % P, i = p % NGL, j = p / NGL;
+    const double *G0 = s_G[k][3 * o], *G1 = s_G[k][3 * o + 1], *G2 = s_G[k][3 * o + 2];
+    double acc = 0.0;
+#pragma unroll 1
+    for (int jq = 0; jq < NQ; jq++) {
+      const double pj = s_psiq[j * NQ + jq], dpj = s_dpsiq[j * NQ + jq];
+#pragma unroll
+      for (int iq = 0; iq < NQ; iq++) {
+        const int qd = jq * NQ + iq;
+        const double pi = s_psiq[i * NQ + iq], dpi = s_dpsiq[i * NQ + iq];
+        const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
+        const double dhdx = h_e * s_qm[0][qd] + h_n * s_qm[2][qd];
+        const double dhdy = h_e * s_qm[1][qd] + h_n * s_qm[3][qd];
+        // o = 0: w*(hi*G0 + dhdx*G1 + G2*dhdy); o = 1: w*(hi*G3 + G4*dhdx + dhdy*G5)
+        const double term = s_qm[4][qd] * (hi * G0[qd] + dhdx * G1[qd] + dhdy * G2[qd]);
+        acc = acc + term;
+      }
+    }
+    const double *fw = m.fstat + FS_W * (size_t)F * NQ;
+    for (int lf = 0; lf < 4; lf++)
+      for (int n = 0; n < NGL; n++) {
+        if (s_map[lf * NGL + n] != p) continue;
+        const size_t b = (size_t)s_face[lf] * NQ;
+        const bool left = s_side[lf] == 0;
+        const double *src = (left ? momL : momR) + ((size_t)k * 2 + o) * F * NQ;
+        for (int iq = 0; iq < NQ; iq++) {
+          const double c = fw[b + iq] * s_psiq[n * NQ + iq] * src[b + iq];
+          acc = left ? acc - c : acc + c;
+        }
+      }
     s_r[k][o][p] = acc;
   }
   __syncthreads();
-  // per node: rhs_mom, update, implicit Coriolis
+
+  // ---- 4: per node: rhs_mom, update with implicit Coriolis (mod_splitting.F90:131-173 /
+  //      :239-280), layer_mom_boundary_df on the element's wall faces in face order
+  //      (mod_layer_terms.F90:529-584), evaluate_bcl / evaluate_bcl_v1 with
+  //      extract_velocity (:198-320)
   for (int p = tid; p < P; p += BS) {
     const size_t I = (size_t)e * P + p;
     const double mi = m.nstat[NS_MINV * (size_t)npoin + I];
     const double f2 = m.nstat[NS_F2 * (size_t)npoin + I], ab = m.nstat[NS_A * (size_t)npoin + I],
                  bb = m.nstat[NS_B * (size_t)npoin + I];
-    for (int k = 0; k < L; k++) {
-      double v0 = m.visc * mi * s_r[k][2][p], v1 = m.visc * mi * s_r[k][3][p];
-      double rm0 = mi * s_r[k][0][p] + v0;
-      double rm1 = mi * s_r[k][1][p] + v1;
-      double q2 = s_qm2[k][0][p], q3 = s_qm2[k][1][p];
-      double t1 = q2 + m.dt * rm0, t2 = q3 + m.dt * rm1;
-      double tu = t1 + f2 * q3, tv = t2 - f2 * q2;
-      s_new[k][1][p] = ab * tu + bb * tv;
-      s_new[k][2][p] = -bb * tu + ab * tv;
-      s_new[k][0][p] = q[((size_t)k * npoin + I) * 3];
+    const double b1 = qb[I * 4], b3 = qb[I * 4 + 2], b4 = qb[I * 4 + 3];
+    double nw[MAXL][3];
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
+      const double v0 = m.visc * mi * s_r[k][2][p], v1 = m.visc * mi * s_r[k][3][p];
+      const double rm0 = mi * s_r[k][0][p] + v0;
+      const double rm1 = mi * s_r[k][1][p] + v1;
+      const double q2 = s_qm2[k][0][p], q3 = s_qm2[k][1][p];
+      const double t1 = q2 + m.dt * rm0, t2 = q3 + m.dt * rm1;
+      const double tu = t1 + f2 * q3, tv = t2 - f2 * q2;
+      nw[k][1] = ab * tu + bb * tv;
+      nw[k][2] = -bb * tu + ab * tv;
+      nw[k][0] = q[((size_t)k * npoin + I) * 3];
     }
-  }
-  __syncthreads();
-  // layer_mom_boundary_df on the element's wall faces, face-id order
-  for (int lf = 0; lf < 4; lf++) {
-    const int er = s_bc[lf];
-    if (er != -4 && er != -2) continue;
-    for (int n = tid; n < NGL; n += BS) {
-      const int p = s_map[lf * NGL + n];
-      const size_t fn = (size_t)s_face[lf] * NGL + n, FN = (size_t)F * NGL;
-      double nx = m.fnstat[FN_NX * FN + fn], ny = m.fnstat[FN_NY * FN + fn];
-      for (int k = 0; k < L; k++) {
-        if (er == -4) {
-          double u = s_new[k][1][p], v = s_new[k][2][p];
-          double up = u * nx + v * ny;
-          s_new[k][1][p] = u - up * nx;
-          s_new[k][2][p] = v - up * ny;
-        } else {
-          s_new[k][1][p] = 0.0;
-          s_new[k][2][p] = 0.0;
+    for (int lf = 0; lf < 4; lf++) {
+      const int er = s_bc[lf];
+      if (er != -4 && er != -2) continue;
+      for (int n = 0; n < NGL; n++) {
+        if (s_map[lf * NGL + n] != p) continue;
+        const size_t fn = (size_t)s_face[lf] * NGL + n, FN = (size_t)F * NGL;
+        const double nx = m.fnstat[FN_NX * FN + fn], ny = m.fnstat[FN_NY * FN + fn];
+#pragma unroll
+        for (int k = 0; k < MAXL; k++) {
+          if (k >= L) break;
+          if (er == -4) {
+            const double u = nw[k][1], v = nw[k][2];
+            const double up = u * nx + v * ny;
+            nw[k][1] = u - up * nx;
+            nw[k][2] = v - up * ny;
+          } else {
+            nw[k][1] = 0.0;
+            nw[k][2] = 0.0;
+          }
         }
       }
     }
-    __syncthreads();
-  }
-  // evaluate_bcl / evaluate_bcl_v1 with extract_velocity (mod_layer_terms.F90:272-320), per node
-  for (int p = tid; p < P; p += BS) {
-    const size_t I = (size_t)e * P + p;
-    const double b1 = qb[I * 4], b3 = qb[I * 4 + 2], b4 = qb[I * 4 + 3];
     double uv[MAXL][2], h[MAXL];
+#pragma unroll
     for (int pass = 0; pass < 2; pass++) {
-      for (int k = 0; k < L; k++) {
-        h[k] = s_new[k][0][p];
-        uv[k][0] = s_new[k][1][p] / h[k];
-        uv[k][1] = s_new[k][2][p] / h[k];
+#pragma unroll
+      for (int k = 0; k < MAXL; k++) {
+        if (k >= L) break;
+        h[k] = nw[k][0];
+        uv[k][0] = nw[k][1] / h[k];
+        uv[k][1] = nw[k][2] / h[k];
       }
       double ub = 0.0, vb = 0.0;
-      for (int k = 0; k < L; k++) {
+#pragma unroll
+      for (int k = 0; k < MAXL; k++) {
+        if (k >= L) break;
         ub = ub + uv[k][0] * h[k];
         vb = vb + uv[k][1] * h[k];
       }
       if (b1 > 0.0) {
         ub = ub / b1;
         vb = vb / b1;
-        for (int k = 0; k < L; k++) {
+#pragma unroll
+        for (int k = 0; k < MAXL; k++) {
+          if (k >= L) break;
           uv[k][0] = uv[k][0] - ub + b3 / b1;
           uv[k][1] = uv[k][1] - vb + b4 / b1;
         }
       } else {
-        for (int k = 0; k < L; k++) uv[k][0] = uv[k][1] = 0.0;
+#pragma unroll
+        for (int k = 0; k < MAXL; k++) uv[k][0] = uv[k][1] = 0.0;
       }
-      if (pass == 0)
-        for (int k = 0; k < L; k++) {
-          s_new[k][1][p] = uv[k][0] * h[k];
-          s_new[k][2][p] = uv[k][1] * h[k];
+      if (pass == 0) {
+#pragma unroll
+        for (int k = 0; k < MAXL; k++) {
+          if (k >= L) break;
+          nw[k][1] = uv[k][0] * h[k];
+          nw[k][2] = uv[k][1] * h[k];
         }
+      }
     }
     double ope = 0.0;
     if (mode == 0) {
-      for (int k = 0; k < L; k++) ope = ope + h[k];
+#pragma unroll
+      for (int k = 0; k < MAXL; k++)
+        if (k < L) ope = ope + h[k];
       ope = ope / m.nstat[NS_PB * (size_t)npoin + I];
     }
-    for (int k = 0; k < L; k++) {
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
       double *qq = q + ((size_t)k * npoin + I) * 3;
-      qq[1] = s_new[k][1][p];
-      qq[2] = s_new[k][2][p];
+      qq[1] = nw[k][1];
+      qq[2] = nw[k][2];
       double *o = qp_out + ((size_t)k * npoin + I) * 3;
       if (mode == 0) o[0] = h[k] / ope;
       o[1] = uv[k][0] - b3 / b1;
