@@ -337,6 +337,7 @@ static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp,
       a.write_trace = !(mstep == NB - 1 && ik == K - 1);
       a.accumulate = 1;
       a.prof = e->stage_prof;
+      a.dbg = getenv("HNUMO_STAGE_DBG") ? atoi(getenv("HNUMO_STAGE_DBG")) : 0;
       DISPATCH(e, stage(e, a));
       if (a.write_trace && e->comm_mode) {
         // ghosts take the owners' new state; their traces go into the owned elements' slots

@@ -45,6 +45,7 @@ struct StageArgs {
   double a1, a2, a3, dtt;
   int rhs_only, write_trace, accumulate;
   unsigned long long *prof;                  // optional [E][32] phase clocks (diagnostics)
+  int dbg;
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -79,11 +80,11 @@ struct StageCfg {
   static constexpr int FBLK = EF_N * NQ + EFN_N * NGL;      // efstat block per element side
   static constexpr int EFC = 4 * NQ + 10 * NGL;             // efcoef block per element side
   static constexpr int ECO = 4 * Q + 5 * P;                 // ecoef record per element
-  static constexpr int NB = 2 * NGL * NQ + NGL * NGL;       // psiq, dpsiq, dpsi
+  static constexpr int NB = 2 * NGL * NQ + NGL * NGL;       // psiq, dpsiq, dpsi (+ a zero slot)
   static_assert(Q <= BS, "one quad-point task per thread");
   // LDS arena (doubles).  Persistent (A..E); the wall normals of the face nodes are copied
   // out of the face statics (which live in the B region) for E1:
-  static constexpr int O_BASIS = 0, O_EREC = O_BASIS + NB, O_QB = O_EREC + ERSD, O_Q0 = O_QB + 4 * P,
+  static constexpr int O_BASIS = 0, O_EREC = O_BASIS + NB + 1, O_QB = O_EREC + ERSD, O_Q0 = O_QB + 4 * P,
                        O_Q2 = O_Q0 + 4 * P, O_QK = O_Q2 + 4 * P, O_NS = O_QK + QE_KEEP * Q, O_NC = O_NS + NE_N * P,
                        O_UV = O_NC + 5 * P, O_WN = O_UV + 2 * P;
   // working arrays: quad-point values (exact: the 7 integrand factors; SF: the 8 weighted
@@ -118,68 +119,70 @@ struct StageCfg {
   static constexpr int OF = WIDE ? OFa : Q, OG = WIDE ? OGa : OF + 4 * NQ, OL = OG + P, WEND = OL + 4 * NGL;
 };
 
-// The 2*NGL-1 nonzero source nodes of a nodal derivative at node (i,j), in the reference
-// loop order (outer index jj / mm, inner ii / n): r < j -> (jj=r, ii=i); j <= r < j+NGL ->
-// (jj=j, ii=r-j); r >= j+NGL -> (jj=r-NGL+1, ii=i).  Uniform trip count, no divergence.
+// Nodal derivatives at node (i,j) keep the reference's 2*NGL-1 nonzero terms (mm==j or
+// n==i) in its order.  Each term's coefficient is written uniformly as A*e + B*n with
+//   A = HE_DF coefficient = dpsi(n,i) on the row through the node (mm == j), else 0,
+//   B = HN_DF coefficient = dpsi(mm,j) on the column (n == i), else 0,
+// taken from the LDS table with a zero slot at index NGL*NGL: on the node itself both are
+// present and A*e + B*n is the reference's full expression, elsewhere the missing half adds
+// a signed zero (x + 0 == x), so the sums are the reference's without selects or branches.
 template <int NGL>
-__device__ __forceinline__ void nz_term(int r, int i, int j, int &jj, int &ii) {
-  if (r < j) {
-    jj = r;
-    ii = i;
-  } else if (r < j + NGL) {
-    jj = j;
-    ii = r - j;
-  } else {
-    jj = r - NGL + 1;
-    ii = i;
-  }
+__device__ __forceinline__ void nz_coef(int r, int i, int j, int &mm, int &n, int &ia, int &ib) {
+  const bool row = (r >= j) && (r < j + NGL);
+  mm = row ? j : (r < j ? r : r - NGL + 1);
+  n = row ? r - j : i;
+  ia = row ? n * NGL + i : NGL * NGL;
+  ib = (!row || n == i) ? mm * NGL + j : NGL * NGL;
 }
 
 // grad of u_bar at node (i,j) along one metric pair: sum over source nodes (mm,n) of
-// (HE_DF(n,mm,i,j)*ex + HN_DF(n,mm,i,j)*nx) * u(mm,n)  (mod_barotropic_terms.F90:427-441),
-// nonzero terms only (mm==j or n==i), in the reference order; u = qb(comp)/qb(0).
-// All loads and divisions are issued before the ordered sum (no dependent LDS chains).
+// (HE_DF(n,mm,i,j)*ex + HN_DF(n,mm,i,j)*nx) * u(mm,n)  (mod_barotropic_terms.F90:427-441);
+// u = qb(comp)/qb(0).  s_dpsi needs the zero slot [NGL*NGL].
 template <int NGL>
 __device__ __forceinline__ double nodal_grad(const double *s_dpsi, int i, int j, double ex, double nx,
                                              const double *s_w) {
   constexpr int NT = 2 * NGL - 1;
-  const double full = s_dpsi[i * NGL + i] * ex + s_dpsi[j * NGL + j] * nx;
-  double gsum = 0.0;
+  double A[NT], B[NT], W[NT];
 #pragma unroll
   for (int r = 0; r < NT; r++) {
-    const bool mid = (r >= j) && (r < j + NGL);
-    const int mm = mid ? j : (r < j ? r : r - NGL + 1);
-    const int n = mid ? r - j : i;
-    const double d = mid ? (n == i ? full : s_dpsi[n * NGL + i] * ex) : s_dpsi[mm * NGL + j] * nx;
-    gsum = gsum + d * s_w[mm * NGL + n];
+    int mm, n, ia, ib;
+    nz_coef<NGL>(r, i, j, mm, n, ia, ib);
+    A[r] = s_dpsi[ia];
+    B[r] = s_dpsi[ib];
+    W[r] = s_w[mm * NGL + n];
   }
+  asm volatile("" ::: "memory");  // all loads in flight before the ordered sum
+  double gsum = 0.0;
+#pragma unroll
+  for (int r = 0; r < NT; r++) gsum = gsum + (A[r] * ex + B[r] * nx) * W[r];
   return gsum;
 }
 
 // all four components grad(u_bar) = (du/dx, du/dy, dv/dx, dv/dy) at node (i,j): the same four
-// ordered sums as nodal_grad, interleaved over shared source-node loads
+// ordered sums as nodal_grad, sharing the coefficient and source-node loads
 template <int NGL>
 __device__ __forceinline__ void nodal_grad4(const double *s_dpsi, int i, int j, double ex, double ey, double nx,
                                             double ny, const double *s_u, const double *s_v, double g[4]) {
   constexpr int NT = 2 * NGL - 1;
-  const double dii = s_dpsi[i * NGL + i], djj = s_dpsi[j * NGL + j];
-  const double fullx = dii * ex + djj * nx, fully = dii * ey + djj * ny;
+  double A[NT], B[NT], U[NT], V[NT];
+#pragma unroll
+  for (int r = 0; r < NT; r++) {
+    int mm, n, ia, ib;
+    nz_coef<NGL>(r, i, j, mm, n, ia, ib);
+    A[r] = s_dpsi[ia];
+    B[r] = s_dpsi[ib];
+    U[r] = s_u[mm * NGL + n];
+    V[r] = s_v[mm * NGL + n];
+  }
+  asm volatile("" ::: "memory");
   g[0] = g[1] = g[2] = g[3] = 0.0;
 #pragma unroll
   for (int r = 0; r < NT; r++) {
-    const bool mid = (r >= j) && (r < j + NGL);
-    const int mm = mid ? j : (r < j ? r : r - NGL + 1);
-    const int n = mid ? r - j : i;
-    const int s = mm * NGL + n;
-    const double u = s_u[s], v = s_v[s];
-    const double hx = s_dpsi[n * NGL + i], hn = s_dpsi[mm * NGL + j];
-    const int kind = mid ? (n == i ? 0 : 1) : 2;  // both terms | HE_DF only | HN_DF only
-    const double d0 = kind == 0 ? fullx : (kind == 1 ? hx * ex : hn * nx);
-    const double d1 = kind == 0 ? fully : (kind == 1 ? hx * ey : hn * ny);
-    g[0] = g[0] + d0 * u;
-    g[1] = g[1] + d1 * u;
-    g[2] = g[2] + d0 * v;
-    g[3] = g[3] + d1 * v;
+    const double d0 = A[r] * ex + B[r] * nx, d1 = A[r] * ey + B[r] * ny;
+    g[0] = g[0] + d0 * U[r];
+    g[1] = g[1] + d1 * U[r];
+    g[2] = g[2] + d0 * V[r];
+    g[3] = g[3] + d1 * V[r];
   }
 }
 
@@ -281,6 +284,8 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
   }
   __syncthreads();
   STAGE_MARK(21);
+
+  if (tid == 0) S[C::O_BASIS + C::NB] = 0.0;  // zero slot of the dpsi table (nz_coef)
 
   // ------------------------------------------------------------- A2
   // u_bar, v_bar of the stage-input state once per node (Uk of mod_laplacian_quad.F90:48-49);
@@ -583,13 +588,10 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
       const int r = s_pf[2 * p + kf];
       if (r < 0) continue;
       const int lf = r / NGL, n = r % NGL;
-      const bool left = s_side[lf] == 0;
+      const double sg = s_side[lf] == 0 ? -1.0 : 1.0;  // acc - c == acc + (-c)
       const double *fq = s_fq + lf * NQ * 4;
 #pragma unroll
-      for (int iq = 0; iq < NQ; iq++) {
-        const double c = fq[iq * 4] * s_psiq[n * NQ + iq] * fq[iq * 4 + 1 + v];
-        acc = left ? acc - c : acc + c;
-      }
+      for (int iq = 0; iq < NQ; iq++) acc = acc + sg * (fq[iq * 4] * s_psiq[n * NQ + iq] * fq[iq * 4 + 1 + v]);
     }
     return acc;
   };
@@ -662,20 +664,39 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
     const int i = p % NGL, j = p / NGL;
     double acc = 0.0;
     const int qa = (2 * c) * P, qb_ = (2 * c + 1) * P;
+    // batches of LB source nodes: loads first, then the ordered updates
+    constexpr int NT = 2 * NGL - 1, LB = 3;
 #pragma unroll
-    for (int r = 0; r < 2 * NGL - 1; r++) {
-      const bool mid = (r >= j) && (r < j + NGL);
-      const int jj = mid ? j : (r < j ? r : r - NGL + 1);
-      const int ii = mid ? r - j : i;
-      const int s = jj * NGL + ii;
-      // HE_DF(i,j,ii,jj) = dpsi(i,ii) [jj==j], HN_DF(i,j,ii,jj) = dpsi(j,jj) [ii==i]
-      const double he = s_dpsi[i * NGL + ii], hn = s_dpsi[j * NGL + jj];
-      const double ex_ = he * s_ns[NE_EX * P + s], ey_ = he * s_ns[NE_EY * P + s];
-      const double nx_ = hn * s_ns[NE_NX * P + s], ny_ = hn * s_ns[NE_NY * P + s];
-      const bool both = mid && ii == i;
-      const double dx = both ? ex_ + nx_ : (mid ? ex_ : nx_);
-      const double dy = both ? ey_ + ny_ : (mid ? ey_ : ny_);
-      acc = acc - s_ns[NE_W * P + s] * (dx * s_qq[qa + s] + dy * s_qq[qb_ + s]);
+    for (int r0 = 0; r0 < NT; r0 += LB) {
+      double L_[9][LB];
+#pragma unroll
+      for (int r = r0; r < r0 + LB && r < NT; r++) {
+        const bool mid = (r >= j) && (r < j + NGL);
+        const int jj = mid ? j : (r < j ? r : r - NGL + 1);
+        const int ii = mid ? r - j : i;
+        const int s = jj * NGL + ii;
+        const int b = r - r0;
+        // HE_DF(i,j,ii,jj) = dpsi(i,ii) on the row (jj==j), HN_DF(i,j,ii,jj) = dpsi(j,jj) on
+        // the column (ii==i), the zero slot elsewhere (see nz_coef)
+        L_[0][b] = s_dpsi[mid ? i * NGL + ii : NGL * NGL];
+        L_[1][b] = s_dpsi[(!mid || ii == i) ? j * NGL + jj : NGL * NGL];
+        L_[2][b] = s_ns[NE_EX * P + s];
+        L_[3][b] = s_ns[NE_EY * P + s];
+        L_[4][b] = s_ns[NE_NX * P + s];
+        L_[5][b] = s_ns[NE_NY * P + s];
+        L_[6][b] = s_ns[NE_W * P + s];
+        L_[7][b] = s_qq[qa + s];
+        L_[8][b] = s_qq[qb_ + s];
+      }
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int r = r0; r < r0 + LB && r < NT; r++) {
+        const int b = r - r0;
+        const double he = L_[0][b], hn = L_[1][b];
+        const double dx = he * L_[2][b] + hn * L_[4][b];
+        const double dy = he * L_[3][b] + hn * L_[5][b];
+        acc = acc - L_[6][b] * (dx * L_[7][b] + dy * L_[8][b]);
+      }
     }
     const int r0 = s_pf[2 * p], r1 = s_pf[2 * p + 1];
     if (r0 >= 0) acc = acc + s_fl[r0 * 2 + c];
@@ -766,37 +787,55 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
 #pragma unroll
       for (int v = 0; v < 3; v++) acc[v] = k == 0 ? 0.0 : s_rhs[v * P + p];
       const double *T = tbuf(k) + p * QCP;
-      // blocks of SBK quad points: their loads are issued together (bounded VGPRs)
+      // blocks of SBK quad points: all loads of a block are issued before its adds (the
+      // empty asm keeps the compiler from sinking them into the dependent chain)
       constexpr int SBK = 9;
 #pragma unroll
       for (int q0 = 0; q0 < QC; q0 += SBK) {
+        double tv[3][SBK];
+#pragma unroll
+        for (int qi = q0; qi < q0 + SBK && qi < QC; qi++)
+#pragma unroll
+          for (int v = 0; v < 3; v++) tv[v][qi - q0] = qi < nq_k ? T[v * P * QCP + qi] : 0.0;
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int qi = q0; qi < q0 + SBK && qi < QC; qi++)
           if (qi < nq_k) {
 #pragma unroll
-            for (int v = 0; v < 3; v++) acc[v] = acc[v] + T[v * P * QCP + qi];
+            for (int v = 0; v < 3; v++) acc[v] = acc[v] + tv[v][qi - q0];
           }
       }
-      if (k == NCH - 1) {
-        // face projections of the three components, each in the reference order
+      if (k == NCH - 1 && !(a.dbg & 1)) {
+        // face projections of the three components, each in the reference order; a face's
+        // NQ points are loaded as one batch, and acc - c is formed as acc + (-c) (exact) so
+        // only the adds sit on the dependent chain
 #pragma unroll
         for (int kf = 0; kf < 2; kf++) {
+          asm volatile("" ::: "memory");
           const int r = s_pf[2 * p + kf];
           if (r < 0) continue;
           const int lf = r / NGL, n = r % NGL;
-          const bool left = s_side[lf] == 0;
+          const double sg = s_side[lf] == 0 ? -1.0 : 1.0;
           const double *fq = s_fq + lf * NQ * 4;
+          double c[3][NQ], fw[NQ], ps[NQ];
 #pragma unroll
           for (int iq = 0; iq < NQ; iq++) {
-            if (iq % 3 == 0) asm volatile("" ::: "memory");  // loads issued 3 points at a time
-            const double wp = fq[iq * 4] * s_psiq[n * NQ + iq];
+            fw[iq] = fq[iq * 4];
+            ps[iq] = s_psiq[n * NQ + iq];
 #pragma unroll
-            for (int v = 0; v < 3; v++) {
-              const double c = wp * fq[iq * 4 + 1 + v];
-              acc[v] = left ? acc[v] - c : acc[v] + c;
-            }
+            for (int v = 0; v < 3; v++) c[v][iq] = fq[iq * 4 + 1 + v];
           }
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int iq = 0; iq < NQ; iq++) {
+            const double wp = fw[iq] * ps[iq];
+#pragma unroll
+            for (int v = 0; v < 3; v++) c[v][iq] = sg * (wp * c[v][iq]);
+          }
+#pragma unroll
+          for (int iq = 0; iq < NQ; iq++)
+#pragma unroll
+            for (int v = 0; v < 3; v++) acc[v] = acc[v] + c[v][iq];
         }
       }
 #pragma unroll
@@ -812,12 +851,12 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
       asm volatile("" ::: "memory");  // keep LDS reads inside their phase (no hoisting)
       const int WT = (k < NCH) ? ((k == NCH - 1) ? (Q - k * QC) : QC) * NGL : 0;  // term tasks
       for_tasks<BS>(tid, 0, WT, [&](int t, bool) { term_task(k, t); });
-      if (k >= 1) for_tasks<BS>(tid, OSUM, P, [&](int t, bool) { sum_task(k - 1, t); });
+      if (k >= 1 && !((a.dbg & 4) && k == NCH)) for_tasks<BS>(tid, OSUM, P, [&](int t, bool) { sum_task(k - 1, t); });
       if (k == 0) {
         for_tasks<BS>(tid, WT, P, [&](int t, bool) { qq_task(t); });
         for_tasks<BS>(tid, C::OL, 4 * NGL, ldg_task);
       }
-      if (k == NCH) for_tasks<BS>(tid, 0, 2 * P, [&](int t, bool) { lap_task(t / P, t % P); });
+      if (k == NCH && !(a.dbg & 2)) for_tasks<BS>(tid, 0, 2 * P, [&](int t, bool) { lap_task(t / P, t % P); });
       LDS_BARRIER();
       if (k < 6) STAGE_MARK(6 + k);
     }
@@ -911,9 +950,10 @@ template <int NGL, int NQ>
 __global__ void __launch_bounds__(64) grad_trace_kernel(DevMesh m, const double *qb, double *trace, int e0) {
   constexpr int P = NGL * NGL, ERS = EREC_SIZE(NGL);
   const int e = e0 + blockIdx.x, tid = threadIdx.x;
-  __shared__ double s_dpsi[NGL * NGL], s_qb[P * 4], s_nm[4 * P], s_u[P], s_v[P];
+  __shared__ double s_dpsi[NGL * NGL + 1], s_qb[P * 4], s_nm[4 * P], s_u[P], s_v[P];
   __shared__ int s_er[ERS];
   for (int t = tid; t < NGL * NGL; t += 64) s_dpsi[t] = m.basis[2 * NGL * NQ + t];
+  if (tid == 0) s_dpsi[NGL * NGL] = 0.0;  // zero slot (nz_coef)
   for (int t = tid; t < ERS; t += 64) s_er[t] = m.erec[(size_t)e * ERS + t];
   for (int t = tid; t < 4 * P; t += 64) s_qb[t] = qb[(size_t)e * 4 * P + t];
   for (int t = tid; t < 4 * P; t += 64) s_nm[t] = m.nstatE[(size_t)e * NE_N * P + t];  // e_x, e_y, n_x, n_y

@@ -13,7 +13,10 @@ case = build_case(make_config(cfg), dense=False)
 eng = Engine(case)
 eng.set_resident(True)
 q, qb, qp = eng.state()
-eng.ti_rk_bcl(q, qb, qp)
+try:
+    eng.ti_rk_bcl(q, qb, qp)
+except Exception as ex:  # HNUMO_STAGE_DBG experiments break the physics; timing still counts
+    print("warm-up step:", ex)
 ms = eng.time_stage_kernel(1)
 pr = eng.stage_profile().astype(np.int64)
 print(f"{cfg}: stage avg {ms*1e3:.1f} us (direct events)")
