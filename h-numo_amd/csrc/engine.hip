@@ -85,6 +85,14 @@ struct hnumo_engine {
   bool capturing = false, kernel_events = false, no_graph = false;
   int summation = HNUMO_SUM_REFERENCE;        // hnumo_set_summation
   unsigned long long *stage_prof = nullptr;  // HNUMO_STAGE_PROF=1: per-element phase clocks
+  int stage_dbg = 0;                         // HNUMO_STAGE_DBG: diagnostic phase switches (timing only)
+  // persistent sub-cycle (btp_subcycle_kernel): allowed per summation mode when every element's
+  // workgroup fits on the device at once (and HNUMO_PERSISTENT != 0); used on single-rank engines
+  bool persistent_ok[2] = {false, false};
+  TraceGranule *gtr[2] = {nullptr, nullptr};  // tagged face traces of the persistent sub-cycle
+  unsigned long long *epoch = nullptr;        // tag epoch, bumped before every persistent sub-cycle
+  StageArgs *d_stages[2] = {nullptr, nullptr};  // per-stage arguments: predictor (qp), corrector (qp2)
+  int sub_final = 0;                          // qbuf index holding the sub-cycle result
 };
 
 template <typename T>
@@ -111,10 +119,31 @@ struct Launch {
       hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, true>), dim3(e->nelem_owned), dim3(StageCfg<NGL, NQ, true>::BS), 0,
                          e->stream, a);
   }
+  static void subcycle(hnumo_engine *e, const StageArgs *stages, int ns) {
+    SubArgs sa{stages, ns, e->epoch};
+    if (e->summation == HNUMO_SUM_REFERENCE)
+      hipLaunchKernelGGL((btp_subcycle_kernel<NGL, NQ, false>), dim3(e->nelem_owned),
+                         dim3(StageCfg<NGL, NQ, false>::BS), 0, e->stream, sa);
+    else
+      hipLaunchKernelGGL((btp_subcycle_kernel<NGL, NQ, true>), dim3(e->nelem_owned), dim3(StageCfg<NGL, NQ, true>::BS),
+                         0, e->stream, sa);
+  }
+  // can every workgroup of the persistent sub-cycle kernel be resident at once?
+  static void occupancy(hnumo_engine *e, int ncu) {
+    int nb0 = 0, nb1 = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb0, btp_subcycle_kernel<NGL, NQ, false>,
+                                                       StageCfg<NGL, NQ, false>::BS, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb1, btp_subcycle_kernel<NGL, NQ, true>,
+                                                       StageCfg<NGL, NQ, true>::BS, 0);
+    (void)hipGetLastError();
+    e->persistent_ok[0] = (long)nb0 * ncu >= e->nelem_owned;
+    e->persistent_ok[1] = (long)nb1 * ncu >= e->nelem_owned;
+  }
   // face traces of elements [e0, e0+n) into their neighbours' slots
-  static void grad_trace(hnumo_engine *e, const double *qb, double *gt, int e0, int n) {
+  static void grad_trace(hnumo_engine *e, const double *qb, double *gt, int e0, int n, TraceGranule *gtr = nullptr) {
     if (n > 0)
-      hipLaunchKernelGGL((grad_trace_kernel<NGL, NQ>), dim3(n), dim3(64), 0, e->stream, e->m, qb, gt, e0);
+      hipLaunchKernelGGL((grad_trace_kernel<NGL, NQ>), dim3(n), dim3(64), 0, e->stream, e->m, qb, gt, e0, gtr,
+                         e->epoch);
   }
   static void extract(hnumo_engine *e, const double *qp, double *qf, int only_dp) {
     size_t n = (size_t)e->nface * NGL;
@@ -277,6 +306,8 @@ static void exchange_qb(hnumo_engine *e, double *qb) { exchange(e, qb, 4, 1, 0);
 static void exchange_qp(hnumo_engine *e, double *qp) { exchange(e, qp, 3, e->L, 3 * (size_t)e->npoin); }
 static void exchange_dpp(hnumo_engine *e) { exchange(e, e->dpp, 1, e->L, (size_t)e->npoin); }
 
+__global__ void epoch_bump_kernel(unsigned long long *epoch) { *epoch = *epoch + 1; }
+
 static void launch_copy(hnumo_engine *e, double *dst, const double *src, size_t n) {
   (void)hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, e->stream);
 }
@@ -298,15 +329,13 @@ static void launch_bcl_coeffs(hnumo_engine *e, const double *qp, double *qf) {
   DISPATCH(e, bcl_coeffs(e, qp, qf));
 }
 
-// ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:19-151) on device state qb_state
-static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp, bool timed = false) {
-  zero_accumulators(e);
-  launch_copy(e, e->qbuf[0], qb_state, 4 * (size_t)e->npoin);
-  exchange_qb(e, e->qbuf[0]);
-  DISPATCH(e, grad_trace(e, e->qbuf[0], e->gtrace[0], 0, e->nelem));
-  if (timed && e->kernel_events) (void)hipEventRecord(e->evk0, e->stream);
+// The stages of one sub-cycle: Shu-Osher coefficients and the rotation of the four state
+// buffers (input, stage-0 state, stage-2 state of the 5-stage scheme, output) and of the two
+// trace buffers.  Returns the buffer holding the result.
+static int stage_table(hnumo_engine *e, const double *qp, std::vector<StageArgs> &out_args) {
   int cur = 0, gt = 0, qb0i = 0, qb2i = -1;
   const int K = e->K, NB = e->p.N_btp;
+  out_args.clear();
   for (int mstep = 0; mstep < NB; mstep++) {
     qb0i = cur;
     qb2i = -1;
@@ -337,19 +366,55 @@ static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp,
       a.write_trace = !(mstep == NB - 1 && ik == K - 1);
       a.accumulate = 1;
       a.prof = e->stage_prof;
-      a.dbg = getenv("HNUMO_STAGE_DBG") ? atoi(getenv("HNUMO_STAGE_DBG")) : 0;
-      DISPATCH(e, stage(e, a));
-      if (a.write_trace && e->comm_mode) {
-        // ghosts take the owners' new state; their traces go into the owned elements' slots
-        exchange_qb(e, e->qbuf[out]);
-        DISPATCH(e, grad_trace(e, e->qbuf[out], e->gtrace[1 - gt], e->nelem_owned, e->nelem - e->nelem_owned));
-      }
+      a.dbg = e->stage_dbg;
+      const int stage = (int)out_args.size();
+      a.gtr_in = e->gtr[gt];
+      a.gtr_out = e->gtr[1 - gt];
+      a.tag_in = (unsigned long long)stage + 1;
+      a.tag_out = (unsigned long long)stage + 2;
+      a.first_of_step = ik == 0;
+      a.save_q2 = K == 5 && ik == 2;
+      a.err = e->neg_flag;
+      out_args.push_back(a);
       gt = 1 - gt;
       cur = out;
       if (K == 5 && ik == 1) qb2i = out;
     }
   }
-  if (timed && e->kernel_events) (void)hipEventRecord(e->evk1, e->stream);
+  return cur;
+}
+
+static bool use_persistent(const hnumo_engine *e) { return e->comm_mode == 0 && e->persistent_ok[e->summation]; }
+
+// ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:19-151) on device state qb_state
+static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp, bool timed = false) {
+  zero_accumulators(e);
+  launch_copy(e, e->qbuf[0], qb_state, 4 * (size_t)e->npoin);
+  exchange_qb(e, e->qbuf[0]);
+  const bool pers = use_persistent(e);
+  if (pers) hipLaunchKernelGGL(epoch_bump_kernel, dim3(1), dim3(1), 0, e->stream, e->epoch);
+  DISPATCH(e, grad_trace(e, e->qbuf[0], e->gtrace[0], 0, e->nelem, pers ? e->gtr[0] : nullptr));
+  const int K = e->K, NB = e->p.N_btp;
+  int cur;
+  if (pers) {
+    if (timed && e->kernel_events) (void)hipEventRecord(e->evk0, e->stream);
+    DISPATCH(e, subcycle(e, e->d_stages[qp == e->qp ? 0 : 1], K * NB));
+    if (timed && e->kernel_events) (void)hipEventRecord(e->evk1, e->stream);
+    cur = e->sub_final;
+  } else {
+    std::vector<StageArgs> st;
+    cur = stage_table(e, qp, st);
+    if (timed && e->kernel_events) (void)hipEventRecord(e->evk0, e->stream);
+    for (const StageArgs &a : st) {
+      DISPATCH(e, stage(e, a));
+      if (a.write_trace && e->comm_mode) {
+        // ghosts take the owners' new state; their traces go into the owned elements' slots
+        exchange_qb(e, a.qb_out);
+        DISPATCH(e, grad_trace(e, a.qb_out, a.trace_out, e->nelem_owned, e->nelem - e->nelem_owned));
+      }
+    }
+    if (timed && e->kernel_events) (void)hipEventRecord(e->evk1, e->stream);
+  }
   int nblk = 1024;
   hipLaunchKernelGGL(btp_finalize_kernel, dim3(nblk), dim3(256), 0, e->stream, e->qacc, e->facc, e->nacc, e->gfacc,
                      e->tau_wind_ave, e->tau_wind, e->npq, 4 * e->nelem * e->nq, e->npoin, 4 * e->nelem * e->ngl, NB,
@@ -687,6 +752,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   eng->neg_flag = dalloc<int>(eng, 1);
   if (const char *sm = getenv("HNUMO_SUMMATION"))
     eng->summation = (sm[0] == 'r' || sm[0] == '0') ? HNUMO_SUM_REFERENCE : HNUMO_SUM_FACTORED;
+  if (const char *sd = getenv("HNUMO_STAGE_DBG")) eng->stage_dbg = atoi(sd);
   if (const char *sp = getenv("HNUMO_STAGE_PROF"))
     if (sp[0] == '1') eng->stage_prof = dalloc<unsigned long long>(eng, (size_t)eng->nelem * 32);
   if (halo && halo->nranks > 1) {
@@ -755,6 +821,26 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   m.alpha = eng->alpha;
   m.gravity = par->gravity; m.cd = par->cd_mlswe; m.visc = par->visc_mlswe; m.dt = par->dt; m.dt_btp = par->dt_btp;
   m.botfr = par->botfr;
+
+  // persistent sub-cycle: stage tables for the two sub-cycles of a step and the residency check
+  if (supported_ngl(ngl) && eng->K <= 8) {
+    eng->epoch = dalloc<unsigned long long>(eng, 1);
+    for (int b = 0; b < 2; b++) eng->gtr[b] = dalloc<TraceGranule>(eng, (size_t)E * 32 * ngl);
+    const double *qps[2] = {eng->qp, eng->qp2};
+    for (int v = 0; v < 2; v++) {
+      std::vector<StageArgs> st;
+      eng->sub_final = stage_table(eng, qps[v], st);
+      eng->d_stages[v] = dalloc<StageArgs>(eng, st.size());
+      if (eng->alloc_failed) return fail(eng, HNUMO_ERR_DEVICE, "hipMalloc failed (stage tables)");
+      HIPCHK(hipMemcpy(eng->d_stages[v], st.data(), st.size() * sizeof(StageArgs), hipMemcpyHostToDevice));
+    }
+    const char *pe = getenv("HNUMO_PERSISTENT");
+    if (!(pe && pe[0] == '0')) {
+      int ncu = 0;
+      HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, eng->device));
+      DISPATCH(eng, occupancy(eng, ncu));
+    }
+  }
   HIPCHK(hipDeviceSynchronize());
   return HNUMO_OK;
 }
@@ -821,6 +907,7 @@ static int run_steps(hnumo_engine *eng, int nsteps) {
   HIPCHK(hipGetLastError());
   if (*eng->h_neg & 1) return fail(eng, HNUMO_ERR_NEGATIVE_THICKNESS, "Negative mass in thickness at some points");
   if (*eng->h_neg & 2) return fail(eng, HNUMO_ERR_NONFINITE, "non-finite barotropic state");
+  if (*eng->h_neg & 8) return fail(eng, HNUMO_ERR_DEVICE, "persistent sub-cycle: a trace granule wait timed out");
   return 0;
 }
 
@@ -865,6 +952,8 @@ int hnumo_set_summation(hnumo_engine *eng, int mode) {
 }
 
 int hnumo_get_summation(hnumo_engine *eng) { return eng ? eng->summation : -1; }
+
+int hnumo_stage_path(hnumo_engine *eng) { return eng ? (use_persistent(eng) ? 1 : 0) : -1; }
 
 int hnumo_sync(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df) {
   if (!eng) return HNUMO_ERR_INVALID;

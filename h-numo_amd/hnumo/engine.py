@@ -55,6 +55,8 @@ def lib():
         L.hnumo_set_summation.argtypes = [vp, C.c_int]
         L.hnumo_get_summation.argtypes = [vp]
         L.hnumo_get_summation.restype = C.c_int
+        L.hnumo_stage_path.argtypes = [vp]
+        L.hnumo_stage_path.restype = C.c_int
         _lib = L
     return _lib
 
@@ -132,6 +134,11 @@ class Engine:
     @property
     def summation(self) -> str:
         return {v: k for k, v in SUMMATION.items()}[lib().hnumo_get_summation(self.h)]
+
+    @property
+    def stage_path(self) -> str:
+        """'persistent' (one launch per sub-cycle) or 'per-stage' (one launch per stage)."""
+        return "persistent" if lib().hnumo_stage_path(self.h) == 1 else "per-stage"
 
     def set_resident(self, on: bool):
         self._check(lib().hnumo_set_resident(self.h, int(on)))

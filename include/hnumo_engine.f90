@@ -77,7 +77,7 @@ module hnumo_engine_c
     public :: hnumo_engine_create, hnumo_engine_destroy, hnumo_abi_version, hnumo_ti_rk_bcl, &
         hnumo_ti_barotropic_ssprk, hnumo_btp_bcl_coeffs, hnumo_create_rhs_btp, hnumo_get_field_c, &
         hnumo_set_resident, hnumo_sync, hnumo_last_error_c, hnumo_last_error, hnumo_get_field, &
-        hnumo_set_summation, hnumo_get_summation
+        hnumo_set_summation, hnumo_get_summation, hnumo_stage_path
 
     interface
         integer(c_int) function hnumo_engine_create(mesh, statics, params, halo, device, eng) &
@@ -162,6 +162,12 @@ module hnumo_engine_c
             import :: c_int, c_ptr
             type(c_ptr), value :: eng
         end function hnumo_get_summation
+
+        ! 1: one persistent launch per barotropic sub-cycle, 0: one launch per stage
+        integer(c_int) function hnumo_stage_path(eng) bind(C, name='hnumo_stage_path')
+            import :: c_int, c_ptr
+            type(c_ptr), value :: eng
+        end function hnumo_stage_path
 
         integer(c_int) function hnumo_sync(eng, q_df, qb_df, qprime_df) bind(C, name='hnumo_sync')
             import :: c_int, c_ptr, c_double

@@ -189,6 +189,12 @@ int hnumo_sync(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df
 int hnumo_set_summation(hnumo_engine *eng, int mode);
 int hnumo_get_summation(hnumo_engine *eng);
 
+/* How the barotropic stages run: 1 = one persistent launch per sub-cycle
+ * (btp_subcycle_kernel; single-rank engines whose elements all fit on the device at once,
+ * unless HNUMO_PERSISTENT=0 at create), 0 = one launch per stage (btp_stage_kernel).
+ * Both give the same bits.                                                            */
+int hnumo_stage_path(hnumo_engine *eng);
+
 /* RCCL unique id (128 bytes) for hnumo_halo_desc.comm_id: generated by one rank and
  * broadcast by the host (MPI / torch.distributed) before hnumo_engine_create.        */
 int hnumo_rccl_unique_id(unsigned char *out128);

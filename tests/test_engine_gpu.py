@@ -212,3 +212,26 @@ def test_factored_summation_parity(cfg, case_factory, engines):
     assert rel(qbe[0], qb[0]) < TOL and np.abs(qbe[1] - qb[1]).max() / pb < TOL
     for v in (2, 3):
         assert np.abs(qbe[v] - qb[v]).max() / (pb * np.sqrt(g * pb)) < 1e-6, v
+
+
+@pytest.mark.parametrize("cfg", ["bump10", "dg25L3"])
+def test_persistent_subcycle_matches_stage_launches(cfg, case_factory, monkeypatch):
+    """The persistent sub-cycle kernel (one launch per sub-cycle, neighbour hand-offs in the
+    launch) gives the same bits as one launch per stage (HNUMO_PERSISTENT=0)."""
+    from hnumo.engine import Engine
+    case = case_factory(cfg)
+    e1 = Engine(case)
+    monkeypatch.setenv("HNUMO_PERSISTENT", "0")
+    e0 = Engine(case)
+    monkeypatch.delenv("HNUMO_PERSISTENT")
+    a, b = e1.state(), e0.state()
+    for _ in range(2):
+        e1.ti_rk_bcl(*a)
+        e0.ti_rk_bcl(*b)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    from hnumo import bundle as B
+    for f, _ in B.FIELDS:
+        assert np.array_equal(e1.field(f), e0.field(f)), f
+    e1.close()
+    e0.close()

@@ -49,3 +49,13 @@ for e in list(range(8)) + [256, 257, 512, 513]:
 key = xcc * 1000 + se[:, 0] * 100 + cu[:, 0]
 u, c = np.unique(key, return_counts=True)
 print(f"  distinct CUs used {len(u)}, blocks per CU: {np.bincount(c).tolist()}")
+
+if pr[:, 26].max() > 0:
+    nst = pr[:, 26].astype(float)
+    aw, wk = pr[:, 24] / nst, pr[:, 25] / nst
+    bpc = c[np.searchsorted(u, key)]
+    print(f"  persistent: per stage A(+waits) mean {aw.mean():.0f} clk, work mean {wk.mean():.0f} clk")
+    for k in sorted(set(bpc.tolist())):
+        sel = bpc == k
+        print(f"    CUs with {k} blocks: {sel.sum()} blocks, A(+waits) {aw[sel].mean():.0f}, work {wk[sel].mean():.0f} "
+              f"(max {wk[sel].max():.0f}) clk")
