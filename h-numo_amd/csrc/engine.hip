@@ -364,7 +364,7 @@ static int stage_table(hnumo_engine *e, const double *qp, std::vector<StageArgs>
       a.dtt = e->p.dt_btp * e->ssprk_beta[ik];
       a.rhs_only = 0;
       a.write_trace = !(mstep == NB - 1 && ik == K - 1);
-      a.accumulate = 1;
+      a.accumulate = !(e->stage_dbg & 32);  // dbg bit 32: no time averages (timing experiments)
       a.prof = e->stage_prof;
       a.dbg = e->stage_dbg;
       const int stage = (int)out_args.size();

@@ -42,10 +42,18 @@ for k in sorted(set(fetch) | set(write)):
                   "hbm_bytes_per_dispatch": (2.0 * f_kb + w_kb) * 1024.0}
 json.dump({"note": "FETCH_SIZE doubled for gfx950 (MI355X_MICROARCH.md, HBM section); kB = 1024 B",
            "kernels": summary}, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
-stage = [k for k in summary if "btp_stage_kernel" in k]
-if stage:
-    b = summary[stage[0]]["hbm_bytes_per_dispatch"]
-    json.dump({"config": "dg25L3", "kernel": stage[0], "hbm_bytes_per_launch": round(b), "source": dst},
-              open(os.path.join("profiles", "pmc_btp_stage.json"), "w"), indent=1)
-    print("stage kernel HBM bytes/launch", b)
+# dominant kernel: the persistent sub-cycle kernel (one launch = N_btp*kstages stages) or the
+# per-stage kernel; roofline.traffic is per stage, like roofline.achieved
+bj = json.load(open(os.path.join(dst, "bench.json"))) if os.path.exists(os.path.join(dst, "bench.json")) else {}
+cfgname = bj.get("config", {}).get("workload", "dg25L3:").split(":")[0] or "dg25L3"
+spl = int(sys.argv[2]) if len(sys.argv) > 2 else 100   # stages per sub-cycle launch (dg25L3: 20 x 5)
+for short, per in (("btp_subcycle_kernel", spl), ("btp_stage_kernel", 1)):
+    ks = [k for k in summary if short in k]
+    if ks:
+        b = summary[ks[0]]["hbm_bytes_per_dispatch"] / per
+        json.dump({"config": cfgname, "kernel": short, "hbm_bytes_per_launch": round(b),
+                   "note": f"per barotropic stage ({per} stage(s) per dispatch of {ks[0]})", "source": dst},
+                  open(os.path.join("profiles", "pmc_btp_stage.json"), "w"), indent=1)
+        print(short, "HBM bytes per stage", b)
+        break
 print("wrote", dst)
