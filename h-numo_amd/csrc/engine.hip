@@ -697,7 +697,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   {
     const int qmap[QE_N] = {QS_W, QS_EX, QS_EY, QS_NX, QS_NY, QS_COR, QS_TW1, QS_TW2, QS_GZ1, QS_GZ2, QS_OOP};
     const int nmap[NE_N] = {NS_EX, NS_EY, NS_NX, NS_NY, NS_W, NS_MINV, NS_PB, NS_OOP};
-    const int fmap_[EF_N] = {FS_NX, FS_NY, FS_W, FS_CL, FS_CR, FS_CLR, FS_CML, FS_CMR, FS_CMLR, FS_OOPE};
+    const int fmap_[EF_PBLQ] = {FS_NX, FS_NY, FS_W, FS_CL, FS_CR, FS_CLR, FS_CML, FS_CMR, FS_CMLR, FS_OOPE};
     const int fnmap[EFN_N] = {FN_NX, FN_NY, FN_W, FN_PBL, FN_PBR};
     for (int e = 0; e < E; e++) {
       for (int c = 0; c < QE_N; c++)
@@ -707,8 +707,18 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
       for (int lf = 0; lf < 4; lf++) {
         const size_t f = efaces[4 * e + lf];
         double *b = &efs[((size_t)e * 4 + lf) * FBLK];
-        for (int c = 0; c < EF_N; c++)
+        for (int c = 0; c < EF_PBLQ; c++)
           for (int iq = 0; iq < nq; iq++) b[c * nq + iq] = fs[fmap_[c] * FQ + f * nq + iq];
+        // creat_btp_fluxes_qdf's pbl/pbr (mod_rhs_btp.F90:255-258): same products, same order
+        for (int iq = 0; iq < nq; iq++) {
+          double pl = 0.0, pr = 0.0;
+          for (int n = 0; n < ngl; n++) {
+            pl = pl + hb[n * nq + iq] * fns[FN_PBL * FN + f * ngl + n];
+            pr = pr + hb[n * nq + iq] * fns[FN_PBR * FN + f * ngl + n];
+          }
+          b[EF_PBLQ * nq + iq] = pl;
+          b[EF_PBRQ * nq + iq] = pr;
+        }
         for (int c = 0; c < EFN_N; c++)
           for (int n = 0; n < ngl; n++) b[EF_N * nq + c * ngl + n] = fns[fnmap[c] * FN + f * ngl + n];
       }

@@ -69,7 +69,9 @@ constexpr int QE_KEEP = 5;
 // element-major nodal statics order (nstatE)
 enum NStatE { NE_EX = 0, NE_EY, NE_NX, NE_NY, NE_W, NE_MINV, NE_PB, NE_OOP, NE_N };
 // element-side face statics block: FS fields at NQ face quad points, then FN fields at NGL nodes
-enum EFStat { EF_NX = 0, EF_NY, EF_W, EF_CL, EF_CR, EF_CLR, EF_CML, EF_CMR, EF_CMLR, EF_OOPE, EF_N };
+// (EF_PBLQ/EF_PBRQ: pbprime_df_face interpolated to the face quad points, sum_n psiq(n,iq) *
+//  pbprime_df_face(s,n,f) in the reference's order -- static, so computed once on the host)
+enum EFStat { EF_NX = 0, EF_NY, EF_W, EF_CL, EF_CR, EF_CLR, EF_CML, EF_CMR, EF_CMLR, EF_OOPE, EF_PBLQ, EF_PBRQ, EF_N };
 enum EFNStat { EFN_NX = 0, EFN_NY, EFN_W, EFN_PBL, EFN_PBR, EFN_N };
 // per-element int record (erec) offsets
 #define EREC_FACE 0

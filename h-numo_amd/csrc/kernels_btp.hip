@@ -30,6 +30,17 @@
 //       next stage, written straight into the neighbours' trace slots.
 #include "engine_internal.h"
 
+// Layout/schedule variants kept for A/B measurement (tools/ab3.sh), both off by default: at
+// dg25L3 they measured slower (18.2 / 17.4 us per stage against 15.1) because the resident B
+// inputs leave room for 2-row term chunks only, i.e. two more D phases per stage.
+//   HNUMO_RES   B inputs (face statics, coefficients, traces) resident in LDS for the launch
+//   HNUMO_LATE  (with RES) face fluxes beside the volume terms, neighbour traces polled late
+#ifndef HNUMO_LATE
+#define HNUMO_LATE 0
+#endif
+#ifndef HNUMO_RES
+#define HNUMO_RES 0
+#endif
 namespace hnumo {
 
 // A trace value with the tag of the stage it is for: one 16-byte write-through store makes
@@ -50,12 +61,6 @@ __device__ __forceinline__ void st_granule(TraceGranule *p, double v, unsigned l
   asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
 }
 typedef unsigned granule_u4 __attribute__((ext_vector_type(4)));
-// issue a granule load without waiting for it (the caller waits with vmcnt before use)
-__device__ __forceinline__ granule_u4 ld_granule_issue(const TraceGranule *p) {
-  granule_u4 x;
-  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(x) : "v"(p) : "memory");
-  return x;
-}
 __device__ __forceinline__ void ld_granule(const TraceGranule *p, double &v, unsigned long long &tag) {
   typedef unsigned u4 __attribute__((ext_vector_type(4)));
   u4 x;
@@ -129,30 +134,47 @@ struct StageCfg {
   static constexpr int NQV = SF ? 8 : 7, NYV = 7;
   static constexpr int O_QV = O_WN + 8 * NGL, O_GR = O_QV + NQV * Q, O_FQ = O_GR + 4 * P, O_FL = O_FQ + 16 * NQ,
                        O_W = O_FL + 8 * NGL, O_QQ = O_W, O_RHS = O_QQ + 4 * P, O_LAP = O_RHS + 3 * P,
-                       O_QN = O_LAP + 2 * P, O_Y = O_W, W_END = O_QN + 4 * P,
-                       O_B = (SF && O_Y + NYV * NGL * NQ > W_END) ? O_Y + NYV * NGL * NQ : W_END;
-  // B region: inputs read up to B (bottom-layer qprime, face statics, neighbour traces, face
-  // coefficients), then the term buffers (exact) / contraction partials (SF)
+                       O_QN = O_LAP + 2 * P, O_Y = O_W, W_END = O_QN + 4 * P, QN_END_W = W_END - O_W,
+                       O_BIN = (SF && O_Y + NYV * NGL * NQ > W_END) ? O_Y + NYV * NGL * NQ : W_END;
+  // B inputs: the bottom-layer qprime, face statics, neighbour traces, face coefficients.
+  // RES: resident for the whole launch (the persistent sub-cycle loads them once), the work
+  // region (term buffers / contraction partials) follows; otherwise reloaded every stage and
+  // overlaid by term buffer 1 once B and the LDG fluxes (D0) are done
+  static constexpr bool RES = HNUMO_RES;
   static constexpr int B_QP = 0, B_EF = B_QP + 3 * P, B_TR = B_EF + 4 * FBLK, B_EC = B_TR + 32 * NGL,
-                       B_SIZE = B_EC + 4 * EFC;
+                       B_SIZE = B_EC + 4 * EFC, O_B = RES ? O_BIN + B_SIZE : O_BIN;
   // exact: term chunks of RC quad rows, two buffers of [3P][QCP] (odd pitch against bank
-  // conflicts), as many rows as the LDS budget allows.  Buffer 0 (D0, D2, ..) lies past the
-  // B inputs, which the LDG face fluxes still read in D0; buffer 1 overlays them.
+  // conflicts), as many rows as the LDS budget allows
   static constexpr int TAV = (BUDGET - O_B) / 2;
   static constexpr int RC0 = (TAV / (3 * P) - 1) / NQ;  // largest RC with 3P*((RC*NQ)|1) <= TAV
   static constexpr int RCM = RC0 < 1 ? 1 : (RC0 > NQ ? NQ : RC0);
   static constexpr int NCH = (NQ + RCM - 1) / RCM, RC = (NQ + NCH - 1) / NCH, QC = RC * NQ;
   static constexpr int QCP = QC | 1, TSZ = 3 * P * QCP;
-  static constexpr int TB0 = TSZ > B_SIZE ? TSZ : B_SIZE, TB1 = 0;
-  // SF: first-pass contraction partials U, W [3][2][NGL][NQ], past the B inputs (C1 runs
-  // the LDG face fluxes)
-  static constexpr int UWSZ = 3 * 2 * NGL * NQ, B_UW = B_SIZE;
-  static constexpr int ARENA = O_B + (SF ? B_SIZE + UWSZ : TB0 + TSZ);
-  // B task ranges: quad points [0,Q) | face points [OF,OF+4NQ) | nodal grad [OG,OG+P) |
-  // LDG face nodes [OL,OL+4NGL), the face and nodal ranges on their own waves when they fit
-  static constexpr int RU = 64, OFa = ((Q + RU - 1) / RU) * RU, OGa = ((OFa + 4 * NQ + RU - 1) / RU) * RU;
-  static constexpr bool WIDE = OGa + P + 4 * NGL <= BS;
-  static constexpr int OF = WIDE ? OFa : Q, OG = WIDE ? OGa : OF + 4 * NQ, OL = OG + P, WEND = OL + 4 * NGL;
+  static constexpr int TB0 = RES ? 0 : (TSZ > B_SIZE ? TSZ : B_SIZE), TB1 = RES ? TSZ : 0;
+  // SF: first-pass contraction partials U, W [3][2][NGL][NQ] (C1 runs the LDG face fluxes)
+  static constexpr int UWSZ = 3 * 2 * NGL * NQ, B_UW = RES ? 0 : B_SIZE;
+  static constexpr int ARENA = O_B + (SF ? B_UW + UWSZ : TB0 + TSZ);
+  // LATE (exact, >= 3 chunks): the neighbour traces are needed only from chunk phase KP+1 on,
+  // where the face fluxes and the LDG face fluxes run beside the volume terms; the
+  // persistent kernel polls the traces in phase KP, late in the stage, so the hand-off
+  // latency and the neighbours' skew hide behind the volume work.  Otherwise (SF, or too few
+  // chunks) the face fluxes run in B and the traces are polled after the interpolation.
+  static constexpr bool LATE = HNUMO_LATE && RES && !SF && NCH >= 3;
+  static constexpr int KP = NCH - 3;
+  // B task ranges: quad points [0,Q) | face points [OF,OF+4NQ) (early only) | nodal grad
+  // [OG,OG+P) | LDG face nodes [OL,OL+4NGL) (SF: C1), on their own
+  // waves when they fit
+  static constexpr int RU = 64, OFa = ((Q + RU - 1) / RU) * RU,
+                       OGa = LATE ? OFa : ((OFa + 4 * NQ + RU - 1) / RU) * RU;
+  static constexpr bool WIDE = OGa + P + (SF ? 4 * NGL : 0) <= BS;  // (exact: the LDG range runs in D0)
+  static constexpr int OF = WIDE ? OFa : Q, OG = WIDE ? OGa : (LATE ? Q : OF + 4 * NQ), OL = OG + P,
+                       WEND = OL + 4 * NGL, BEND = OL;
+  // FPRE (exact, not LATE): A2 also interpolates each face's own-side traces and, on physical
+  // boundaries, the ghost-side traces to the face quad points, into s_fi [4][NQ][8] (in the
+  // W region, dead from A to D0), so B's face fluxes interpolate only the neighbour traces
+  static constexpr bool FPRE = !SF && !LATE && 4 * NQ * 8 <= QN_END_W;
+  // LATE chunk phase KP+1: face fluxes from OFD, LDG fluxes from OLD, past the term tasks
+  static constexpr int WTMAX = QC * NGL, OFD = ((WTMAX + RU - 1) / RU) * RU, OLD = OFD + 4 * NQ;
 };
 
 // Nodal derivatives at node (i,j) keep the reference's 2*NGL-1 nonzero terms (mm==j or
@@ -274,11 +296,14 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   double *s_fl = S + C::O_FL;      // [4][NGL][2]
   double *s_rhs = S + C::O_RHS, *s_lap = S + C::O_LAP;  // [3][P], [2][P]
   double *s_qn = S + C::O_QN;      // [P][4]
-  double *SB = S + C::O_B;         // B-region inputs, then the term buffers / partials
-  double *s_qp = SB + C::B_QP;     // [P][3] qprime of the bottom layer
-  double *s_ef = SB + C::B_EF;     // [4][FBLK]
-  double *s_tr = SB + C::B_TR;     // [4][8][NGL]
-  double *s_ec = SB + C::B_EC;     // [4][EFC]
+  double *s_fi = S + C::O_W;       // FPRE: [4][NQ][8] face-quad traces, own side | ghost side (A2 -> B)
+  double *SI = S + C::O_BIN;       // B inputs
+  double *SB = S + C::O_B;         // term buffers / partials
+  double *s_qp = SI + C::B_QP;     // [P][3] qprime of the bottom layer
+  double *s_ef = SI + C::B_EF;     // [4][FBLK]
+  double *s_tr = SI + C::B_TR;     // [4][8][NGL]
+  double *s_ec = SI + C::B_EC;     // [4][EFC]
+  constexpr bool LATE = C::LATE;
 
   // ------------------------------------------------------------- A: async loads
   if (a.prof && tid == 0) s_prof[30] = wall_clock64();
@@ -287,6 +312,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     if (tid == 0) s_prof[20] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
   }
   STAGE_MARK(0);
+  if (a.prof && tid == 0) s_prof[22] = 0;
   const bool use_q0 = !a.rhs_only && a.a1 != 0.0, use_q2 = !a.rhs_only && a.a3 != 0.0;
   {
     int rot = 0;
@@ -303,9 +329,12 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       if (use_q2) glds_copy<BS>(a.qb2 + (size_t)e * 4 * P, s_q2, 8 * P, tid, rot);
       glds_copy<BS>(a.trace_in + (size_t)e * 32 * NGL, s_tr, 2 * 32 * NGL, tid, rot);
     }
-    if (m.botfr) glds_copy<BS>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
-    glds_copy<BS>(m.efstat + (size_t)e * 4 * C::FBLK, s_ef, 2 * 4 * C::FBLK, tid, rot);
-    glds_copy<BS>(a.efcoef + (size_t)e * 4 * C::EFC, s_ec, 2 * 4 * C::EFC, tid, rot);
+    // qprime, the face statics and the face coefficients are constant over a sub-cycle
+    if (!PERSIST || first || !C::RES) {
+      if (m.botfr) glds_copy<BS>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
+      glds_copy<BS>(m.efstat + (size_t)e * 4 * C::FBLK, s_ef, 2 * 4 * C::FBLK, tid, rot);
+      glds_copy<BS>(a.efcoef + (size_t)e * 4 * C::EFC, s_ec, 2 * 4 * C::EFC, tid, rot);
+    }
   }
   if constexpr (PERSIST) {
     // the element's state stays in LDS from stage to stage: the previous stage's result
@@ -334,7 +363,10 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
 #pragma unroll
     for (int k = 0; k < 4; k++) pre[NST + k] = eco[k * Q];
   }
-  __syncthreads();
+  if (!PERSIST || first || !C::RES)
+    __syncthreads();  // the async LDS copies have landed
+  else
+    LDS_BARRIER();    // LDS-only hand-off: the previous stage's trace stores stay in flight
   STAGE_MARK(21);
 
   if (tid == 0) S[C::O_BASIS + C::NB] = 0.0;  // zero slot of the dpsi table (nz_coef)
@@ -351,17 +383,59 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   constexpr bool GR1 = 32 * NGL <= BS;  // at most one granule per thread
   granule_u4 gx = {0u, 0u, 0u, 0u};
   bool gwant = false;
-  if constexpr (PERSIST && GR1) {
-    if (tid < 32 * NGL) {
-      gwant = s_bc[tid / (8 * NGL)] > 0;  // interior face: a neighbour writes this slot
-      if (gwant) gx = ld_granule_issue(a.gtr_in + (size_t)e * 32 * NGL + tid);
+  // issue this thread's granule load (GR1) now; poll_traces checks it and polls again while
+  // it is older than this stage
+  auto issue_granule = [&]() {
+    if constexpr (PERSIST && GR1) {
+      if (tid < 32 * NGL) {
+        gwant = s_bc[tid / (8 * NGL)] > 0;  // interior face: a neighbour writes this slot
+        if (gwant) {
+          // a compiler-tracked sc1 (L1-bypassing, L2-served) 16-byte load: it may stay in
+          // flight across phases, and the compiler waits for it where gx is first used
+          const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+              (void *)(a.gtr_in + (size_t)e * 32 * NGL), 0, 32 * NGL * (int)sizeof(TraceGranule), 0x00020000);
+          gx = __builtin_amdgcn_raw_buffer_load_b128(r, tid * (int)sizeof(TraceGranule), 0, 16 /* sc1 */);
+        }
+      }
     }
-  }
+  };
+  auto poll_traces = [&]() {
+    if constexpr (PERSIST) {
+      const unsigned long long want = (ep << 20) | a.tag_in;
+      const unsigned long long c0 = a.prof ? clock64() : 0;
+      for (int t = tid; t < 32 * NGL; t += BS) {
+        bool w_ = GR1 ? gwant : s_bc[t / (8 * NGL)] > 0;
+        if (!w_) continue;
+        const TraceGranule *g = a.gtr_in + (size_t)e * 32 * NGL + t;
+        double v;
+        unsigned long long tag;
+        if (GR1) {
+          v = __builtin_bit_cast(double, ((unsigned long long)gx[1] << 32) | gx[0]);
+          tag = ((unsigned long long)gx[3] << 32) | gx[2];
+        } else {
+          ld_granule(g, v, tag);
+        }
+        unsigned spins = 0;
+        while (tag != want && !(a.dbg & 16)) {
+          __builtin_amdgcn_s_sleep(1);
+          ld_granule(g, v, tag);
+          if (++spins > (1u << 20)) {  // never expected: report instead of hanging the GPU
+            atomicOr(a.err, 8);
+            break;
+          }
+        }
+        s_tr[t] = v;
+      }
+      if (a.prof) atomicMax(&s_prof[22], clock64() - c0);  // longest trace wait of the stage
+    }
+  };
+  if constexpr (!LATE) issue_granule();
   {
     const int ng = m.botfr ? 3 : 2;
     constexpr int TPG = SF ? NQ * NGL : Q;  // tasks per group
     const int nint = ng * TPG;
-    for (int w = tid; w < nint + 8 * NGL + P; w += BS) {
+    constexpr int NFP = C::FPRE ? 8 * NQ : 0;  // face-quad pre-interpolation tasks (own | ghost side)
+    for (int w = tid; w < nint + 8 * NGL + P + NFP; w += BS) {
       asm volatile("" ::: "memory");
       if (w < nint) {
         const int g = w / TPG, r = w % TPG;
@@ -435,46 +509,166 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       } else if (w < nint + 8 * NGL) {
         const int t = w - nint, lf = t / (2 * NGL), c = (t / NGL) & 1, n = t % NGL;
         s_wn[t] = s_ef[lf * C::FBLK + EF_N * NQ + (c ? EFN_NY : EFN_NX) * NGL + n];
-      } else {
+      } else if (w < nint + 8 * NGL + P) {
         const int p = w - nint - 8 * NGL;
         s_u[p] = s_qb[p * 4 + 2] / s_qb[p * 4];
         s_v[p] = s_qb[p * 4 + 3] / s_qb[p * 4];
-      }
-    }
-  }
-  if constexpr (PERSIST) {
-    const unsigned long long want = (ep << 20) | a.tag_in;
-    // resolve the granule issued before the interpolation; poll again while it is older
-    for (int t = tid; t < 32 * NGL; t += BS) {
-      bool w_ = GR1 ? gwant : s_bc[t / (8 * NGL)] > 0;
-      if (!w_) continue;
-      const TraceGranule *g = a.gtr_in + (size_t)e * 32 * NGL + t;
-      double v;
-      unsigned long long tag;
-      if (GR1) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        v = __builtin_bit_cast(double, ((unsigned long long)gx[1] << 32) | gx[0]);
-        tag = ((unsigned long long)gx[3] << 32) | gx[2];
-      } else {
-        ld_granule(g, v, tag);
-      }
-      unsigned spins = 0;
-      while (tag != want && !(a.dbg & 16)) {
-        __builtin_amdgcn_s_sleep(1);
-        ld_granule(g, v, tag);
-        if (++spins > (1u << 20)) {  // never expected: report instead of hanging the GPU
-          atomicOr(a.err, 8);
-          break;
+      } else if constexpr (C::FPRE) {
+        // face lf, quad iq: own-side traces (part 0), or on a physical boundary the ghost state
+        // of btp_extract_df (mod_barotropic_terms.F90:75-91) (part 1), interpolated in the
+        // reference's node order (creat_btp_fluxes_qdf, mod_rhs_btp.F90:246-259)
+        const int t = w - nint - 8 * NGL - P, part = t / (4 * NQ), lf = (t / NQ) & 3, iq = t % NQ;
+        const int er = s_bc[lf];
+        if (part == 0 || er <= 0) {
+          const double *efn = s_ef + lf * C::FBLK + EF_N * NQ;
+          double x[4][NGL], hv[NGL];
+#pragma unroll
+          for (int n = 0; n < NGL; n++) {
+            hv[n] = s_psiq[n * NQ + iq];
+            const int p = s_map[lf * NGL + n];
+#pragma unroll
+            for (int c = 0; c < 4; c++) x[c][n] = s_qb[p * 4 + c];
+            if (part == 1) {
+              if (er == -4) {
+                const double nxn = efn[EFN_NX * NGL + n], nyn = efn[EFN_NY * NGL + n];
+                const double un = nxn * x[2][n] + nyn * x[3][n];
+                x[2][n] = x[2][n] - 2.0 * un * nxn;
+                x[3][n] = x[3][n] - 2.0 * un * nyn;
+              } else if (er == -2) {
+                x[2][n] = -x[2][n];
+                x[3][n] = -x[3][n];
+              }
+            }
+          }
+          double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int n = 0; n < NGL; n++)
+#pragma unroll
+            for (int c = 0; c < 4; c++) acc[c] = acc[c] + hv[n] * x[c][n];
+#pragma unroll
+          for (int c = 0; c < 4; c++) s_fi[(lf * NQ + iq) * 8 + 4 * part + c] = acc[c];
         }
       }
-      s_tr[t] = v;
     }
   }
+  if constexpr (!LATE) poll_traces();  // (the granule was issued before the interpolation)
   LDS_BARRIER();
   STAGE_MARK(1);
 
+  // ---- creat_btp_fluxes_qdf at (face lf, quad iq) (mod_rhs_btp.F90:246-337); t = lf*NQ + iq
+  auto face_task = [&](int t) {
+    const int lf = t / NQ, iq = t % NQ;
+    const int side = s_side[lf], er = s_bc[lf];
+    const bool keep = a.accumulate && s_acc[lf];
+    const double *ef = s_ef + lf * C::FBLK, *efn = ef + EF_N * NQ;
+    const double *ec = s_ec + lf * C::EFC;
+    const double *tr = s_tr + lf * 8 * NGL;
+    double ql[4] = {0, 0, 0, 0}, qr[4] = {0, 0, 0, 0};
+    const double pbl = ef[EF_PBLQ * NQ + iq], pbr = ef[EF_PBRQ * NQ + iq];
+    if constexpr (C::FPRE) {
+      // own side and ghost side interpolated in A2; the neighbour side here
+      const double *fi = s_fi + (lf * NQ + iq) * 8;
+      double fo[4], fr[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) fo[c] = fi[c];
+      if (er > 0) {
+        double tv[4][NGL], hv[NGL];
+#pragma unroll
+        for (int n = 0; n < NGL; n++) {
+          hv[n] = s_psiq[n * NQ + iq];
+#pragma unroll
+          for (int c = 0; c < 4; c++) tv[c][n] = tr[c * NGL + n];
+        }
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int c = 0; c < 4; c++) fr[c] = 0.0;
+#pragma unroll
+        for (int n = 0; n < NGL; n++)
+#pragma unroll
+          for (int c = 0; c < 4; c++) fr[c] = fr[c] + hv[n] * tv[c][n];
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; c++) fr[c] = fi[4 + c];
+      }
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        ql[c] = side == 0 ? fo[c] : fr[c];
+        qr[c] = side == 0 ? fr[c] : fo[c];
+      }
+    } else {
+#pragma unroll
+    for (int n = 0; n < NGL; n++) {
+      const double hi = s_psiq[n * NQ + iq];
+      const int p = s_map[lf * NGL + n];
+      double own[4] = {s_qb[p * 4], s_qb[p * 4 + 1], s_qb[p * 4 + 2], s_qb[p * 4 + 3]};
+      double oth[4];
+      if (er > 0) {
+#pragma unroll
+        for (int c = 0; c < 4; c++) oth[c] = tr[c * NGL + n];
+      } else {
+        // ghost state of btp_extract_df (mod_barotropic_terms.F90:75-91)
+#pragma unroll
+        for (int c = 0; c < 4; c++) oth[c] = own[c];
+        if (er == -4) {
+          const double nxn = efn[EFN_NX * NGL + n], nyn = efn[EFN_NY * NGL + n];
+          const double un = nxn * own[2] + nyn * own[3];
+          oth[2] = own[2] - 2.0 * un * nxn;
+          oth[3] = own[3] - 2.0 * un * nyn;
+        } else if (er == -2) {
+          oth[2] = -own[2];
+          oth[3] = -own[3];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const double l = side == 0 ? own[c] : oth[c], r = side == 0 ? oth[c] : own[c];
+        ql[c] = ql[c] + hi * l;
+        qr[c] = qr[c] + hi * r;
+      }
+    }
+    }
+    const double nxl = ef[EF_NX * NQ + iq], nyl = ef[EF_NY * NQ + iq];
+    const double nxr = -nxl, nyr = -nyl;
+    const double pU_L = nxl * ql[2] + nyl * ql[3];
+    const double pU_R = nxr * qr[2] + nyr * qr[3];
+    const double pbpert_edge =
+        ef[EF_CL * NQ + iq] * ql[1] + ef[EF_CR * NQ + iq] * qr[1] + ef[EF_CLR * NQ + iq] * (pU_L + pU_R);
+    const double ope_e = 1.0 + pbpert_edge * ef[EF_OOPE * NQ + iq];
+    const double cml = ef[EF_CML * NQ + iq], cmr = ef[EF_CMR * NQ + iq], cmlr = ef[EF_CMLR * NQ + iq];
+    const double fex = cml * ql[2] + cmr * qr[2] + cmlr * (nxl * ql[1] + nxr * qr[1]);
+    const double fey = cml * ql[3] + cmr * qr[3] + cmlr * (nyl * ql[1] + nyr * qr[1]);
+    const double ul = ql[2] / ql[0], ur = qr[2] / qr[0], vl = ql[3] / ql[0], vr = qr[3] / qr[0];
+    const double quu = 0.5 * (ul * ql[2] + ur * qr[2]) + ope_e * ec[FC_QUU * NQ + iq];
+    const double quv = 0.5 * (vl * ql[2] + vr * qr[2]) + ope_e * ec[FC_QUV * NQ + iq];
+    const double qvu = 0.5 * (ul * ql[3] + ur * qr[3]) + ope_e * ec[FC_QUV * NQ + iq];
+    const double qvv = 0.5 * (vl * ql[3] + vr * qr[3]) + ope_e * ec[FC_QVV * NQ + iq];
+    const double Hf = (ope_e * ope_e) * ec[FC_HBCL * NQ + iq];
+    if (keep) {  // face time averages, kept by one element per face
+      const double opl = 1.0 + (ql[1] / pbl), opr = 1.0 + (qr[1] / pbr);
+      double add[FA_N];
+      add[FA_MFX] = fex; add[FA_MFY] = fey; add[FA_H] = Hf; add[FA_QUU] = quu; add[FA_QUV] = quv;
+      add[FA_QVU] = qvu; add[FA_QVV] = qvv; add[FA_OPEL] = opl; add[FA_OPER] = opr;
+      add[FA_OPE2L] = opl * opl; add[FA_OPE2R] = opr * opr; add[FA_OPEE2] = ope_e * ope_e;
+      add[FA_UL] = ul; add[FA_UR] = ur; add[FA_VL] = vl; add[FA_VR] = vr;
+#pragma unroll
+      for (int k = 0; k < FA_N; k++) atomicAdd(&a.facc[FACC_I(k, e * 4 + lf, iq)], add[k]);
+    }
+    const double H_kx = nxl * Hf, H_ky = nyl * Hf;
+    const double lamb = cmlr;
+    const double dispu = 0.5 * lamb * (qr[2] - ql[2]);
+    const double dispv = 0.5 * lamb * (qr[3] - ql[3]);
+    const double flux_x = nxl * quu + nyl * quv - dispu;
+    const double flux_y = nxl * qvu + nyl * qvv - dispv;
+    const double flux = nxl * fex + nyl * fey;
+    double *fq = s_fq + (lf * NQ + iq) * 4;
+    fq[0] = ef[EF_W * NQ + iq];
+    fq[1] = flux;
+    fq[2] = H_kx + flux_x;
+    fq[3] = H_ky + flux_y;
+  };
+
   // ------------------------------------------------------------- B
-  for (int w = tid; w < C::OL; w += BS) {
+  for (int w = tid; w < C::BEND; w += BS) {
     asm volatile("" ::: "memory");
     if (w < Q) {
       // ---- quad-point physics (mod_rhs_btp.F90:136-192)
@@ -569,87 +763,9 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         s_qv[5 * Q + q] = sc_y;
         s_qv[6 * Q + q] = Hq + qv;
       }
-    } else if (w >= C::OF && w < C::OF + 4 * NQ) {
-      // ---- creat_btp_fluxes_qdf at (face lf, quad iq) (mod_rhs_btp.F90:246-337)
-      const int t = w - C::OF, lf = t / NQ, iq = t % NQ;
-      const int side = s_side[lf], er = s_bc[lf];
-      const bool keep = a.accumulate && s_acc[lf];
-      const double *ef = s_ef + lf * C::FBLK, *efn = ef + EF_N * NQ;
-      const double *ec = s_ec + lf * C::EFC;
-      const double *tr = s_tr + lf * 8 * NGL;
-      double ql[4] = {0, 0, 0, 0}, qr[4] = {0, 0, 0, 0}, pbl = 0.0, pbr = 0.0;
-#pragma unroll
-      for (int n = 0; n < NGL; n++) {
-        const double hi = s_psiq[n * NQ + iq];
-        const int p = s_map[lf * NGL + n];
-        double own[4] = {s_qb[p * 4], s_qb[p * 4 + 1], s_qb[p * 4 + 2], s_qb[p * 4 + 3]};
-        double oth[4];
-        if (er > 0) {
-#pragma unroll
-          for (int c = 0; c < 4; c++) oth[c] = tr[c * NGL + n];
-        } else {
-          // ghost state of btp_extract_df (mod_barotropic_terms.F90:75-91)
-#pragma unroll
-          for (int c = 0; c < 4; c++) oth[c] = own[c];
-          if (er == -4) {
-            const double nxn = efn[EFN_NX * NGL + n], nyn = efn[EFN_NY * NGL + n];
-            const double un = nxn * own[2] + nyn * own[3];
-            oth[2] = own[2] - 2.0 * un * nxn;
-            oth[3] = own[3] - 2.0 * un * nyn;
-          } else if (er == -2) {
-            oth[2] = -own[2];
-            oth[3] = -own[3];
-          }
-        }
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-          const double l = side == 0 ? own[c] : oth[c], r = side == 0 ? oth[c] : own[c];
-          ql[c] = ql[c] + hi * l;
-          qr[c] = qr[c] + hi * r;
-        }
-        pbl = pbl + hi * efn[EFN_PBL * NGL + n];
-        pbr = pbr + hi * efn[EFN_PBR * NGL + n];
-      }
-      const double nxl = ef[EF_NX * NQ + iq], nyl = ef[EF_NY * NQ + iq];
-      const double nxr = -nxl, nyr = -nyl;
-      const double pU_L = nxl * ql[2] + nyl * ql[3];
-      const double pU_R = nxr * qr[2] + nyr * qr[3];
-      const double pbpert_edge =
-          ef[EF_CL * NQ + iq] * ql[1] + ef[EF_CR * NQ + iq] * qr[1] + ef[EF_CLR * NQ + iq] * (pU_L + pU_R);
-      const double ope_e = 1.0 + pbpert_edge * ef[EF_OOPE * NQ + iq];
-      const double cml = ef[EF_CML * NQ + iq], cmr = ef[EF_CMR * NQ + iq], cmlr = ef[EF_CMLR * NQ + iq];
-      const double fex = cml * ql[2] + cmr * qr[2] + cmlr * (nxl * ql[1] + nxr * qr[1]);
-      const double fey = cml * ql[3] + cmr * qr[3] + cmlr * (nyl * ql[1] + nyr * qr[1]);
-      const double ul = ql[2] / ql[0], ur = qr[2] / qr[0], vl = ql[3] / ql[0], vr = qr[3] / qr[0];
-      const double quu = 0.5 * (ul * ql[2] + ur * qr[2]) + ope_e * ec[FC_QUU * NQ + iq];
-      const double quv = 0.5 * (vl * ql[2] + vr * qr[2]) + ope_e * ec[FC_QUV * NQ + iq];
-      const double qvu = 0.5 * (ul * ql[3] + ur * qr[3]) + ope_e * ec[FC_QUV * NQ + iq];
-      const double qvv = 0.5 * (vl * ql[3] + vr * qr[3]) + ope_e * ec[FC_QVV * NQ + iq];
-      const double Hf = (ope_e * ope_e) * ec[FC_HBCL * NQ + iq];
-      if (keep) {  // face time averages, kept by one element per face
-        const double opl = 1.0 + (ql[1] / pbl), opr = 1.0 + (qr[1] / pbr);
-        double add[FA_N];
-        add[FA_MFX] = fex; add[FA_MFY] = fey; add[FA_H] = Hf; add[FA_QUU] = quu; add[FA_QUV] = quv;
-        add[FA_QVU] = qvu; add[FA_QVV] = qvv; add[FA_OPEL] = opl; add[FA_OPER] = opr;
-        add[FA_OPE2L] = opl * opl; add[FA_OPE2R] = opr * opr; add[FA_OPEE2] = ope_e * ope_e;
-        add[FA_UL] = ul; add[FA_UR] = ur; add[FA_VL] = vl; add[FA_VR] = vr;
-#pragma unroll
-        for (int k = 0; k < FA_N; k++) atomicAdd(&a.facc[FACC_I(k, e * 4 + lf, iq)], add[k]);
-      }
-      const double H_kx = nxl * Hf, H_ky = nyl * Hf;
-      const double lamb = cmlr;
-      const double dispu = 0.5 * lamb * (qr[2] - ql[2]);
-      const double dispv = 0.5 * lamb * (qr[3] - ql[3]);
-      const double flux_x = nxl * quu + nyl * quv - dispu;
-      const double flux_y = nxl * qvu + nyl * qvv - dispv;
-      const double flux = nxl * fex + nyl * fey;
-      double *fq = s_fq + (lf * NQ + iq) * 4;
-      fq[0] = ef[EF_W * NQ + iq];
-      fq[1] = flux;
-      fq[2] = H_kx + flux_x;
-      fq[3] = H_ky + flux_y;
+    } else if (!LATE && w >= C::OF && w < C::OF + 4 * NQ) {
+      face_task(w - C::OF);
     } else if (w >= C::OG && w < C::OL) {
-      // ---- nodal grad(u_bar) (compute_gradient_uv) + stage-start nodal averages
       const int p = w - C::OG, i = p % NGL, j = p / NGL;
       double g[4];
       nodal_grad4<NGL>(s_dpsi, i, j, s_ns[NE_EX * P + p], s_ns[NE_EY * P + p], s_ns[NE_NX * P + p],
@@ -659,7 +775,6 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       if (a.accumulate) {
 #pragma unroll
         for (int c = 0; c < 4; c++) atomicAdd(&a.nacc[NACC_I(NA_G1 + c, e, p)], g[c]);
-        // mod_rk_mlswe.F90:90-92
         const double t1 = 1.0 + s_qb[p * 4 + 1] * s_ns[NE_OOP * P + p];
         atomicAdd(&a.nacc[NACC_I(NA_OPE2, e, p)], t1 * t1);
         atomicAdd(&a.nacc[NACC_I(NA_UB, e, p)], s_u[p]);
@@ -933,21 +1048,29 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       for (int v = 0; v < 3; v++) s_rhs[v * P + p] = acc[v];
     };
     // lanes: terms from 0, the sums on the last wave when they fit beside the terms, qq
-    // after the terms (D0), the LDG fluxes on their preload threads (D0), the Laplacian
-    // from 0 in the last phase (no terms there)
-    constexpr int WTMAX = QC * NGL;
+    // after the terms (D0), the Laplacian from 0 in the last phase (no terms there).  Face
+    // fluxes and LDG face fluxes: LATE, in chunk phase KP+1 past the terms (the persistent
+    // kernel polls the neighbour traces in phase KP); otherwise the face fluxes ran in B and
+    // the LDG fluxes run in D0
+    constexpr int WTMAX = C::WTMAX;
     constexpr int OSUM = (P <= 64 && WTMAX <= BS - 64) ? BS - 64 : WTMAX;
 #pragma unroll
     for (int k = 0; k <= NCH; k++) {
       asm volatile("" ::: "memory");  // keep LDS reads inside their phase (no hoisting)
       const int WT = (k < NCH) ? ((k == NCH - 1) ? (Q - k * QC) : QC) * NGL : 0;  // term tasks
+      if (LATE && k == C::KP) issue_granule();
       for_tasks<BS>(tid, 0, WT, [&](int t, bool) { term_task(k, t); });
       if (k >= 1 && !((a.dbg & 4) && k == NCH)) for_tasks<BS>(tid, OSUM, P, [&](int t, bool) { sum_task(k - 1, t); });
       if (k == 0) {
         for_tasks<BS>(tid, WT, P, [&](int t, bool) { qq_task(t); });
-        for_tasks<BS>(tid, C::OL, 4 * NGL, ldg_task);
+        if (!LATE) for_tasks<BS>(tid, C::OL, 4 * NGL, ldg_task);
+      }
+      if (LATE && k == C::KP + 1) {
+        for_tasks<BS>(tid, C::OFD, 4 * NQ, [&](int t, bool) { face_task(t); });
+        for_tasks<BS>(tid, C::OLD, 4 * NGL, ldg_task);
       }
       if (k == NCH && !(a.dbg & 2)) for_tasks<BS>(tid, 0, 2 * P, [&](int t, bool) { lap_task(t / P, t % P); });
+      if (LATE && k == C::KP) poll_traces();
       LDS_BARRIER();
       if (k < 6) STAGE_MARK(6 + k);
     }
@@ -1036,7 +1159,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     STAGE_MARK(5);
     if (tid == 0) {
       if (PERSIST) {  // sums over the stages: A incl. the trace waits | the rest | stages
-        if (first) s_prof[24] = s_prof[25] = s_prof[26] = 0;
+        if (first) s_prof[24] = s_prof[25] = s_prof[26] = s_prof[27] = 0;
+        s_prof[27] += s_prof[22];
         s_prof[24] += s_prof[21] - s_prof[0];
         s_prof[25] += s_prof[5] - s_prof[21];
         s_prof[26] += 1;

@@ -14,7 +14,8 @@ import numpy as np
 from . import bundle as _bundle
 from .abi import Descriptors, Halo, HaloDesc
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libhnumo_engine.so")
+LIB_PATH = os.environ.get("HNUMO_LIB") or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                    "libhnumo_engine.so")  # HNUMO_LIB: A/B experiments only
 _lib = None
 
 ERRORS = {1: "negative layer thickness", 2: "non-finite value", 3: "HIP/RCCL error", 4: "invalid argument"}

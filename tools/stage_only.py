@@ -12,5 +12,8 @@ case = build_case(make_config(cfg), dense=False)
 eng = Engine(case)
 eng.set_resident(True)
 q, qb, qp = eng.state()
-eng.ti_rk_bcl(q, qb, qp)
+try:
+    eng.ti_rk_bcl(q, qb, qp)
+except Exception as ex:  # HNUMO_STAGE_DBG timing experiments break the physics
+    print("warm-up step:", ex)
 print(f"{cfg}: stage avg {eng.time_stage_kernel(n) * 1e3:.2f} us")

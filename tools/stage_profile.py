@@ -52,10 +52,15 @@ print(f"  distinct CUs used {len(u)}, blocks per CU: {np.bincount(c).tolist()}")
 
 if pr[:, 26].max() > 0:
     nst = pr[:, 26].astype(float)
-    aw, wk = pr[:, 24] / nst, pr[:, 25] / nst
+    aw, wk, wt = pr[:, 24] / nst, pr[:, 25] / nst, pr[:, 27] / nst
+    print(f"  trace wait per stage (longest thread): mean {wt.mean():.0f} clk, p10 {np.percentile(wt, 10):.0f}, "
+          f"p90 {np.percentile(wt, 90):.0f}; work without it: mean {(wk - wt).mean():.0f}, max {(wk - wt).max():.0f}")
+    for x in range(8):
+        sel = xcc == x
+        print(f"    xcc {x}: work-wait mean {(wk - wt)[sel].mean():.0f}, wait {wt[sel].mean():.0f}")
     bpc = c[np.searchsorted(u, key)]
     print(f"  persistent: per stage A(+waits) mean {aw.mean():.0f} clk, work mean {wk.mean():.0f} clk")
     for k in sorted(set(bpc.tolist())):
         sel = bpc == k
         print(f"    CUs with {k} blocks: {sel.sum()} blocks, A(+waits) {aw[sel].mean():.0f}, work {wk[sel].mean():.0f} "
-              f"(max {wk[sel].max():.0f}) clk")
+              f"(max {wk[sel].max():.0f}) clk, trace wait {wt[sel].mean():.0f}, work-wait {(wk - wt)[sel].mean():.0f}")
