@@ -330,7 +330,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       glds_copy<BS>(a.trace_in + (size_t)e * 32 * NGL, s_tr, 2 * 32 * NGL, tid, rot);
     }
     // qprime, the face statics and the face coefficients are constant over a sub-cycle
-    if (!PERSIST || first || !C::RES) {
+    // (persistent, not RES: the previous stage re-fetched them in E1, see there)
+    if (!PERSIST || first) {
       if (m.botfr) glds_copy<BS>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
       glds_copy<BS>(m.efstat + (size_t)e * 4 * C::FBLK, s_ef, 2 * 4 * C::FBLK, tid, rot);
       glds_copy<BS>(a.efcoef + (size_t)e * 4 * C::EFC, s_ec, 2 * 4 * C::EFC, tid, rot);
@@ -355,18 +356,27 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   // keeps the reference's summation order.)
   constexpr int NST = QE_N - QE_KEEP, NPRE = NST + 4;
   double pre[NPRE];
-  if (tid < Q) {
-    const double *qse = m.qstatE + (size_t)e * QE_N * Q + tid;
+  auto load_pre = [&]() {
+    if (tid < Q) {
+      const double *qse = m.qstatE + (size_t)e * QE_N * Q + tid;
 #pragma unroll
-    for (int k = 0; k < NST; k++) pre[k] = qse[(QE_KEEP + k) * Q];
-    const double *eco = a.ecoef + (size_t)e * C::ECO + tid;
+      for (int k = 0; k < NST; k++) pre[k] = qse[(QE_KEEP + k) * Q];
+      const double *eco = a.ecoef + (size_t)e * C::ECO + tid;
 #pragma unroll
-    for (int k = 0; k < 4; k++) pre[NST + k] = eco[k * Q];
-  }
-  if (!PERSIST || first || !C::RES)
+      for (int k = 0; k < 4; k++) pre[NST + k] = eco[k * Q];
+    }
+  };
+  if (!PERSIST || first) {
+    load_pre();
     __syncthreads();  // the async LDS copies have landed
-  else
-    LDS_BARRIER();    // LDS-only hand-off: the previous stage's trace stores stay in flight
+  } else {
+    // persistent, later stages: RES: nothing was loaded; otherwise the B inputs re-fetched in
+    // the previous stage's E1 must have landed (this wave's copies; the barrier covers the
+    // others').  The register loads go out after the wait, so it does not cover them.
+    if constexpr (!C::RES) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    LDS_BARRIER();
+    load_pre();
+  }
   STAGE_MARK(21);
 
   if (tid == 0) S[C::O_BASIS + C::NB] = 0.0;  // zero slot of the dpsi table (nz_coef)
@@ -1076,6 +1086,20 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     }
   }
   STAGE_MARK(3);
+
+  // persistent, B inputs not resident: the term buffers are dead now, so the next stage's
+  // bottom-layer qprime, face statics and face coefficients (constant over the sub-cycle,
+  // overlaid by term buffer 1 in D1..D2) are re-fetched here, behind E1/E2, instead of at
+  // the start of the next stage (the traces' slot is not touched: A2 of the next stage
+  // fills it)
+  if constexpr (PERSIST && !C::RES) {
+    if (a.write_trace) {  // a next stage follows
+      int rot = 0;
+      if (m.botfr) glds_copy<BS>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
+      glds_copy<BS>(m.efstat + (size_t)e * 4 * C::FBLK, s_ef, 2 * 4 * C::FBLK, tid, rot);
+      glds_copy<BS>(a.efcoef + (size_t)e * 4 * C::EFC, s_ec, 2 * 4 * C::EFC, tid, rot);
+    }
+  }
 
   // ------------------------------------------------------------- E1: update + wall fix
   for (int p = tid; p < P; p += BS) {
