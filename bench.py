@@ -185,8 +185,9 @@ def main():
         "value": round(value, 1), "unit": "element-updates/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic (analytic double-gyre IC)",
-        "config": {"workload": f"{args.config}: double-gyre 25x25 elements, N=4, 3 layers, "
-                               f"N_btp={case.scalars['N_btp']}, kstages=5",
+        "config": {"workload": f"{args.config}: double-gyre {base_cfg['nelx']}x{base_cfg['nely']} elements per GPU, "
+                               f"N={case.scalars['ngl'] - 1}, {case.scalars['nlayers']} layers, "
+                               f"N_btp={case.scalars['N_btp']}, kstages={case.scalars['kstages']}",
                    "elements": case.scalars["nelem"], "nlayers": case.scalars["nlayers"],
                    "nop": case.scalars["ngl"] - 1, "parallelism": parallelism,
                    "summation": args.summation, "stage_path": path},

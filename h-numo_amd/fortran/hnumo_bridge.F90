@@ -50,7 +50,7 @@ contains
     subroutine hnumo_bridge_init(device, resident)
         use mod_basis, only: ngl, nq, psiq, dpsiq, psi, dpsi
         use mod_grid, only: nelem, npoin, npoin_q, nface, face
-        use mod_face, only: imapl, imapr, normal_vector, normal_vector_q, jac_face, jac_faceq
+        use mod_face, only: imapl, imapr, imapl_q, imapr_q, normal_vector, normal_vector_q, jac_face, jac_faceq
         use mod_metrics, only: massinv, ksiq_x, ksiq_y, etaq_x, etaq_y, jacq, ksi_x, ksi_y, eta_x, eta_y, jac
         use mod_input, only: nlayers, dt, dt_btp, kstages, method_visc, visc_mlswe, botfr, cd_mlswe, ad_mlswe
         use mod_constants, only: gravity
@@ -67,6 +67,7 @@ contains
         type(hnumo_params) :: par
         ! the face arrays carry a dead second face index on this 2-D path: pass (:,:,1,:)
         integer(c_int32_t), allocatable, target :: face8(:, :), imapl1(:, :, :), imapr1(:, :, :)
+        integer(c_int32_t), allocatable, target :: imaplq1(:, :, :), imaprq1(:, :, :)
         real(c_double), allocatable, target :: nv1(:, :, :), nvq1(:, :, :), jf1(:, :), jfq1(:, :)
         integer(c_int) :: rc
 
@@ -74,6 +75,8 @@ contains
         face8 = face(1:8, 1:nface)
         imapl1 = imapl(:, :, 1, :)
         imapr1 = imapr(:, :, 1, :)
+        imaplq1 = imapl_q(:, :, 1, :)
+        imaprq1 = imapr_q(:, :, 1, :)
         nv1 = normal_vector(:, :, 1, :)
         nvq1 = normal_vector_q(:, :, 1, :)
         jf1 = jac_face(:, 1, :)
@@ -82,6 +85,7 @@ contains
         mesh%nelem = nelem; mesh%npoin = npoin; mesh%npoin_q = npoin_q; mesh%nface = nface
         mesh%ngl = ngl; mesh%nq = nq; mesh%nlayers = nlayers
         mesh%face = c_loc(face8); mesh%imapl = c_loc(imapl1); mesh%imapr = c_loc(imapr1)
+        mesh%imapl_q = c_loc(imaplq1); mesh%imapr_q = c_loc(imaprq1)
         mesh%normal_vector = c_loc(nv1); mesh%normal_vector_q = c_loc(nvq1)
         mesh%jac_face = c_loc(jf1); mesh%jac_faceq = c_loc(jfq1)
         mesh%massinv = pd(massinv)

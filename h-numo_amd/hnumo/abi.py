@@ -21,6 +21,7 @@ class MeshDesc(C.Structure):
         ("ksi_x", _dp), ("ksi_y", _dp), ("eta_x", _dp), ("eta_y", _dp), ("jac", _dp),
         ("psih", _dp), ("dpsidx", _dp), ("dpsidy", _dp), ("wjac", _dp), ("indexq", _ip),
         ("dpsidx_df", _dp), ("dpsidy_df", _dp), ("wjac_df", _dp), ("index_df", _ip),
+        ("imapl_q", _ip), ("imapr_q", _ip),
     ]
 
 
@@ -103,7 +104,7 @@ class Descriptors:
     def __init__(self, case, dense: bool = False):
         A, S = case.arrays, case.scalars
         self.keep = {}
-        for k in ("face", "imapl", "imapr"):
+        for k in ("face", "imapl", "imapr", "imapl_q", "imapr_q"):
             self.keep[k] = _f(A[k], np.int32)
         for k in self.MESH_F8:
             self.keep[k] = _f(A[k], np.float64)
@@ -117,7 +118,7 @@ class Descriptors:
         m = MeshDesc()
         for k in ("nelem", "npoin", "npoin_q", "nface", "ngl", "nq", "nlayers"):
             setattr(m, k, S[k])
-        for k in ["face", "imapl", "imapr"] + self.MESH_F8:
+        for k in ["face", "imapl", "imapr", "imapl_q", "imapr_q"] + self.MESH_F8:
             setattr(m, k, ptr(self.keep[k]))
         if dense:
             for k in self.DENSE_F8 + self.DENSE_I4:

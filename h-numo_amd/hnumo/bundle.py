@@ -11,6 +11,7 @@ import numpy as np
 # (name, dtype, shape in terms of the header dims)
 BUNDLE_ARRAYS = [
     ("face", "i4", "8,nface"), ("imapl", "i4", "3,ngl,nface"), ("imapr", "i4", "3,ngl,nface"),
+    ("imapl_q", "i4", "3,nq,nface"), ("imapr_q", "i4", "3,nq,nface"),
     ("indexq", "i4", "npts,npoin_q"), ("index_df", "i4", "npts,npoin"),
     ("normal_vector", "f8", "3,ngl,nface"), ("normal_vector_q", "f8", "3,nq,nface"),
     ("jac_face", "f8", "ngl,nface"), ("jac_faceq", "f8", "nq,nface"), ("massinv", "f8", "npoin"),

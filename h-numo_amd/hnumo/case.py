@@ -58,6 +58,13 @@ CONFIGS = {
     "dg25N7L3": dict(test_case="double-gyre-3", nelx=25, nely=25, nop=7, nlayers=3,
                      xdims=(0.0, 2.0e6), ydims=(0.0, 2.0e6), dt=180.0, dt_btp=9.0,
                      method_visc=3, visc=50.0, botfr=1, cd=1.0e-7, f0=0.93e-4, beta=2.0e-11),
+    # method_visc == 1 (quad-point LDG viscosity): not in a shipped namelist
+    "bump10q": dict(test_case="bump", nelx=10, nely=10, nop=4, nlayers=2,
+                    xdims=(0.0, 2000.0), ydims=(0.0, 2000.0), dt=100.0, dt_btp=1.8,
+                    method_visc=1, visc=25.0, botfr=0, cd=0.0, f0=0.0, beta=0.0),
+    "dg8L3q": dict(test_case="double-gyre-3", nelx=8, nely=8, nop=4, nlayers=3,
+                   xdims=(0.0, 2.0e6), ydims=(0.0, 2.0e6), dt=500.0, dt_btp=25.0,
+                   method_visc=1, visc=50.0, botfr=1, cd=1.0e-7, f0=0.93e-4, beta=2.0e-11),
     # C4: ~1e5 elements, dt scaled for CFL
     "dg316L3": dict(test_case="double-gyre-3", nelx=316, nely=316, nop=4, nlayers=3,
                     xdims=(0.0, 2.0e6), ydims=(0.0, 2.0e6), dt=40.0, dt_btp=2.0,
@@ -172,7 +179,8 @@ def build_case(cfg: dict, dense: bool = True) -> Case:
     A["massinv"] = 1.0 / A["jac"].reshape(-1, order="F")
 
     # ---------------- mesh arrays
-    for k in ("face", "imapl", "imapr", "normal_vector", "normal_vector_q", "jac_face", "jac_faceq"):
+    for k in ("face", "imapl", "imapr", "imapl_q", "imapr_q", "normal_vector", "normal_vector_q", "jac_face",
+              "jac_faceq"):
         A[k] = getattr(mesh, k)
     A["psiq"] = np.asfortranarray(basis.psiq)
     A["dpsiq"] = np.asfortranarray(basis.dpsiq)

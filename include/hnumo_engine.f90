@@ -15,7 +15,7 @@ module hnumo_engine_c
 
     integer(c_int), parameter, public :: HNUMO_OK = 0, HNUMO_ERR_NEGATIVE_THICKNESS = 1, &
         HNUMO_ERR_NONFINITE = 2, HNUMO_ERR_DEVICE = 3, HNUMO_ERR_INVALID = 4
-    integer(c_int), parameter, public :: HNUMO_ABI_EXPECTED = 2   ! must equal hnumo_abi_version()
+    integer(c_int), parameter, public :: HNUMO_ABI_EXPECTED = 3   ! must equal hnumo_abi_version()
     integer(c_int), parameter, public :: HNUMO_SUM_REFERENCE = 0, HNUMO_SUM_FACTORED = 1
 
     ! = hnumo_mesh_desc (mod_grid, mod_face, mod_basis, mod_metrics; optional dense tables)
@@ -39,6 +39,7 @@ module hnumo_engine_c
         type(c_ptr) :: indexq = c_null_ptr
         type(c_ptr) :: dpsidx_df = c_null_ptr, dpsidy_df = c_null_ptr, wjac_df = c_null_ptr
         type(c_ptr) :: index_df = c_null_ptr
+        type(c_ptr) :: imapl_q = c_null_ptr, imapr_q = c_null_ptr ! (3,nq,nface), method_visc == 1
     end type hnumo_mesh_desc
 
     ! = hnumo_static_desc (mod_initial.F90:42-53)

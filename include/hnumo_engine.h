@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define HNUMO_ABI_VERSION 2
+#define HNUMO_ABI_VERSION 3
 
 enum {
   HNUMO_OK = 0,
@@ -81,6 +81,10 @@ typedef struct hnumo_mesh_desc {
   const int32_t *indexq;                              /* (npts,npoin_q)                 */
   const double *dpsidx_df, *dpsidy_df, *wjac_df;      /* (npts,npoin), wjac_df (npoin)  */
   const int32_t *index_df;                            /* (npts,npoin)                   */
+  /* face quad point -> element quad point maps, (3,nq,nface) = imapl_q(:,:,1,:)
+   * (mod_face, create_normals_quad.F90:335-350); read only when method_visc == 1
+   * (quad-point LDG viscosity), NULL allowed otherwise.                              */
+  const int32_t *imapl_q, *imapr_q;
 } hnumo_mesh_desc;
 
 /* Reference state and forcing built at start-up: mod_initial (mod_initial.F90:42-53). */

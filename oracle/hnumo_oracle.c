@@ -17,9 +17,11 @@
  * Each function cites the reference routine it restates.  Arrays use the reference's
  * Fortran layouts; the A*() macros index them 1-based exactly as the Fortran does.
  *
- * Not restated (unsupported, returns HNUMO_ERR_INVALID): method_visc == 1 quad-point
- * LDG (mod_laplacian_quad.F90:125-223,252-355) and ad_mlswe > 0 vertical shear stress
- * (mod_create_rhs_mlswe.F90:146-279) -- SURVEY.md §8f row f1; multi-rank halos (np=1).
+ * method_visc == 1 (quad-point LDG viscosity, mod_laplacian_quad.F90:125-223,252-355) is
+ * restated below.  Not restated (unsupported, returns HNUMO_ERR_INVALID): ad_mlswe > 0
+ * vertical shear stress (mod_create_rhs_mlswe.F90:146-279), whose reference reads two
+ * uninitialised arrays (tau_u(nlayers+1) at :246-247, uv at mod_splitting.F90:158);
+ * multi-rank halos (np=1).
  */
 #include <math.h>
 #include <stdio.h>
@@ -60,6 +62,7 @@ typedef struct oracle {
   double *Qu_face_ave, *Qv_face_ave, *Quv_face_ave;                 /* 2,nq,nface  */
   double *H_face_ave, *one_plus_eta_edge_2_ave;                     /* nq,nface    */
   double *dpprime_visc;                                             /* npoin,L     */
+  double *dpprime_visc_q;                                           /* npoin_q,L   */
   double *pbprime_visc;                                             /* npoin       */
   double *btp_dpp_graduv;                                           /* 4,npoin     */
   double *dpp_graduv;                                               /* 4,npoin,L   */
@@ -410,6 +413,177 @@ static void btp_create_laplacian(oracle *o, double *rhs_lap, const double *qb) {
   free(gf);
 }
 
+/* ---------------------------------------------- method_visc == 1: quad-point LDG */
+
+/* intma_dg_quad (mod_grid.F90:242-250) */
+static inline int INTMA_Q(const oracle *o, int i, int j, int e) { return (e - 1) * o->nq * o->nq + (j - 1) * o->nq + i; }
+
+/* interpolate_dpp (mod_layer_terms.F90:25-55): dprimeq(Iq,:) += dprime_df(I,:)*hi */
+static void interpolate_dpp(oracle *o) {
+  const int npts = o->npts, npoin = o->npoin, npq = o->npoin_q, L = o->L;
+  memset(o->dpprime_visc_q, 0, sizeof(double) * (size_t)npq * L);
+  for (int Iq = 1; Iq <= npq; Iq++)
+    for (int ip = 1; ip <= npts; ip++) {
+      int I = A2(o->m.indexq, ip, Iq, npts);
+      double hi = A2(o->m.psih, ip, Iq, npts);
+      for (int k = 1; k <= L; k++)
+        A2(o->dpprime_visc_q, Iq, k, npq) = A2(o->dpprime_visc_q, Iq, k, npq) + A2(o->dpprime_visc, I, k, npoin) * hi;
+    }
+}
+
+/* compute_gradient_uv_q (mod_barotropic_terms.F90:445-477): grad(2,2,npoin_q) of uv(2,npoin) */
+static void gradient_uv_q(oracle *o, double *grad, const double *uv) {
+  const int npts = o->npts;
+  memset(grad, 0, sizeof(double) * 4 * (size_t)o->npoin_q);
+  for (int Iq = 1; Iq <= o->npoin_q; Iq++)
+    for (int ip = 1; ip <= npts; ip++) {
+      int I = A2(o->m.indexq, ip, Iq, npts);
+      double dhdx = A2(o->m.dpsidx, ip, Iq, npts), dhdy = A2(o->m.dpsidy, ip, Iq, npts);
+      A3(grad, 1, 1, Iq, 2, 2) = A3(grad, 1, 1, Iq, 2, 2) + dhdx * A2(uv, 1, I, 2);
+      A3(grad, 1, 2, Iq, 2, 2) = A3(grad, 1, 2, Iq, 2, 2) + dhdy * A2(uv, 1, I, 2);
+      A3(grad, 2, 1, Iq, 2, 2) = A3(grad, 2, 1, Iq, 2, 2) + dhdx * A2(uv, 2, I, 2);
+      A3(grad, 2, 2, Iq, 2, 2) = A3(grad, 2, 2, Iq, 2, 2) + dhdy * A2(uv, 2, I, 2);
+    }
+}
+
+/* flux_uv_visc(4,npoin_q) -> face values flux_uv_visc_face(4,2,nq,nface) with the wall
+ * reflection (mod_laplacian_quad.F90:156-212 / :296-344, one layer) */
+static void lapq_face_values(oracle *o, double *ff, const double *fl) {
+  const int nq = o->nq, nface = o->nface;
+  const hnumo_mesh_desc *m = &o->m;
+  for (int f = 1; f <= nface; f++) {
+    int iel = A2(m->face, 7, f, 8), ier = A2(m->face, 8, f, 8);
+    for (int iq = 1; iq <= nq; iq++) {
+      int Iq = INTMA_Q(o, A3(m->imapl_q, 1, iq, f, 3, nq), A3(m->imapl_q, 2, iq, f, 3, nq), iel);
+      for (int v = 1; v <= 4; v++) A4(ff, v, 1, iq, f, 4, 2, nq) = A2(fl, v, Iq, 4);
+      if (ier > 0) {
+        int Ir = INTMA_Q(o, A3(m->imapr_q, 1, iq, f, 3, nq), A3(m->imapr_q, 2, iq, f, 3, nq), ier);
+        for (int v = 1; v <= 4; v++) A4(ff, v, 2, iq, f, 4, 2, nq) = A2(fl, v, Ir, 4);
+      } else {
+        for (int v = 1; v <= 4; v++) A4(ff, v, 2, iq, f, 4, 2, nq) = A4(ff, v, 1, iq, f, 4, 2, nq);
+        if (ier == -4) {
+          double nx = A3(m->normal_vector_q, 1, iq, f, 3, nq), ny = A3(m->normal_vector_q, 2, iq, f, 3, nq);
+          double un = A2(fl, 1, Iq, 4) * nx + A2(fl, 2, Iq, 4) * ny;
+          A4(ff, 1, 2, iq, f, 4, 2, nq) = A2(fl, 1, Iq, 4) - 2.0 * un * nx;
+          A4(ff, 2, 2, iq, f, 4, 2, nq) = A2(fl, 2, Iq, 4) - 2.0 * un * ny;
+          un = A2(fl, 3, Iq, 4) * nx + A2(fl, 4, Iq, 4) * ny;
+          A4(ff, 3, 2, iq, f, 4, 2, nq) = A2(fl, 3, Iq, 4) - 2.0 * un * nx;
+          A4(ff, 4, 2, iq, f, 4, 2, nq) = A2(fl, 4, Iq, 4) - 2.0 * un * ny;
+        }
+      }
+    }
+  }
+}
+
+/* compute_laplacian_quad (mod_laplacian_quad.F90:613-642) + create_rhs_laplacian_flux_quad
+ * (:644-722) of one flux field, then visc*massinv (:217-218 / :349-350) into rhs_lap(2,npoin) */
+static void lapq_apply(oracle *o, double *rhs_lap, const double *fl, const double *ff) {
+  const int npts = o->npts, npoin = o->npoin, nq = o->nq, ngl = o->ngl, nface = o->nface;
+  const hnumo_mesh_desc *m = &o->m;
+  memset(rhs_lap, 0, sizeof(double) * 2 * (size_t)npoin);
+  for (int Iq = 1; Iq <= o->npoin_q; Iq++) {
+    double wq = m->wjac[Iq - 1];
+    for (int ip = 1; ip <= npts; ip++) {
+      int I = A2(m->indexq, ip, Iq, npts);
+      double dhdx = A2(m->dpsidx, ip, Iq, npts), dhdy = A2(m->dpsidy, ip, Iq, npts);
+      double u_visc = dhdx * A2(fl, 1, Iq, 4) + dhdy * A2(fl, 2, Iq, 4);
+      double v_visc = dhdx * A2(fl, 3, Iq, 4) + dhdy * A2(fl, 4, Iq, 4);
+      A2(rhs_lap, 1, I, 2) = A2(rhs_lap, 1, I, 2) - wq * u_visc;
+      A2(rhs_lap, 2, I, 2) = A2(rhs_lap, 2, I, 2) - wq * v_visc;
+    }
+  }
+  const double beta = 0.5, alpha = 1.0 - beta;
+  for (int f = 1; f <= nface; f++) {
+    int iel = A2(m->face, 7, f, 8), ier = A2(m->face, 8, f, 8);
+    for (int iq = 1; iq <= nq; iq++) {
+      double qul[2] = {A4(ff, 1, 1, iq, f, 4, 2, nq), A4(ff, 2, 1, iq, f, 4, 2, nq)};
+      double qvl[2] = {A4(ff, 3, 1, iq, f, 4, 2, nq), A4(ff, 4, 1, iq, f, 4, 2, nq)};
+      double qur[2] = {A4(ff, 1, 2, iq, f, 4, 2, nq), A4(ff, 2, 2, iq, f, 4, 2, nq)};
+      double qvr[2] = {A4(ff, 3, 2, iq, f, 4, 2, nq), A4(ff, 4, 2, iq, f, 4, 2, nq)};
+      double qu_mean[2], qv_mean[2];
+      for (int c = 0; c < 2; c++) {
+        qu_mean[c] = alpha * qul[c] + beta * qur[c];
+        qv_mean[c] = alpha * qvl[c] + beta * qvr[c];
+      }
+      double wq = A2(m->jac_faceq, iq, f, nq);
+      double nx = A3(m->normal_vector_q, 1, iq, f, 3, nq), ny = A3(m->normal_vector_q, 2, iq, f, 3, nq);
+      double flux_qu = (qu_mean[0] - qul[0] * nx) + (qu_mean[1] - qul[1] * ny);
+      double flux_qv = (qv_mean[0] - qvl[0] * nx) + (qv_mean[1] - qvl[1] * ny);
+      for (int i = 1; i <= ngl; i++) {
+        double hi = A2(m->psiq, i, iq, ngl);
+        int ip = INTMA(o, A3(m->imapl, 1, i, f, 3, ngl), A3(m->imapl, 2, i, f, 3, ngl), iel);
+        A2(rhs_lap, 1, ip, 2) = A2(rhs_lap, 1, ip, 2) + wq * hi * flux_qu;
+        A2(rhs_lap, 2, ip, 2) = A2(rhs_lap, 2, ip, 2) + wq * hi * flux_qv;
+        if (ier > 0) {
+          ip = INTMA(o, A3(m->imapr, 1, i, f, 3, ngl), A3(m->imapr, 2, i, f, 3, ngl), ier);
+          A2(rhs_lap, 1, ip, 2) = A2(rhs_lap, 1, ip, 2) - wq * hi * flux_qu;
+          A2(rhs_lap, 2, ip, 2) = A2(rhs_lap, 2, ip, 2) - wq * hi * flux_qv;
+        }
+      }
+    }
+  }
+  for (int I = 1; I <= npoin; I++) {
+    A2(rhs_lap, 1, I, 2) = o->p.visc_mlswe * m->massinv[I - 1] * A2(rhs_lap, 1, I, 2);
+    A2(rhs_lap, 2, I, 2) = o->p.visc_mlswe * m->massinv[I - 1] * A2(rhs_lap, 2, I, 2);
+  }
+}
+
+/* btp_create_laplacian_v2 (mod_laplacian_quad.F90:125-223) */
+static void btp_create_laplacian_v2(oracle *o, double *rhs_lap, const double *qp, const double *qb) {
+  const int npoin = o->npoin, npq = o->npoin_q, L = o->L;
+  double *Uk = zalloc(2 * (size_t)npoin), *grad = zalloc(4 * (size_t)npq), *fl = zalloc(4 * (size_t)npq);
+  double *ff = zalloc(8 * (size_t)o->nq * o->nface);
+  for (int k = 1; k <= L; k++) {
+    for (int I = 1; I <= npoin; I++) {
+      A2(Uk, 1, I, 2) = A3(qp, 2, I, k, 3, npoin) + A2(qb, 3, I, 4) / A2(qb, 1, I, 4);
+      A2(Uk, 2, I, 2) = A3(qp, 3, I, k, 3, npoin) + A2(qb, 4, I, 4) / A2(qb, 1, I, 4);
+    }
+    gradient_uv_q(o, grad, Uk);
+    for (int Iq = 1; Iq <= npq; Iq++) {
+      double d = A2(o->dpprime_visc_q, Iq, k, npq);
+      A2(fl, 1, Iq, 4) = A2(fl, 1, Iq, 4) + d * A3(grad, 1, 1, Iq, 2, 2);
+      A2(fl, 2, Iq, 4) = A2(fl, 2, Iq, 4) + d * A3(grad, 1, 2, Iq, 2, 2);
+      A2(fl, 3, Iq, 4) = A2(fl, 3, Iq, 4) + d * A3(grad, 2, 1, Iq, 2, 2);
+      A2(fl, 4, Iq, 4) = A2(fl, 4, Iq, 4) + d * A3(grad, 2, 2, Iq, 2, 2);
+    }
+  }
+  lapq_face_values(o, ff, fl);
+  lapq_apply(o, rhs_lap, fl, ff);
+  free(Uk);
+  free(grad);
+  free(fl);
+  free(ff);
+}
+
+/* bcl_create_laplacian_v2 (mod_laplacian_quad.F90:252-355) into rhs_lap(2,npoin,nlayers) */
+static void bcl_create_laplacian_v2(oracle *o, double *rhs_lap, const double *qp) {
+  const int npoin = o->npoin, npq = o->npoin_q, L = o->L;
+  double *Uk = zalloc(2 * (size_t)npoin), *grad = zalloc(4 * (size_t)npq), *fl = zalloc(4 * (size_t)npq);
+  double *ff = zalloc(8 * (size_t)o->nq * o->nface);
+  for (int k = 1; k <= L; k++) {
+    for (int I = 1; I <= npoin; I++) {
+      A2(Uk, 1, I, 2) = A3(qp, 2, I, k, 3, npoin) + A2(o->uvb_ave_df, 1, I, 2);
+      A2(Uk, 2, I, 2) = A3(qp, 3, I, k, 3, npoin) + A2(o->uvb_ave_df, 2, I, 2);
+    }
+    gradient_uv_q(o, grad, Uk);
+    for (int Iq = 1; Iq <= npq; Iq++) {
+      double d = A2(o->dpprime_visc_q, Iq, k, npq);
+      A2(fl, 1, Iq, 4) = d * A3(grad, 1, 1, Iq, 2, 2);
+      A2(fl, 2, Iq, 4) = d * A3(grad, 1, 2, Iq, 2, 2);
+      A2(fl, 3, Iq, 4) = d * A3(grad, 2, 1, Iq, 2, 2);
+      A2(fl, 4, Iq, 4) = d * A3(grad, 2, 2, Iq, 2, 2);
+    }
+    /* (the reference builds every layer's face values before the laplacians; per layer the
+     *  arithmetic is the same) */
+    lapq_face_values(o, ff, fl);
+    lapq_apply(o, rhs_lap + (size_t)(k - 1) * 2 * npoin, fl, ff);
+  }
+  free(Uk);
+  free(grad);
+  free(fl);
+  free(ff);
+}
+
 /* create_rhs_btp (mod_rhs_btp.F90:28-59) */
 static void create_rhs_btp(oracle *o, double *rhs, const double *qb, const double *qp) {
   const int npoin = o->npoin;
@@ -418,7 +592,10 @@ static void create_rhs_btp(oracle *o, double *rhs, const double *qb, const doubl
   btp_extract_df(o, qbf, qb);
   btp_volume(o, rhs, qb, qp);
   btp_fluxes(o, rhs, qbf);
-  btp_create_laplacian(o, rv, qb);
+  if (o->p.method_visc == 1)
+    btp_create_laplacian_v2(o, rv, qp, qb);
+  else
+    btp_create_laplacian(o, rv, qb);
   for (int I = 1; I <= npoin; I++) {
     A2(rhs, 2, I, 3) = A2(rhs, 2, I, 3) + A2(rv, 1, I, 2);
     A2(rhs, 3, I, 3) = A2(rhs, 3, I, 3) + A2(rv, 2, I, 2);
@@ -1225,7 +1402,10 @@ static void apply_layers_fluxes(oracle *o, double *rhs_mom, const double *qf) {
 static void rhs_momentum(oracle *o, double *rhs_mom, const double *qp, const double *q, const double *qf) {
   const int npoin = o->npoin, L = o->L;
   double *visc = zalloc(2 * (size_t)npoin * L);
-  bcl_create_laplacian(o, visc);
+  if (o->p.method_visc == 1)
+    bcl_create_laplacian_v2(o, visc, qp);
+  else
+    bcl_create_laplacian(o, visc);
   dynamics_volume_layers(o, rhs_mom, qp, q);
   apply_layers_fluxes(o, rhs_mom, qf);
   for (int k = 1; k <= L; k++)
@@ -1410,6 +1590,7 @@ static void set_dpprime_visc(oracle *o, const double *qp) {
   for (int k = 1; k <= o->L; k++)
     for (int I = 1; I <= o->npoin; I++)
       A2(o->dpprime_visc, I, k, o->npoin) = A3(qp, 1, I, k, 3, o->npoin);
+  if (o->p.method_visc == 1) interpolate_dpp(o);  /* ti_rk_bcl.F90:48,67 */
 }
 
 /* ============================================================== exported API */
@@ -1536,7 +1717,8 @@ int oracle_create(const hnumo_mesh_desc *m, const hnumo_static_desc *s, const hn
   o->nface = m->nface;
   o->nelem = m->nelem;
   o->L = m->nlayers;
-  if (p->method_visc == 1) return set_err(o, HNUMO_ERR_INVALID, "method_visc==1 not supported");
+  if (p->method_visc == 1 && (!m->imapl_q || !m->imapr_q))
+    return set_err(o, HNUMO_ERR_INVALID, "method_visc==1 needs imapl_q/imapr_q");
   if (p->ad_mlswe > 0.0) return set_err(o, HNUMO_ERR_INVALID, "ad_mlswe>0 not supported");
   if (o->L < 1 || o->L > 3) return set_err(o, HNUMO_ERR_INVALID, "nlayers must be 1..3 (qp(k) quirk)");
   if (o->nq > 32 || !m->psih || !m->index_df) return set_err(o, HNUMO_ERR_INVALID, "dense tables required");
@@ -1554,7 +1736,7 @@ int oracle_create(const hnumo_mesh_desc *m, const hnumo_static_desc *s, const hn
   o->btp_mass_flux_face_ave = zalloc(2 * nqf); o->ope_face_ave = zalloc(2 * nqf);
   o->ope2_face_ave = zalloc(2 * nqf); o->Qu_face_ave = zalloc(2 * nqf); o->Qv_face_ave = zalloc(2 * nqf);
   o->Quv_face_ave = zalloc(2 * nqf); o->H_face_ave = zalloc(nqf); o->one_plus_eta_edge_2_ave = zalloc(nqf);
-  o->dpprime_visc = zalloc(N * L); o->pbprime_visc = zalloc(N); o->btp_dpp_graduv = zalloc(4 * N);
+  o->dpprime_visc = zalloc(N * L); o->dpprime_visc_q = zalloc(Nq * L); o->pbprime_visc = zalloc(N); o->btp_dpp_graduv = zalloc(4 * N);
   o->dpp_graduv = zalloc(4 * N * L); o->graduv_dpp_face = zalloc(10 * ngf * L);
   o->btp_graduv_dpp_face = zalloc(10 * ngf); o->graduvb_face_ave = zalloc(8 * ngf);
   o->graduvb_ave = zalloc(4 * N); o->sum_layer_mass_flux = zalloc(2 * Nq);
@@ -1570,7 +1752,7 @@ void oracle_destroy(oracle *o) {
                      &o->tau_wind_ave, &o->ope2_ave_df, &o->uvb_ave_df, &o->uvb_face_ave,
                      &o->btp_mass_flux_face_ave, &o->ope_face_ave, &o->ope2_face_ave, &o->Qu_face_ave,
                      &o->Qv_face_ave, &o->Quv_face_ave, &o->H_face_ave, &o->one_plus_eta_edge_2_ave,
-                     &o->dpprime_visc, &o->pbprime_visc, &o->btp_dpp_graduv, &o->dpp_graduv,
+                     &o->dpprime_visc, &o->dpprime_visc_q, &o->pbprime_visc, &o->btp_dpp_graduv, &o->dpp_graduv,
                      &o->graduv_dpp_face, &o->btp_graduv_dpp_face, &o->graduvb_face_ave, &o->graduvb_ave,
                      &o->sum_layer_mass_flux, &o->sum_layer_mass_flux_face};
   for (size_t i = 0; i < sizeof ptrs / sizeof ptrs[0]; i++) free(*ptrs[i]);

@@ -48,7 +48,7 @@ program ref_driver
         Qv_face_ave, Quv_face_ave, H_face_ave, one_plus_eta_edge_2_ave, graduvb_ave, &
         graduvb_face_ave, Q_uu_dp, Q_uv_dp, Q_vv_dp, H_bcl, Q_uu_dp_edge, Q_uv_dp_edge, &
         Q_vv_dp_edge, H_bcl_edge, btp_dpp_graduv, pbprime_visc, btp_graduv_dpp_face, &
-        sum_layer_mass_flux, sum_layer_mass_flux_face, dpprime_visc
+        sum_layer_mass_flux, sum_layer_mass_flux_face, dpprime_visc, dpprime_visc_q
     use mod_mpi_communicator, only: ireq, status
     use mod_parallel, only: num_nbh, num_send_recv, nbh_send_recv, nbh_send_recv_multi, nbh_proc
     use mod_ref, only: q_send, q_recv, recv_data_dg, send_data_dg, lap_q_recv_df1, lap_q_send_df1, &
@@ -56,7 +56,7 @@ program ref_driver
     use mod_rk_mlswe, only: ti_barotropic_ssprk_mlswe
     use mod_rhs_btp, only: create_rhs_btp
     use mod_barotropic_terms, only: btp_bcl_coeffs_qdf
-    use mod_layer_terms, only: extract_qprime_df_face
+    use mod_layer_terms, only: extract_qprime_df_face, interpolate_dpp
 
     implicit none
 
@@ -107,6 +107,9 @@ program ref_driver
     imapl = 0; imapr = 0; imapl_q = 0; imapr_q = 0
     read(u) iface3; imapl(:, :, 1, :) = iface3
     read(u) iface3; imapr(:, :, 1, :) = iface3
+    deallocate(iface3); allocate(iface3(3, nq, nface))
+    read(u) iface3; imapl_q(:, :, 1, :) = iface3
+    read(u) iface3; imapr_q(:, :, 1, :) = iface3
     allocate(indexq(npts, npoin_q), index_df(npts, npoin))
     read(u) indexq
     read(u) index_df
@@ -189,6 +192,7 @@ program ref_driver
         allocate(qf(3, 2, ngl, nface, nlayers))
         call extract_qprime_df_face(qf, qprime_df)
         dpprime_visc(:, :) = qprime_df(1, :, :)
+        if (method_visc == 1) call interpolate_dpp(dpprime_visc_q, dpprime_visc)  ! as ti_rk_bcl.F90:48
         call btp_bcl_coeffs_qdf(qf, qprime_df)
         if (mode == 1) then
             call zero_accumulators()

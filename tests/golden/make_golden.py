@@ -30,6 +30,8 @@ GOLDEN = [
     ("lake10_step1", "lake10", "step", 1, 1),
     ("dg25_step1", "dg25", "step", 1, 7),
     ("dg25L3_step1", "dg25L3", "step", 1, 7),
+    ("bump10q_step1", "bump10q", "step", 1, 1),
+    ("dg8L3q_step1", "dg8L3q", "step", 1, 1),
 ]
 FIELDS_KEPT = ["ope_ave", "H_ave", "Qu_ave", "btp_mass_flux_ave", "uvb_face_ave", "H_face_ave",
                "graduvb_ave", "Q_uu_dp", "H_bcl_edge", "btp_graduv_dpp_face"]

@@ -11,7 +11,8 @@ from util import layer_mass
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = os.path.join(HERE, "golden")
-GOLDEN = ["bump10_rhs", "bump10_btp", "bump10_step2", "lake10_step1", "dg25_step1", "dg25L3_step1"]
+GOLDEN = ["bump10_rhs", "bump10_btp", "bump10_step2", "lake10_step1", "dg25_step1", "dg25L3_step1",
+          "bump10q_step1", "dg8L3q_step1"]
 
 
 def load(name):
@@ -70,6 +71,8 @@ def test_oracle_matches_golden(name, case_factory):
     dict(name="bump10", botfr=2, cd=1e-3, visc=25.0, method_visc=3, y_boundary=(2, 2)),
     dict(name="bump10", botfr=1, cd=1e-7, f0=1e-4, beta=1e-11, x_boundary=(2, 4)),
     dict(name="lake10", nlayers=3),
+    dict(name="bump10q", y_boundary=(2, 2), botfr=2, cd=1e-3),   # quad-point LDG + no-slip walls
+    dict(name="dg8L3q", x_boundary=(2, 4)),                       # 3 layers, wind, drag, mixed walls
 ])
 def test_oracle_matches_reference_fortran(variant):
     """Branches the shipped configs do not exercise (quadratic drag, no-slip walls, mixed
@@ -106,3 +109,17 @@ def test_lake_at_rest_is_well_balanced(case_factory):
     q, qb, qp = o.state()
     o.ti_rk_bcl(q, qb, qp)
     assert np.abs(qb[2:4]).max() < 1e-6 * np.abs(qb[0]).max()
+
+
+def test_quad_ldg_branch_is_live(case_factory):
+    """method_visc == 1 (quad-point LDG, mod_laplacian_quad.F90:125-223,252-355) takes its own
+    path: the state after one step differs from the nodal-LDG run of the same case."""
+    import oracle as O
+    out = []
+    for mv in (1, 3):
+        case = case_factory("bump10q", method_visc=mv)
+        o = O.Oracle(case)
+        q, qb, qp = o.state()
+        o.ti_rk_bcl(q, qb, qp)
+        out.append(qb.copy())
+    assert not np.array_equal(out[0], out[1])
