@@ -22,6 +22,7 @@
 #include "engine_internal.h"
 #include "kernels_bcl.hip"
 #include "kernels_btp.hip"
+#include "kernels_lapq.hip"
 
 using namespace hnumo;
 
@@ -93,6 +94,12 @@ struct hnumo_engine {
   unsigned long long *epoch = nullptr;        // tag epoch, bumped before every persistent sub-cycle
   StageArgs *d_stages[2] = {nullptr, nullptr};  // per-stage arguments: predictor (qp), corrector (qp2)
   int sub_final = 0;                          // qbuf index holding the sub-cycle result
+  // method_visc == 1 (quad-point LDG, kernels_lapq.hip)
+  bool lapq_on = false;
+  double *dpq = nullptr;      // dpprime_visc_q [L][npoin_q]
+  double *lq_flux = nullptr;  // LDG fluxes at the quad points [L][E][4][Q] (barotropic: layer block 0)
+  double *lapq = nullptr;     // Laplacians [L][2][npoin] (barotropic: [2][npoin])
+  int *fqLR = nullptr;        // [2][F][NQ] element-local quad point of each face quad point, left | right
 };
 
 template <typename T>
@@ -155,6 +162,23 @@ struct Launch {
                        e->qcoef, e->ncoef, e->dpp_graduv, e->dpprime_visc, e->ecoef);
     hipLaunchKernelGGL((bcl_coeffs_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf,
                        e->dpp_graduv, e->dpprime_visc, e->fcoef, e->fncoef, e->gdpp_face, e->efcoef);
+    if (e->lapq_on)  // interpolate_dpp right after dpprime_visc is set (ti_rk_bcl.F90:48,67)
+      hipLaunchKernelGGL((lapq_dpp_kernel<NGL, NQ>), dim3(std::min<size_t>(((size_t)e->L * e->npq + 255) / 256, 4096)),
+                         dim3(256), 0, e->stream, e->m, e->dpprime_visc, e->dpq);
+  }
+  // method_visc == 1, one barotropic stage: btp_create_laplacian_v2's Laplacian of state qb
+  static void lapq_btp(hnumo_engine *e, const double *qb, const double *qp) {
+    hipLaunchKernelGGL((lapq_flux_kernel<NGL, NQ>), dim3(e->nelem), dim3(256), 0, e->stream, e->m, qb, qp, e->nacc,
+                       e->dpq, e->lq_flux, 0, 0);
+    hipLaunchKernelGGL((lapq_apply_kernel<NGL, NQ>), dim3(e->nelem_owned, 1), dim3(64), 0, e->stream, e->m, e->lq_flux,
+                       e->lapq, e->fqLR, e->fqLR + e->FQ);
+  }
+  // method_visc == 1, baroclinic: bcl_create_laplacian_v2's per-layer Laplacians of qprime
+  static void lapq_bcl(hnumo_engine *e, const double *qp) {
+    hipLaunchKernelGGL((lapq_flux_kernel<NGL, NQ>), dim3(e->nelem), dim3(256), 0, e->stream, e->m, nullptr, qp,
+                       e->nacc, e->dpq, e->lq_flux, 1, 0);
+    hipLaunchKernelGGL((lapq_apply_kernel<NGL, NQ>), dim3(e->nelem_owned, e->L), dim3(64), 0, e->stream, e->m,
+                       e->lq_flux, e->lapq, e->fqLR, e->fqLR + e->FQ);
   }
   // layer mass update (owned elements); produces dp' (e->dpp) for the consistency step
   static void mass(hnumo_engine *e, const double *qp, const double *qf, double *q) {
@@ -171,10 +195,12 @@ struct Launch {
   }
   static void momentum(hnumo_engine *e, const double *qf, const double *qp_in, const double *qb, double *q,
                        double *qp_out, int mode) {
+    if (e->lapq_on) lapq_bcl(e, qp_in);
     hipLaunchKernelGGL((mom_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
                        e->gdpp_face, e->gfacc, e->momL, e->momR, e->lapf);
     hipLaunchKernelGGL((mom_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(MomCfg<NGL, NQ>::BS), 0, e->stream, e->m, qp_in, e->qacc,
-                       e->nacc, e->dpp_graduv, e->dpprime_visc, e->momL, e->momR, e->lapf, qb, q, qp_out, mode);
+                       e->nacc, e->dpp_graduv, e->dpprime_visc, e->momL, e->momR, e->lapf, qb, q, qp_out, mode,
+                       e->lapq_on ? e->lapq : nullptr);
   }
 };
 
@@ -375,6 +401,7 @@ static int stage_table(hnumo_engine *e, const double *qp, std::vector<StageArgs>
       a.first_of_step = ik == 0;
       a.save_q2 = K == 5 && ik == 2;
       a.err = e->neg_flag;
+      a.lapq = e->lapq_on ? e->lapq : nullptr;
       out_args.push_back(a);
       gt = 1 - gt;
       cur = out;
@@ -384,7 +411,10 @@ static int stage_table(hnumo_engine *e, const double *qp, std::vector<StageArgs>
   return cur;
 }
 
-static bool use_persistent(const hnumo_engine *e) { return e->comm_mode == 0 && e->persistent_ok[e->summation]; }
+// (method_visc == 1 needs its Laplacian kernels between the stages: per-stage launches)
+static bool use_persistent(const hnumo_engine *e) {
+  return e->comm_mode == 0 && !e->lapq_on && e->persistent_ok[e->summation];
+}
 
 // ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:19-151) on device state qb_state
 static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp, bool timed = false) {
@@ -406,6 +436,7 @@ static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp,
     cur = stage_table(e, qp, st);
     if (timed && e->kernel_events) (void)hipEventRecord(e->evk0, e->stream);
     for (const StageArgs &a : st) {
+      if (e->lapq_on) DISPATCH(e, lapq_btp(e, a.qb_in, a.qprime));
       DISPATCH(e, stage(e, a));
       if (a.write_trace && e->comm_mode) {
         // ghosts take the owners' new state; their traces go into the owned elements' slots
@@ -499,7 +530,11 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
       if (halo->num_send_recv && halo->num_send_recv[k] > 0)
         return fail(eng, HNUMO_ERR_INVALID, "processor-face halos are not supported: use the ghost-element lists");
   }
-  if (par->method_visc == 1) return fail(eng, HNUMO_ERR_INVALID, "method_visc==1 (quad-point LDG) not supported");
+  if (par->method_visc == 1) {
+    if (!mesh->imapl_q || !mesh->imapr_q) return fail(eng, HNUMO_ERR_INVALID, "method_visc==1 needs imapl_q/imapr_q");
+    if (halo && halo->nranks > 1)
+      return fail(eng, HNUMO_ERR_INVALID, "method_visc==1 (quad-point LDG) is single-rank only in this build");
+  }
   if (par->ad_mlswe > 0.0) return fail(eng, HNUMO_ERR_INVALID, "ad_mlswe>0 (vertical shear stress) not supported");
   if (mesh->nlayers < 1 || mesh->nlayers > MAXL)
     return fail(eng, HNUMO_ERR_INVALID, "nlayers must be 1..3 (qp(k) quirk, mod_create_rhs_mlswe.F90:382)");
@@ -758,6 +793,25 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   eng->fmass = dalloc<double>(eng, FQ * L); eng->fcons = dalloc<double>(eng, FQ * L);
   eng->momL = dalloc<double>(eng, 2 * FQ * L); eng->momR = dalloc<double>(eng, 2 * FQ * L);
   eng->lapf = dalloc<double>(eng, 2 * FN * L);
+  if (par->method_visc == 1) {  // quad-point LDG (kernels_lapq.hip)
+    eng->lapq_on = true;
+    eng->dpq = dalloc<double>(eng, npq * L);
+    eng->lq_flux = dalloc<double>(eng, 4 * npq * L);
+    eng->lapq = dalloc<double>(eng, 2 * npoin * L);
+    std::vector<int> fq(2 * FQ, -1);
+    for (int s = 0; s < 2; s++) {
+      const int32_t *imq = s == 0 ? mesh->imapl_q : mesh->imapr_q;
+      for (int f = 0; f < F; f++)
+        for (int iq = 0; iq < nq; iq++) {
+          const int i = imq[3 * (iq + nq * f)] - 1, j = imq[3 * (iq + nq * f) + 1] - 1;
+          if (s == 1 && mesh->face[8 * f + 7] <= 0) continue;
+          if (i < 0 || i >= nq || j < 0 || j >= nq) return fail(eng, HNUMO_ERR_INVALID, "imapl_q/imapr_q out of range");
+          fq[s * FQ + (size_t)f * nq + iq] = j * nq + i;
+        }
+    }
+    eng->fqLR = dalloc<int>(eng, 2 * FQ);
+    if (eng->fqLR) HIPCHK(hipMemcpy(eng->fqLR, fq.data(), fq.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
   eng->rhs = dalloc<double>(eng, 3 * npoin);
   eng->neg_flag = dalloc<int>(eng, 1);
   if (const char *sm = getenv("HNUMO_SUMMATION"))
@@ -1007,6 +1061,8 @@ int hnumo_create_rhs_btp(hnumo_engine *eng, double *rhs, const double *qb_df, co
   a.qacc = eng->qacc; a.facc = eng->facc; a.nacc = eng->nacc; a.gfacc = eng->gfacc;
   a.qb_out = eng->qbuf[0]; a.rhs_out = eng->rhs;
   a.rhs_only = 1; a.write_trace = 0; a.accumulate = 1;
+  a.lapq = eng->lapq_on ? eng->lapq : nullptr;
+  if (eng->lapq_on) DISPATCH(eng, lapq_btp(eng, eng->qb, eng->qp));
   DISPATCH(eng, stage(eng, a));
   HIPCHK(hipMemcpyAsync(rhs, eng->rhs, 3 * (size_t)eng->npoin * 8, hipMemcpyDeviceToHost, eng->stream));
   HIPCHK(hipStreamSynchronize(eng->stream));

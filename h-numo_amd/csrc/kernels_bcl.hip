@@ -751,7 +751,7 @@ template <int NGL, int NQ>
 __global__ void __launch_bounds__(256, 2)
     mom_elem_kernel(DevMesh m, const double *qp_in, const double *qacc, const double *nacc, const double *dpp_graduv,
                     const double *dpprime_visc, const double *momL, const double *momR, const double *lapf,
-                    const double *qb, double *q, double *qp_out, int mode) {
+                    const double *qb, double *q, double *qp_out, int mode, const double *lapx) {
   constexpr int P = MomCfg<NGL, NQ>::P, Q = MomCfg<NGL, NQ>::Q, BS = MomCfg<NGL, NQ>::BS;
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
   const double g = m.gravity, eps1 = 1.0e-20;
@@ -1039,7 +1039,10 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
     for (int k = 0; k < MAXL; k++) {
       if (k >= L) break;
-      const double v0 = m.visc * mi * s_r[k][2][p], v1 = m.visc * mi * s_r[k][3][p];
+      // (method_visc == 1: the layer's Laplacian comes from lapq_apply_kernel, [L][2][npoin])
+      const double l0 = lapx ? lapx[((size_t)k * 2) * npoin + I] : s_r[k][2][p];
+      const double l1 = lapx ? lapx[((size_t)k * 2 + 1) * npoin + I] : s_r[k][3][p];
+      const double v0 = m.visc * mi * l0, v1 = m.visc * mi * l1;
       const double rm0 = mi * s_r[k][0][p] + v0;
       const double rm1 = mi * s_r[k][1][p] + v1;
       const double q2 = s_qm2[k][0][p], q3 = s_qm2[k][1][p];

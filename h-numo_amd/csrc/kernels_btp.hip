@@ -87,6 +87,10 @@ struct StageArgs {
   unsigned long long tag_in, tag_out;        // stage tags (the launch epoch << 20 is or-ed in)
   int first_of_step, save_q2;                // ik == 0 (state -> qb0), K == 5 && ik == 2 (state -> qb2)
   int *err;                                  // bit 8: a granule wait timed out
+  // method_visc == 1: the viscous Laplacian (without visc*massinv) from lapq_apply_kernel,
+  // [2][npoin]; the fused nodal LDG then only keeps its ope2/uvb averages (graduvb_ave and
+  // graduvb_face_ave are not accumulated on that branch, mod_laplacian_quad.F90:125-223)
+  const double *lapq;
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -783,8 +787,9 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
 #pragma unroll
       for (int c = 0; c < 4; c++) s_grad[c * P + p] = g[c];
       if (a.accumulate) {
+        if (!a.lapq)
 #pragma unroll
-        for (int c = 0; c < 4; c++) atomicAdd(&a.nacc[NACC_I(NA_G1 + c, e, p)], g[c]);
+          for (int c = 0; c < 4; c++) atomicAdd(&a.nacc[NACC_I(NA_G1 + c, e, p)], g[c]);
         const double t1 = 1.0 + s_qb[p * 4 + 1] * s_ns[NE_OOP * P + p];
         atomicAdd(&a.nacc[NACC_I(NA_OPE2, e, p)], t1 * t1);
         atomicAdd(&a.nacc[NACC_I(NA_UB, e, p)], s_u[p]);
@@ -816,7 +821,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   auto ldg_task = [&](int t, bool first) {
     const int lf = t / NGL, n = t % NGL;
     const int side = s_side[lf], er = s_bc[lf];
-    const bool keep = a.accumulate && s_acc[lf];
+    const bool keep = a.accumulate && s_acc[lf] && !a.lapq;
     const int p = s_map[lf * NGL + n];
     const double *efn = s_ef + lf * C::FBLK + EF_N * NQ;
     const double *B = s_ec + lf * C::EFC + 4 * NQ;  // btp_graduv_dpp_face(c) at [c][NGL]
@@ -1106,8 +1111,10 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     const size_t I = (size_t)e * P + p;
     const double mi = s_ns[NE_MINV * P + p];
     double rh0 = mi * s_rhs[0 * P + p], rh1 = mi * s_rhs[1 * P + p], rh2 = mi * s_rhs[2 * P + p];
-    rh1 = rh1 + m.visc * mi * s_lap[0 * P + p];
-    rh2 = rh2 + m.visc * mi * s_lap[1 * P + p];
+    const double l0 = a.lapq ? a.lapq[I] : s_lap[0 * P + p];
+    const double l1 = a.lapq ? a.lapq[(size_t)npoin + I] : s_lap[1 * P + p];
+    rh1 = rh1 + m.visc * mi * l0;
+    rh2 = rh2 + m.visc * mi * l1;
     if (a.rhs_only) {
       a.rhs_out[I * 3 + 0] = rh0;
       a.rhs_out[I * 3 + 1] = rh1;

@@ -37,7 +37,7 @@ def get_engine(engines, case, summation="reference"):
     return engines[key]
 
 
-@pytest.mark.parametrize("cfg", ["bump10", "dg25", "dg25L3"])
+@pytest.mark.parametrize("cfg", ["bump10", "dg25", "dg25L3", "bump10q", "dg8L3q"])
 def test_rhs_stage_parity(cfg, case_factory, engines):
     import oracle as O
     case = case_factory(cfg)
@@ -100,7 +100,7 @@ def test_baroclinic_step_parity(cfg, nsteps, case_factory, engines):
         assert rel(qbe[v], qb[v]) < TOL, ("qb", v, rel(qbe[v], qb[v]))
 
 
-@pytest.mark.parametrize("cfg", ["bump10", "dg25L3"])
+@pytest.mark.parametrize("cfg", ["bump10", "dg25L3", "bump10q", "dg8L3q"])
 def test_bitwise_step(cfg, case_factory, engines):
     """The engine reproduces the reference arithmetic bit for bit (2 baroclinic steps)."""
     import oracle as O
@@ -118,7 +118,8 @@ def test_bitwise_step(cfg, case_factory, engines):
         assert np.array_equal(e.field(f), o.field(f)), f
 
 
-@pytest.mark.parametrize("name", ["bump10_step2", "lake10_step1", "dg25_step1", "dg25L3_step1"])
+@pytest.mark.parametrize("name", ["bump10_step2", "lake10_step1", "dg25_step1", "dg25L3_step1", "bump10q_step1",
+                                  "dg8L3q_step1"])
 def test_engine_matches_reference_golden(name, case_factory, engines):
     g = dict(np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False))
     case = case_factory(str(g["config"]))
