@@ -29,7 +29,7 @@ _NODE_C = ["q_df", "qb_df", "qprime_df", "coord"]              # (ncomp, npoin[,
 _QUAD = ["pbprime", "one_over_pbprime", "coriolis_quad", "wjac"]
 _QUAD_C = ["tau_wind", "grad_zbot_quad"]                        # (2, npoin_q)
 _ELEM = ["ksiq_x", "ksiq_y", "etaq_x", "etaq_y", "jacq", "ksi_x", "ksi_y", "eta_x", "eta_y", "jac"]
-_FACE_LAST = ["imapl", "imapr", "normal_vector", "normal_vector_q", "jac_face", "jac_faceq", "pbprime_face",
+_FACE_LAST = ["imapl", "imapr", "imapl_q", "imapr_q", "normal_vector", "normal_vector_q", "jac_face", "jac_faceq", "pbprime_face",
               "pbprime_df_face", "one_over_pbprime_edge", "coeff_pbpert_L", "coeff_pbpert_R", "coeff_pbub_LR",
               "coeff_mass_pbub_L", "coeff_mass_pbub_R", "coeff_mass_pbpert_LR", "zbot_face"]
 _DENSE_Q = ["psih", "dpsidx", "dpsidy"]                         # (P, npoin_q)
@@ -151,8 +151,9 @@ def partition(case: Case, nranks: int, rank: int) -> RankCase:
         lf[7, flip] = -4
         lf[4, flip] = face[5, faces[flip]]
         lf[5, flip] = 0
-        B["imapl"][..., flip] = B["imapr"][..., flip]
-        B["imapr"][..., flip] = 0
+        for a, b in (("imapl", "imapr"), ("imapl_q", "imapr_q")):
+            B[a][..., flip] = B[b][..., flip]
+            B[b][..., flip] = 0
         for k in ("normal_vector", "normal_vector_q"):
             B[k][..., flip] = -B[k][..., flip]
         for k in ("pbprime_face", "pbprime_df_face", "zbot_face"):
@@ -163,6 +164,7 @@ def partition(case: Case, nranks: int, rank: int) -> RankCase:
     if wall_r.any():
         lf[5, wall_r] = 0
         B["imapr"][..., wall_r] = 0
+        B["imapr_q"][..., wall_r] = 0
     B["face"] = lf
 
     # halo lists
