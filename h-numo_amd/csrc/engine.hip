@@ -486,6 +486,9 @@ static void launch_step(hnumo_engine *e) {
   hipLaunchKernelGGL(qprime_final_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp, e->qp2, e->dpp2, nl);
   exchange_qp(e, e->qp);
   hipLaunchKernelGGL(finite_check_kernel, dim3(256), dim3(256), 0, e->stream, e->qb, 4 * (size_t)e->npoin, e->neg_flag);
+  // ad_mlswe > 0 with the reference's corrector input leaves NaN layer momenta (hnumo_params)
+  if (e->p.ad_mlswe > 0.0)
+    hipLaunchKernelGGL(finite_check_kernel, dim3(256), dim3(256), 0, e->stream, e->q, n3, e->neg_flag);
 }
 
 // ------------------------------------------------------------------ C ABI
@@ -535,7 +538,8 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     if (halo && halo->nranks > 1)
       return fail(eng, HNUMO_ERR_INVALID, "method_visc==1 (quad-point LDG) is single-rank only in this build");
   }
-  if (par->ad_mlswe > 0.0) return fail(eng, HNUMO_ERR_INVALID, "ad_mlswe>0 (vertical shear stress) not supported");
+  if (par->shear_corrector != HNUMO_SHEAR_CORRECTOR_REFERENCE && par->shear_corrector != HNUMO_SHEAR_CORRECTOR_PREDICTED)
+    return fail(eng, HNUMO_ERR_INVALID, "shear_corrector must be HNUMO_SHEAR_CORRECTOR_REFERENCE or _PREDICTED");
   if (mesh->nlayers < 1 || mesh->nlayers > MAXL)
     return fail(eng, HNUMO_ERR_INVALID, "nlayers must be 1..3 (qp(k) quirk, mod_create_rhs_mlswe.F90:382)");
   if (!supported_ngl(mesh->ngl) || mesh->nq != 2 * mesh->ngl - 1)
@@ -885,6 +889,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   m.alpha = eng->alpha;
   m.gravity = par->gravity; m.cd = par->cd_mlswe; m.visc = par->visc_mlswe; m.dt = par->dt; m.dt_btp = par->dt_btp;
   m.botfr = par->botfr;
+  m.ad = par->ad_mlswe; m.max_shear_dz = par->max_shear_dz; m.shear_corr = par->shear_corrector;
 
   // persistent sub-cycle: stage tables for the two sub-cycles of a step and the residency check
   if (supported_ngl(ngl) && eng->K <= 8) {

@@ -107,6 +107,8 @@ struct DevMesh {
   const double *alpha;            // [L]
   double gravity, cd, visc, dt, dt_btp;
   int botfr;
+  double ad, max_shear_dz;        // ad_mlswe, max_shear_dz (implicit vertical shear stress)
+  int shear_corr;                 // hnumo_params.shear_corrector
 };
 
 }  // namespace hnumo

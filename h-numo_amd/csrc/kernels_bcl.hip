@@ -1025,17 +1025,16 @@ __global__ void __launch_bounds__(256, 2)
   }
   __syncthreads();
 
-  // ---- 4: per node: rhs_mom, update with implicit Coriolis (mod_splitting.F90:131-173 /
-  //      :239-280), layer_mom_boundary_df on the element's wall faces in face order
-  //      (mod_layer_terms.F90:529-584), evaluate_bcl / evaluate_bcl_v1 with
-  //      extract_velocity (:198-320)
+  // ---- 4: per node: rhs_mom and q_df_temp = q + dt*rhs_mom (mod_splitting.F90:134-137 /
+  //      :242-245), kept in s_r[k][0..1].  With ad_mlswe > 0 also the shear-stress input
+  //      q_df3 = the Coriolis-rotated q_df_temp (:141-150 / :249-257) made consistent with
+  //      u_bar by velocity_df (mod_layer_terms.F90:139-196), into s_qq[k][0..2] (dead since
+  //      phase 2); momentum() (mode 1) passes its never-assigned `uv` instead (mod_splitting.
+  //      F90:119,158): zeros unless shear_corr selects q_df3 (hnumo_params.shear_corrector)
+  const bool shear = m.ad > 0.0, shear_zero = mode == 1 && m.shear_corr != 1;
   for (int p = tid; p < P; p += BS) {
     const size_t I = (size_t)e * P + p;
     const double mi = m.nstat[NS_MINV * (size_t)npoin + I];
-    const double f2 = m.nstat[NS_F2 * (size_t)npoin + I], ab = m.nstat[NS_A * (size_t)npoin + I],
-                 bb = m.nstat[NS_B * (size_t)npoin + I];
-    const double b1 = qb[I * 4], b3 = qb[I * 4 + 2], b4 = qb[I * 4 + 3];
-    double nw[MAXL][3];
 #pragma unroll
     for (int k = 0; k < MAXL; k++) {
       if (k >= L) break;
@@ -1045,9 +1044,168 @@ __global__ void __launch_bounds__(256, 2)
       const double v0 = m.visc * mi * l0, v1 = m.visc * mi * l1;
       const double rm0 = mi * s_r[k][0][p] + v0;
       const double rm1 = mi * s_r[k][1][p] + v1;
+      s_r[k][0][p] = s_qm2[k][0][p] + m.dt * rm0;
+      s_r[k][1][p] = s_qm2[k][1][p] + m.dt * rm1;
+    }
+    if (shear) {
+      const double f2 = m.nstat[NS_F2 * (size_t)npoin + I], ab = m.nstat[NS_A * (size_t)npoin + I],
+                   bb = m.nstat[NS_B * (size_t)npoin + I];
+      const double b1 = qb[I * 4], b3 = qb[I * 4 + 2], b4 = qb[I * 4 + 3];
+      double h[MAXL], uv[MAXL][2], ub = 0.0, vb = 0.0;
+#pragma unroll
+      for (int k = 0; k < MAXL; k++) {
+        if (k >= L) break;
+        h[k] = q[((size_t)k * npoin + I) * 3];
+        const double q2 = s_qm2[k][0][p], q3 = s_qm2[k][1][p];
+        const double tu = s_r[k][0][p] + f2 * q3, tv = s_r[k][1][p] - f2 * q2;
+        uv[k][0] = (ab * tu + bb * tv) / h[k];
+        uv[k][1] = (-bb * tu + ab * tv) / h[k];
+      }
+#pragma unroll
+      for (int k = 0; k < MAXL; k++) {
+        if (k >= L) break;
+        ub = ub + uv[k][0] * h[k];
+        vb = vb + uv[k][1] * h[k];
+      }
+      if (b1 > 0.0) {
+        ub = ub / b1;
+        vb = vb / b1;
+#pragma unroll
+        for (int k = 0; k < MAXL; k++) {
+          if (k >= L) break;
+          uv[k][0] = uv[k][0] - ub + b3 / b1;
+          uv[k][1] = uv[k][1] - vb + b4 / b1;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < MAXL; k++) uv[k][0] = uv[k][1] = 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < MAXL; k++) {
+        if (k >= L) break;
+        s_qq[k][0][p] = shear_zero ? 0.0 : h[k];
+        s_qq[k][1][p] = shear_zero ? 0.0 : uv[k][0] * h[k];
+        s_qq[k][2][p] = shear_zero ? 0.0 : uv[k][1] * h[k];
+      }
+    }
+  }
+  if (shear) {
+    __syncthreads();
+    // ---- 4b: rhs_layer_shear_stress (mod_create_rhs_mlswe.F90:181-251), one thread per quad
+    //      point: dp, u*dp, v*dp of every layer (reference order), the tridiagonal system over
+    //      the layers (sub-diagonal -coeff, super-diagonal -coeff1, as written), the interface
+    //      stresses; g*(tau_k - tau_{k+1}) into s_G[k][0..1] (dead since phase 3).
+    //      tau(nlayers+1) is never assigned there (:160,:246-251): zero, as under the reference
+    //      build's -finit-real=zero
+    const double al1 = m.alpha[0];
+    for (int qd = tid; qd < Q; qd += BS) {
+      const int iq = qd % NQ, jq = qd / NQ;
+      double pa[NGL], pb[NGL], dp[MAXL], udp[MAXL], vdp[MAXL];
+#pragma unroll
+      for (int n = 0; n < NGL; n++) {
+        pa[n] = s_psiq[n * NQ + iq];
+        pb[n] = s_psiq[n * NQ + jq];
+      }
+#pragma unroll
+      for (int k = 0; k < MAXL; k++) dp[k] = udp[k] = vdp[k] = 0.0;
+#pragma unroll 1
+      for (int mm = 0; mm < NGL; mm++)
+#pragma unroll
+        for (int n = 0; n < NGL; n++) {
+          const int ip = mm * NGL + n;
+          const double hi = pa[n] * pb[mm];
+#pragma unroll
+          for (int k = 0; k < MAXL; k++) {
+            if (k >= L) break;
+            dp[k] = dp[k] + hi * s_qq[k][0][ip];
+            udp[k] = udp[k] + hi * s_qq[k][1][ip];
+            vdp[k] = vdp[k] + hi * s_qq[k][2][ip];
+          }
+        }
+      // Fortran MAX as gfortran evaluates it: the second argument if larger or the first is NaN
+      double coeff = sqrt(0.5 * m.qstat[QS_COR * (size_t)npq + (size_t)e * Q + qd] * m.ad) / al1;
+      const double cz = m.ad / (al1 * m.max_shear_dz);
+      if (cz > coeff || isnan(coeff)) coeff = cz;
+      const double coeff1 = g * m.dt * coeff;
+      double bd[MAXL], r0[MAXL], r1[MAXL], tu[MAXL + 1], tv[MAXL + 1];
+#pragma unroll
+      for (int k = 0; k <= MAXL; k++) tu[k] = tv[k] = 0.0;
+#pragma unroll
+      for (int k = 0; k < MAXL; k++) {
+        if (k >= L) break;
+        bd[k] = (k == 0 || k == L - 1) ? dp[k] + coeff1 : dp[k] + 2.0 * coeff1;
+        r0[k] = udp[k] / dp[k];
+        r1[k] = vdp[k] / dp[k];
+      }
+#pragma unroll
+      for (int k = 1; k < MAXL; k++) {
+        if (k >= L) break;
+        const double mult = -coeff / bd[k - 1];
+        bd[k] = bd[k] - mult * (-coeff1);
+        r0[k] = r0[k] - mult * r0[k - 1];
+        r1[k] = r1[k] - mult * r1[k - 1];
+      }
+#pragma unroll
+      for (int k = 0; k < MAXL; k++)
+        if (k == L - 1) {
+          r0[k] = r0[k] / bd[k];
+          r1[k] = r1[k] / bd[k];
+        }
+#pragma unroll
+      for (int k = MAXL - 2; k >= 0; k--) {
+        if (k >= L - 1) continue;
+        r0[k] = (r0[k] - (-coeff1) * r0[k + 1]) / bd[k];
+        r1[k] = (r1[k] - (-coeff1) * r1[k + 1]) / bd[k];
+      }
+#pragma unroll
+      for (int k = 1; k < MAXL; k++) {
+        if (k >= L) break;
+        tu[k] = coeff * (r0[k - 1] - r0[k]);
+        tv[k] = coeff * (r1[k - 1] - r1[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < MAXL; k++) {
+        if (k >= L) break;
+        s_G[k][0][qd] = g * (tu[k] - tu[k + 1]);
+        s_G[k][1][qd] = g * (tv[k] - tv[k + 1]);
+      }
+    }
+    __syncthreads();
+    // ---- 4c: rhs_stress(c,p,k) = sum over the quad points in order of wq*hi*tau_q (:253-269);
+    //      q_df_temp += dt*(massinv*rhs_stress) (mod_splitting.F90:160-163 / :267-270)
+    for (int t = tid; t < L * 2 * P; t += BS) {
+      const int k = t / (2 * P), c = (t / P) % 2, p = t % P, i = p % NGL, j = p / NGL;
+      const double *T = s_G[k][c];
+      double acc = 0.0;
+#pragma unroll 1
+      for (int jq = 0; jq < NQ; jq++) {
+        const double pj = s_psiq[j * NQ + jq];
+#pragma unroll
+        for (int iq = 0; iq < NQ; iq++) {
+          const int qd = jq * NQ + iq;
+          acc = acc + s_qm[4][qd] * (s_psiq[i * NQ + iq] * pj) * T[qd];
+        }
+      }
+      const double mi = m.nstat[NS_MINV * (size_t)npoin + (size_t)e * P + p];
+      s_r[k][c][p] = s_r[k][c][p] + m.dt * (mi * acc);
+    }
+    __syncthreads();
+  }
+
+  // ---- 4d: implicit Coriolis (mod_splitting.F90:166-173 / :273-280), layer_mom_boundary_df
+  //      on the element's wall faces in face order (mod_layer_terms.F90:529-584),
+  //      evaluate_bcl / evaluate_bcl_v1 with extract_velocity (:198-320)
+  for (int p = tid; p < P; p += BS) {
+    const size_t I = (size_t)e * P + p;
+    const double f2 = m.nstat[NS_F2 * (size_t)npoin + I], ab = m.nstat[NS_A * (size_t)npoin + I],
+                 bb = m.nstat[NS_B * (size_t)npoin + I];
+    const double b1 = qb[I * 4], b3 = qb[I * 4 + 2], b4 = qb[I * 4 + 3];
+    double nw[MAXL][3];
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
       const double q2 = s_qm2[k][0][p], q3 = s_qm2[k][1][p];
-      const double t1 = q2 + m.dt * rm0, t2 = q3 + m.dt * rm1;
-      const double tu = t1 + f2 * q3, tv = t2 - f2 * q2;
+      const double tu = s_r[k][0][p] + f2 * q3, tv = s_r[k][1][p] - f2 * q2;
       nw[k][1] = ab * tu + bb * tv;
       nw[k][2] = -bb * tu + ab * tv;
       nw[k][0] = q[((size_t)k * npoin + I) * 3];

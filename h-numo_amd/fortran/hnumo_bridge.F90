@@ -52,7 +52,8 @@ contains
         use mod_grid, only: nelem, npoin, npoin_q, nface, face
         use mod_face, only: imapl, imapr, imapl_q, imapr_q, normal_vector, normal_vector_q, jac_face, jac_faceq
         use mod_metrics, only: massinv, ksiq_x, ksiq_y, etaq_x, etaq_y, jacq, ksi_x, ksi_y, eta_x, eta_y, jac
-        use mod_input, only: nlayers, dt, dt_btp, kstages, method_visc, visc_mlswe, botfr, cd_mlswe, ad_mlswe
+        use mod_input, only: nlayers, dt, dt_btp, kstages, method_visc, visc_mlswe, botfr, cd_mlswe, ad_mlswe, &
+            max_shear_dz
         use mod_constants, only: gravity
         use mod_initial, only: pbprime, pbprime_df, one_over_pbprime, one_over_pbprime_df, pbprime_face, &
             pbprime_df_face, one_over_pbprime_edge, coeff_pbpert_L, coeff_pbpert_R, coeff_pbub_LR, &
@@ -108,7 +109,8 @@ contains
         st%ssprk_a = pd(ssprk_a); st%ssprk_beta = pd(ssprk_beta)
 
         par%dt = dt; par%dt_btp = dt_btp; par%visc_mlswe = visc_mlswe; par%cd_mlswe = cd_mlswe
-        par%ad_mlswe = ad_mlswe; par%gravity = gravity
+        par%ad_mlswe = ad_mlswe; par%gravity = gravity; par%max_shear_dz = max_shear_dz
+        par%shear_corrector = HNUMO_SHEAR_CORRECTOR_REFERENCE   ! the reference's semantics (hnumo_engine.h)
         par%N_btp = N_btp; par%kstages = kstages; par%method_visc = method_visc; par%botfr = botfr
 
         rc = hnumo_engine_create(mesh, st, par, c_null_ptr, int(device, c_int), engine)

@@ -39,6 +39,7 @@ class Params(C.Structure):
         ("dt", C.c_double), ("dt_btp", C.c_double), ("visc_mlswe", C.c_double),
         ("cd_mlswe", C.c_double), ("ad_mlswe", C.c_double), ("gravity", C.c_double),
         ("N_btp", C.c_int32), ("kstages", C.c_int32), ("method_visc", C.c_int32), ("botfr", C.c_int32),
+        ("max_shear_dz", C.c_double), ("shear_corrector", C.c_int32), ("reserved", C.c_int32),
     ]
 
 
@@ -128,5 +129,6 @@ class Descriptors:
             setattr(s, name, ptr(self.keep["s_" + name]))
         p = Params(dt=S["dt"], dt_btp=S["dt_btp"], visc_mlswe=S["visc"], cd_mlswe=S["cd"],
                    ad_mlswe=S["ad"], gravity=S["gravity"], N_btp=S["N_btp"], kstages=S["kstages"],
-                   method_visc=S["method_visc"], botfr=S["botfr"])
+                   method_visc=S["method_visc"], botfr=S["botfr"],
+                   max_shear_dz=S["max_shear_dz"], shear_corrector=S["shear_corrector"])
         self.mesh, self.statics, self.params = m, s, p

@@ -57,7 +57,7 @@ FIELDS = [
     ("sum_layer_mass_flux_face", "2,nq,nface"),
 ]
 
-MODES = {"rhs": 1, "btp": 2, "step": 3}
+MODES = {"rhs": 1, "btp": 2, "step": 3, "predict": 4}
 
 
 def dims(case) -> dict:
@@ -79,7 +79,7 @@ def write_bundle(path: str, case, mode: str, nsteps: int = 1, metrics: bool = Fa
     hi[:14] = [S["nelem"], S["npoin"], S["npoin_q"], S["nface"], S["ngl"], S["nq"], S["nlayers"],
                S["ngl"] - 1, S["kstages"], S["N_btp"], S["method_visc"], S["botfr"], nsteps, MODES[mode]]
     hd = np.zeros(8, dtype="<f8")
-    hd[:6] = [S["dt"], S["dt_btp"], S["visc"], S["cd"], S["ad"], S["gravity"]]
+    hd[:7] = [S["dt"], S["dt_btp"], S["visc"], S["cd"], S["ad"], S["gravity"], S["max_shear_dz"]]
     with open(path, "wb") as fh:
         fh.write(hi.tobytes())
         fh.write(hd.tobytes())

@@ -65,6 +65,16 @@ CONFIGS = {
     "dg8L3q": dict(test_case="double-gyre-3", nelx=8, nely=8, nop=4, nlayers=3,
                    xdims=(0.0, 2.0e6), ydims=(0.0, 2.0e6), dt=500.0, dt_btp=25.0,
                    method_visc=1, visc=50.0, botfr=1, cd=1.0e-7, f0=0.93e-4, beta=2.0e-11),
+    # ad_mlswe > 0 (implicit vertical shear stress between the layers):
+    # not in a shipped namelist; A_D = 1e-2 m^2/s, max_shear_dz 10 m / 50 m
+    "bump10s": dict(test_case="bump", nelx=10, nely=10, nop=4, nlayers=2,
+                    xdims=(0.0, 2000.0), ydims=(0.0, 2000.0), dt=100.0, dt_btp=1.8,
+                    method_visc=0, visc=0.0, botfr=0, cd=0.0, f0=0.0, beta=0.0,
+                    ad_mlswe=1.0e-2, max_shear_dz=10.0),
+    "dg8L3s": dict(test_case="double-gyre-3", nelx=8, nely=8, nop=4, nlayers=3,
+                   xdims=(0.0, 2.0e6), ydims=(0.0, 2.0e6), dt=500.0, dt_btp=25.0,
+                   method_visc=3, visc=50.0, botfr=1, cd=1.0e-7, f0=0.93e-4, beta=2.0e-11,
+                   ad_mlswe=1.0e-2, max_shear_dz=50.0),
     # C4: ~1e5 elements, dt scaled for CFL
     "dg316L3": dict(test_case="double-gyre-3", nelx=316, nely=316, nop=4, nlayers=3,
                     xdims=(0.0, 2.0e6), ydims=(0.0, 2.0e6), dt=40.0, dt_btp=2.0,
@@ -76,6 +86,8 @@ def make_config(name: str, **overrides) -> dict:
     cfg = dict(CONFIGS[name])
     cfg.setdefault("kstages", 5)
     cfg.setdefault("ad_mlswe", 0.0)
+    cfg.setdefault("max_shear_dz", 0.0)     # mod_input.F90:127
+    cfg.setdefault("shear_corrector", 0)    # HNUMO_SHEAR_CORRECTOR_REFERENCE (include/hnumo_engine.h)
     cfg.setdefault("x_boundary", (4, 4))
     cfg.setdefault("y_boundary", (4, 4))
     cfg["name"] = name
@@ -351,7 +363,8 @@ def build_case(cfg: dict, dense: bool = True) -> Case:
     S = dict(nelem=nelem, npoin=npoin, npoin_q=npoin_q, nface=nface, ngl=ngl, nq=nq, nlayers=L,
              kstages=cfg["kstages"], N_btp=N_btp, dt=dt, dt_btp=dt_btp,
              method_visc=cfg["method_visc"], visc=float(cfg["visc"]), botfr=cfg["botfr"],
-             cd=float(cfg["cd"]), ad=float(cfg["ad_mlswe"]), gravity=g)
+             cd=float(cfg["cd"]), ad=float(cfg["ad_mlswe"]), gravity=g,
+             max_shear_dz=float(cfg["max_shear_dz"]), shear_corrector=int(cfg["shear_corrector"]))
     return Case(cfg=cfg, basis=basis, mesh=mesh, arrays=A, scalars=S)
 
 

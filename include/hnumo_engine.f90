@@ -15,6 +15,8 @@ module hnumo_engine_c
 
     integer(c_int), parameter, public :: HNUMO_OK = 0, HNUMO_ERR_NEGATIVE_THICKNESS = 1, &
         HNUMO_ERR_NONFINITE = 2, HNUMO_ERR_DEVICE = 3, HNUMO_ERR_INVALID = 4
+    integer(c_int32_t), parameter, public :: HNUMO_SHEAR_CORRECTOR_REFERENCE = 0, &
+        HNUMO_SHEAR_CORRECTOR_PREDICTED = 1
     integer(c_int), parameter, public :: HNUMO_ABI_EXPECTED = 3   ! must equal hnumo_abi_version()
     integer(c_int), parameter, public :: HNUMO_SUM_REFERENCE = 0, HNUMO_SUM_FACTORED = 1
 
@@ -63,6 +65,8 @@ module hnumo_engine_c
         real(c_double) :: dt = 0, dt_btp = 0
         real(c_double) :: visc_mlswe = 0, cd_mlswe = 0, ad_mlswe = 0, gravity = 0
         integer(c_int32_t) :: N_btp = 0, kstages = 0, method_visc = 0, botfr = 0
+        real(c_double) :: max_shear_dz = 0
+        integer(c_int32_t) :: shear_corrector = 0, reserved = 0
     end type hnumo_params
 
     ! = hnumo_halo_desc (mod_parallel)

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define HNUMO_ABI_VERSION 3
+#define HNUMO_ABI_VERSION 4
 
 enum {
   HNUMO_OK = 0,
@@ -114,7 +114,23 @@ typedef struct hnumo_params {
   double dt, dt_btp;                    /* dt_btp = dt/N_btp (mod_initial.F90:176-177) */
   double visc_mlswe, cd_mlswe, ad_mlswe, gravity;
   int32_t N_btp, kstages, method_visc, botfr;
+  /* ad_mlswe > 0 (implicit vertical shear stress, rhs_layer_shear_stress,
+   * mod_create_rhs_mlswe.F90:146-279): mod_input max_shear_dz (mod_input.F90:127).      */
+  double max_shear_dz;
+  /* What the corrector's shear-stress call reads (mod_splitting.F90:158).  The reference
+   * passes its never-assigned local `uv` (:119) there; under the reference build's
+   * -finit-real=zero (config.user:25) that is all zeros, so dp = 0, the solve divides
+   * 0/0 and the corrector's layer momenta become NaN (the engine then returns
+   * HNUMO_ERR_NONFINITE).
+   *   HNUMO_SHEAR_CORRECTOR_REFERENCE (0, default): exactly that.
+   *   HNUMO_SHEAR_CORRECTOR_PREDICTED (1): the Coriolis-rotated, velocity-smoothed
+   *     momenta q_df3, as momentum_mass passes them at :265 (the evident intent).       */
+  int32_t shear_corrector;
+  int32_t reserved;
 } hnumo_params;
+
+#define HNUMO_SHEAR_CORRECTOR_REFERENCE 0
+#define HNUMO_SHEAR_CORRECTOR_PREDICTED 1
 
 /* Multi-rank description.  The reference partitions with processor faces (face(8)=0)
  * and exchanges face traces per neighbour (mod_parallel num_nbh / nbh_proc /

@@ -1500,20 +1500,138 @@ static int check_thickness(oracle *o, const double *q) {
   return 0;
 }
 
-/* momentum update + implicit Coriolis (mod_splitting.F90:131-175 / :239-282) */
-static void momentum_update(oracle *o, double *q, const double *rhs_mom) {
+/* velocity_df (mod_layer_terms.F90:139-196): layer momenta made consistent with the
+ * barotropic velocity, q(2:3) <- u_k dp_k (the arithmetic of extract_velocity) */
+static void velocity_df(oracle *o, double *q, const double *qb) {
+  const int npoin = o->npoin, L = o->L;
+  double *uv = zalloc(2 * (size_t)npoin * L);
+  extract_velocity(o, uv, q, qb);
+  for (int k = 1; k <= L; k++)
+    for (int I = 1; I <= npoin; I++) {
+      A3(q, 2, I, k, 3, npoin) = A3(uv, 1, I, k, 2, npoin) * A3(q, 1, I, k, 3, npoin);
+      A3(q, 3, I, k, 3, npoin) = A3(uv, 2, I, k, 2, npoin) * A3(q, 1, I, k, 3, npoin);
+    }
+  free(uv);
+}
+
+/* rhs_layer_shear_stress (mod_create_rhs_mlswe.F90:146-279): per quad point the implicit
+ * vertical shear-stress system over the layers (tridiagonal; sub-diagonal -coeff,
+ * super-diagonal -coeff1, as written), the interface stresses and their weak form.
+ * tau(nlayers+1) is never assigned in the reference (:160,:246-251): zero, as under the
+ * reference build's -finit-real=zero. */
+static void rhs_layer_shear_stress(oracle *o, double *rs, const double *q) {
+  const int npts = o->npts, npoin = o->npoin, L = o->L;
+  const hnumo_mesh_desc *m = &o->m;
+  const double g = o->p.gravity, ad = o->p.ad_mlswe, dt = o->p.dt, al1 = o->s.alpha[0];
+  double dp[3], udp[3], vdp[3], a[3], b[3], c[3], r[2][3], uv[2][3], tu[4], tv[4];
+  memset(rs, 0, sizeof(double) * 2 * (size_t)npoin * L);
+  for (int Iq = 1; Iq <= o->npoin_q; Iq++) {
+    for (int k = 0; k < L; k++) dp[k] = udp[k] = vdp[k] = 0.0;
+    for (int ip = 1; ip <= npts; ip++) {
+      int I = A2(m->indexq, ip, Iq, npts);
+      double hi = A2(m->psih, ip, Iq, npts);
+      for (int k = 0; k < L; k++) {
+        dp[k] = dp[k] + hi * A3(q, 1, I, k + 1, 3, npoin);
+        udp[k] = udp[k] + hi * A3(q, 2, I, k + 1, 3, npoin);
+        vdp[k] = vdp[k] + hi * A3(q, 3, I, k + 1, 3, npoin);
+      }
+    }
+    /* Fortran MAX as gfortran evaluates it: the second argument if larger or the first is NaN */
+    double coeff = sqrt(0.5 * o->s.coriolis_quad[Iq - 1] * ad) / al1;
+    const double c2 = ad / (al1 * o->p.max_shear_dz);
+    if (c2 > coeff || isnan(coeff)) coeff = c2;
+    const double coeff1 = g * dt * coeff;
+    for (int k = 0; k < L; k++) {
+      a[k] = -coeff;
+      b[k] = dp[k] + 2.0 * coeff1;
+      c[k] = -coeff1;
+      r[0][k] = udp[k] / dp[k];
+      r[1][k] = vdp[k] / dp[k];
+    }
+    b[0] = dp[0] + coeff1;
+    b[L - 1] = dp[L - 1] + coeff1;
+    a[0] = 0.0;
+    c[L - 1] = 0.0;
+    for (int k = 1; k < L; k++) {
+      const double mult = a[k] / b[k - 1];
+      b[k] = b[k] - mult * c[k - 1];
+      r[0][k] = r[0][k] - mult * r[0][k - 1];
+      r[1][k] = r[1][k] - mult * r[1][k - 1];
+    }
+    r[0][L - 1] = r[0][L - 1] / b[L - 1];
+    r[1][L - 1] = r[1][L - 1] / b[L - 1];
+    uv[0][L - 1] = r[0][L - 1];
+    uv[1][L - 1] = r[1][L - 1];
+    for (int k = L - 2; k >= 0; k--) {
+      r[0][k] = (r[0][k] - c[k] * r[0][k + 1]) / b[k];
+      r[1][k] = (r[1][k] - c[k] * r[1][k + 1]) / b[k];
+      uv[0][k] = r[0][k];
+      uv[1][k] = r[1][k];
+    }
+    tu[0] = tv[0] = 0.0;
+    for (int k = 1; k < L; k++) {
+      tu[k] = coeff * (uv[0][k - 1] - uv[0][k]);
+      tv[k] = coeff * (uv[1][k - 1] - uv[1][k]);
+    }
+    tu[L] = tv[L] = 0.0;
+    const double wq = m->wjac[Iq - 1];
+    for (int k = 0; k < L; k++) {
+      const double tuq = g * (tu[k] - tu[k + 1]), tvq = g * (tv[k] - tv[k + 1]);
+      for (int ip = 1; ip <= npts; ip++) {
+        int I = A2(m->indexq, ip, Iq, npts);
+        double hi = A2(m->psih, ip, Iq, npts);
+        A3(rs, 1, I, k + 1, 2, npoin) = A3(rs, 1, I, k + 1, 2, npoin) + wq * hi * tuq;
+        A3(rs, 2, I, k + 1, 2, npoin) = A3(rs, 2, I, k + 1, 2, npoin) + wq * hi * tvq;
+      }
+    }
+  }
+}
+
+/* momentum update (mod_splitting.F90:131-175 / :239-282): q_df_temp = q + dt*rhs_mom; with
+ * ad_mlswe > 0 the implicit vertical shear stress (:140-164 / :248-271); then the implicit
+ * Coriolis rotation and the wall fix.  corrector != 0: the momentum() call, whose
+ * shear-stress input is its never-assigned `uv` (:119,:158) -- zeros, unless
+ * shear_corrector selects q_df3 (include/hnumo_engine.h, hnumo_params). */
+static void momentum_update(oracle *o, double *q, const double *rhs_mom, const double *qb, int corrector) {
   const int npoin = o->npoin, L = o->L;
   const double dt = o->p.dt;
   const double *f2 = o->s.fdt2_bcl, *a = o->s.a_bcl, *b = o->s.b_bcl;
+  double *tmp = zalloc(2 * (size_t)npoin * L);
   for (int k = 1; k <= L; k++)
     for (int I = 1; I <= npoin; I++) {
-      double t1 = A3(q, 2, I, k, 3, npoin) + dt * A3(rhs_mom, 1, I, k, 2, npoin);
-      double t2 = A3(q, 3, I, k, 3, npoin) + dt * A3(rhs_mom, 2, I, k, 2, npoin);
-      double tu = t1 + f2[I - 1] * A3(q, 3, I, k, 3, npoin);
-      double tv = t2 - f2[I - 1] * A3(q, 2, I, k, 3, npoin);
+      A3(tmp, 1, I, k, 2, npoin) = A3(q, 2, I, k, 3, npoin) + dt * A3(rhs_mom, 1, I, k, 2, npoin);
+      A3(tmp, 2, I, k, 2, npoin) = A3(q, 3, I, k, 3, npoin) + dt * A3(rhs_mom, 2, I, k, 2, npoin);
+    }
+  if (o->p.ad_mlswe > 0.0) {
+    double *q3 = zalloc(3 * (size_t)npoin * L), *rs = zalloc(2 * (size_t)npoin * L);
+    for (int k = 1; k <= L; k++)
+      for (int I = 1; I <= npoin; I++) {
+        double tu = A3(tmp, 1, I, k, 2, npoin) + f2[I - 1] * A3(q, 3, I, k, 3, npoin);
+        double tv = A3(tmp, 2, I, k, 2, npoin) - f2[I - 1] * A3(q, 2, I, k, 3, npoin);
+        A3(q3, 1, I, k, 3, npoin) = A3(q, 1, I, k, 3, npoin);
+        A3(q3, 2, I, k, 3, npoin) = a[I - 1] * tu + b[I - 1] * tv;
+        A3(q3, 3, I, k, 3, npoin) = -b[I - 1] * tu + a[I - 1] * tv;
+      }
+    velocity_df(o, q3, qb);
+    if (corrector && o->p.shear_corrector != HNUMO_SHEAR_CORRECTOR_PREDICTED)
+      memset(q3, 0, sizeof(double) * 3 * (size_t)npoin * L);
+    rhs_layer_shear_stress(o, rs, q3);
+    for (int k = 1; k <= L; k++)
+      for (int I = 1; I <= npoin; I++) {
+        A3(tmp, 1, I, k, 2, npoin) = A3(tmp, 1, I, k, 2, npoin) + dt * (o->m.massinv[I - 1] * A3(rs, 1, I, k, 2, npoin));
+        A3(tmp, 2, I, k, 2, npoin) = A3(tmp, 2, I, k, 2, npoin) + dt * (o->m.massinv[I - 1] * A3(rs, 2, I, k, 2, npoin));
+      }
+    free(q3);
+    free(rs);
+  }
+  for (int k = 1; k <= L; k++)
+    for (int I = 1; I <= npoin; I++) {
+      double tu = A3(tmp, 1, I, k, 2, npoin) + f2[I - 1] * A3(q, 3, I, k, 3, npoin);
+      double tv = A3(tmp, 2, I, k, 2, npoin) - f2[I - 1] * A3(q, 2, I, k, 3, npoin);
       A3(q, 2, I, k, 3, npoin) = a[I - 1] * tu + b[I - 1] * tv;
       A3(q, 3, I, k, 3, npoin) = -b[I - 1] * tu + a[I - 1] * tv;
     }
+  free(tmp);
   layer_mom_boundary(o, q);
 }
 
@@ -1529,7 +1647,7 @@ static int momentum_mass(oracle *o, double *q, double *qf, double *qp, const dou
   if (!rc) {
     apply_consistency(o, q);
     rhs_momentum(o, rhs_mom, qp, q, qf);
-    momentum_update(o, q, rhs_mom);
+    momentum_update(o, q, rhs_mom, qb, 0);
     evaluate_bcl(o, qf, q, qp, qb, 0);
   }
   free(adv);
@@ -1581,7 +1699,7 @@ static void momentum(oracle *o, double *q, double *qp, const double *qb, const d
   const int npoin = o->npoin, L = o->L;
   double *rhs_mom = zalloc(2 * (size_t)npoin * L);
   rhs_momentum(o, rhs_mom, qp, q, qf);
-  momentum_update(o, q, rhs_mom);
+  momentum_update(o, q, rhs_mom, qb, 1);
   evaluate_bcl(o, NULL, q, qp, qb, 1);
   free(rhs_mom);
 }
@@ -1662,6 +1780,20 @@ int oracle_create_rhs_btp(oracle *o, double *rhs, const double *qb_df, const dou
   return 0;
 }
 
+/* The prediction half of ti_rk_bcl (ti_rk_bcl.F90:43-57) in place: q_df, qb_df, qprime_df
+ * become q_df2, qbp_df, qprime_df2 -- the parity hook for momentum_mass (and through it the
+ * ad_mlswe > 0 shear stress), whose reference counterpart is oracle/ref_driver mode 4. */
+int oracle_predict(oracle *o, double *q_df, double *qb_df, double *qprime_df) {
+  double *qf = zalloc(6 * (size_t)o->ngl * o->nface * o->L);
+  extract_qprime_df_face(o, qf, qprime_df);
+  set_dpprime_visc(o, qprime_df);
+  btp_bcl_coeffs(o, qf, qprime_df);
+  ti_barotropic_ssprk(o, qb_df, qprime_df);
+  int rc = momentum_mass(o, q_df, qf, qprime_df, qb_df);
+  free(qf);
+  return rc;
+}
+
 void oracle_zero_accumulators(oracle *o) { zero_btp_accumulators(o); }
 
 const char *oracle_last_error(const oracle *o) { return o->err; }
@@ -1719,7 +1851,6 @@ int oracle_create(const hnumo_mesh_desc *m, const hnumo_static_desc *s, const hn
   o->L = m->nlayers;
   if (p->method_visc == 1 && (!m->imapl_q || !m->imapr_q))
     return set_err(o, HNUMO_ERR_INVALID, "method_visc==1 needs imapl_q/imapr_q");
-  if (p->ad_mlswe > 0.0) return set_err(o, HNUMO_ERR_INVALID, "ad_mlswe>0 not supported");
   if (o->L < 1 || o->L > 3) return set_err(o, HNUMO_ERR_INVALID, "nlayers must be 1..3 (qp(k) quirk)");
   if (o->nq > 32 || !m->psih || !m->index_df) return set_err(o, HNUMO_ERR_INVALID, "dense tables required");
   size_t Nq = (size_t)o->npoin_q, N = (size_t)o->npoin, nqf = (size_t)o->nq * o->nface;

@@ -35,6 +35,7 @@ def lib():
         vp, dp = C.c_void_p, C.POINTER(C.c_double)
         L.oracle_create.argtypes = [vp, vp, vp, C.POINTER(vp)]
         L.oracle_ti_rk_bcl.argtypes = [vp, dp, dp, dp]
+        L.oracle_predict.argtypes = [vp, dp, dp, dp]
         L.oracle_ti_barotropic_ssprk.argtypes = [vp, dp, dp]
         L.oracle_btp_bcl_coeffs.argtypes = [vp, dp]
         L.oracle_create_rhs_btp.argtypes = [vp, dp, dp, dp]
@@ -77,6 +78,10 @@ class Oracle:
 
     def ti_rk_bcl(self, q, qb, qp):
         self._check(lib().oracle_ti_rk_bcl(self.h, _dp(q), _dp(qb), _dp(qp)))
+
+    def predict(self, q, qb, qp):
+        """The prediction half of ti_rk_bcl (ti_rk_bcl.F90:43-57) in place (momentum_mass hook)."""
+        self._check(lib().oracle_predict(self.h, _dp(q), _dp(qb), _dp(qp)))
 
     def btp_bcl_coeffs(self, qp):
         self._check(lib().oracle_btp_bcl_coeffs(self.h, _dp(qp)))

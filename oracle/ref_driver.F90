@@ -23,7 +23,7 @@ program ref_driver
     use mpi
     use mod_input, only: nopx, nopy, nopz, nlayers, dt, dt_btp, kstages, method_visc, &
         visc_mlswe, botfr, cd_mlswe, ad_mlswe, space_method, is_mlswe, dg_integ_exact, &
-        ti_method_btp, is_non_conforming_flg
+        ti_method_btp, is_non_conforming_flg, max_shear_dz
     use mod_basis, only: mod_basis_create, ngl, nq, npts, psiq, dpsiq, psi, dpsi, xgl, wgl, xnq, wnq
     use mod_grid, only: mod_grid_init_unified, npoin, npoin_q, nelem, nface, nboun, face, &
         npoin_cg, nbsido, nNC, face_type
@@ -57,6 +57,7 @@ program ref_driver
     use mod_rhs_btp, only: create_rhs_btp
     use mod_barotropic_terms, only: btp_bcl_coeffs_qdf
     use mod_layer_terms, only: extract_qprime_df_face, interpolate_dpp
+    use mod_splitting, only: momentum_mass
 
     implicit none
 
@@ -88,7 +89,7 @@ program ref_driver
     dt = hd(1); dt_btp = hd(2); visc_mlswe = hd(3); cd_mlswe = hd(4); ad_mlswe = hd(5)
     space_method = 'dg'; is_mlswe = .true.; dg_integ_exact = .true.; ti_method_btp = 'rk35'
     is_non_conforming_flg = 0
-    gravity = hd(6)
+    gravity = hd(6); max_shear_dz = hd(7)
 
     ! ---- mod_basis: the reference builds its own LGL tables (mod_basis.F90:60-186)
     call mod_basis_create(nopx, nopy, nopz)
@@ -219,6 +220,16 @@ program ref_driver
         t1 = mpi_wtime()
         write(*, '(A,ES24.16)') 'REF_TIME ', t1 - t0
 #endif
+    case (4)
+        ! the prediction half of ti_rk_bcl (ti_rk_bcl.F90:43-57), outputs q_df2, qbp_df,
+        ! qprime_df2: pins momentum_mass (with ad_mlswe > 0, the vertical shear stress)
+        allocate(qf(3, 2, ngl, nface, nlayers))
+        call extract_qprime_df_face(qf, qprime_df)
+        dpprime_visc(:, :) = qprime_df(1, :, :)
+        if (method_visc == 1) call interpolate_dpp(dpprime_visc_q, dpprime_visc)
+        call btp_bcl_coeffs_qdf(qf, qprime_df)
+        call ti_barotropic_ssprk_mlswe(qb_df, qprime_df)
+        call momentum_mass(q_df, qf, qprime_df, qb_df)
     case default
         stop 'unknown mode'
     end select

@@ -118,6 +118,45 @@ def test_bitwise_step(cfg, case_factory, engines):
         assert np.array_equal(e.field(f), o.field(f)), f
 
 
+@pytest.mark.parametrize("cfg", ["bump10s", "dg8L3s"])
+def test_shear_stress_bitwise(cfg, case_factory):
+    """ad_mlswe > 0 (implicit vertical shear stress, mod_create_rhs_mlswe.F90:146-279, fused into
+    mom_elem_kernel) with the corrector reading the predicted momenta
+    (HNUMO_SHEAR_CORRECTOR_PREDICTED): engine == oracle bit for bit over 2 steps."""
+    import oracle as O
+    from hnumo.engine import Engine
+    case = case_factory(cfg, shear_corrector=1)
+    o = O.Oracle(case)
+    e = Engine(case)
+    q, qb, qp = o.state()
+    qe, qbe, qpe = e.state()
+    for _ in range(2):
+        o.ti_rk_bcl(q, qb, qp)
+        e.ti_rk_bcl(qe, qbe, qpe)
+    assert np.isfinite(q).all()
+    assert np.array_equal(qe, q) and np.array_equal(qbe, qb) and np.array_equal(qpe, qp)
+    e.close()
+
+
+def test_shear_stress_reference_corrector_is_nonfinite(case_factory):
+    """ad_mlswe > 0 with the default HNUMO_SHEAR_CORRECTOR_REFERENCE: momentum() hands
+    rhs_layer_shear_stress its never-assigned `uv` (mod_splitting.F90:119,158), zeros under
+    the reference build's -finit-real=zero, so the solve divides 0/0 and the corrector's layer
+    momenta are NaN in the oracle; the engine reports it as HNUMO_ERR_NONFINITE."""
+    import oracle as O
+    from hnumo.engine import Engine, EngineError
+    case = case_factory("bump10s")
+    o = O.Oracle(case)
+    q, qb, qp = o.state()
+    o.ti_rk_bcl(q, qb, qp)
+    assert np.isnan(q[1:]).any() and np.isfinite(qb).all()
+    e = Engine(case)
+    with pytest.raises(EngineError) as ei:
+        e.ti_rk_bcl(*e.state())
+    assert ei.value.code == 2
+    e.close()
+
+
 @pytest.mark.parametrize("name", ["bump10_step2", "lake10_step1", "dg25_step1", "dg25L3_step1", "bump10q_step1",
                                   "dg8L3q_step1"])
 def test_engine_matches_reference_golden(name, case_factory, engines):

@@ -89,6 +89,47 @@ def test_oracle_matches_reference_fortran(variant):
         assert np.array_equal(a, ref[k]), k
 
 
+@pytest.mark.ref
+@pytest.mark.parametrize("name", ["bump10s", "dg8L3s"])
+def test_shear_predictor_vs_reference_fortran(name, case_factory):
+    """ad_mlswe > 0: the predictor (momentum_mass with the implicit vertical shear stress,
+    mod_splitting.F90:182-287) against the reference Fortran (ref_driver mode 4).  Layer
+    thicknesses and the barotropic state are bitwise equal.  The layer momenta differ by a
+    spatially uniform velocity offset per layer: rhs_layer_shear_stress reads tau_u(nlayers+1),
+    which it never assigns (mod_create_rhs_mlswe.F90:160,246-258).  The oracle takes it as zero
+    (the reference build's -finit-real=zero); the harness compiled here
+    (amdflang, no zero-init) reads a stale stack value -- one constant per run, a uniform
+    bottom-layer stress that evaluate_bcl then spreads over the layers.  Asserted: that offset
+    is uniform over the interior nodes.  (The engine == oracle bitwise on this branch:
+    tests/test_engine_gpu.py::test_shear_stress_bitwise.)"""
+    import oracle as O
+    case = case_factory(name)
+    ref = O.run_reference(case, "predict", 1)
+    o = O.Oracle(case)
+    q, qb, qp = o.state()
+    o.predict(q, qb, qp)
+    assert np.array_equal(qb, ref["qb_df"])
+    assert np.array_equal(q[0], ref["q_df"][0]) and np.array_equal(qp[0], ref["qprime_df"][0])
+    for k in range(case.scalars["nlayers"]):
+        du = ref["q_df"][1, :, k] / ref["q_df"][0, :, k] - q[1, :, k] / q[0, :, k]
+        med = np.median(du)
+        assert med != 0.0
+        assert np.mean(np.abs(du - med) <= 0.02 * abs(med)) > 0.9, k
+
+
+def test_shear_branch_is_live(case_factory):
+    """ad_mlswe > 0 changes the predicted layer momenta (and only them)."""
+    import oracle as O
+    out = []
+    for ad in (1.0e-2, 0.0):
+        o = O.Oracle(case_factory("bump10s", ad_mlswe=ad))
+        q, qb, qp = o.state()
+        o.predict(q, qb, qp)
+        out.append((q.copy(), qb.copy()))
+    assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][0][0], out[1][0][0])
+    assert not np.array_equal(out[0][0][1:], out[1][0][1:])
+
+
 def test_bump_mass_conservation(case_factory):
     """The reference's only CI assertion: per-layer mass loss <= 1e-12 (CI/bump/check.F90:58)."""
     import oracle as O
