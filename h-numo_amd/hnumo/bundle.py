@@ -57,7 +57,7 @@ FIELDS = [
     ("sum_layer_mass_flux_face", "2,nq,nface"),
 ]
 
-MODES = {"rhs": 1, "btp": 2, "step": 3, "predict": 4}
+MODES = {"rhs": 1, "btp": 2, "step": 3, "predict": 4, "diag": 5}
 
 
 def dims(case) -> dict:
@@ -83,7 +83,8 @@ def write_bundle(path: str, case, mode: str, nsteps: int = 1, metrics: bool = Fa
     with open(path, "wb") as fh:
         fh.write(hi.tobytes())
         fh.write(hd.tobytes())
-        for name, dt, shp in BUNDLE_ARRAYS + (METRIC_ARRAYS if metrics else []):
+        trailer = (METRIC_ARRAYS if metrics else []) + ([("coord", "f8", "3,npoin")] if mode == "diag" else [])
+        for name, dt, shp in BUNDLE_ARRAYS + trailer:
             a = np.asarray(case.arrays[name])
             want = shape_of(shp, d)
             assert a.size == int(np.prod(want)), (name, a.shape, want)

@@ -134,6 +134,7 @@ def run_reference(case, mode: str, nsteps: int = 1, workdir: str | None = None, 
     if r.returncode != 0:
         raise RuntimeError(f"{os.path.basename(driver)} failed ({r.returncode}): {r.stdout[-2000:]} {r.stderr[-2000:]}")
     out = _bundle.read_outputs(fout, case, mode)
+    out["stdout"] = r.stdout
     if workdir is None:
         for f in (fin, fout):
             os.remove(f)

@@ -58,10 +58,18 @@ program ref_driver
     use mod_barotropic_terms, only: btp_bcl_coeffs_qdf
     use mod_layer_terms, only: extract_qprime_df_face, interpolate_dpp
     use mod_splitting, only: momentum_mass
+    use mod_grid, only: coord
+    use mod_global_grid, only: npoin_g
+    use mod_parallel, only: nproc, npoin_l, npoin_l_max
+    use mod_mpi_utilities, only: irank
+    use mod_input, only: lcheck_conserved
 
     implicit none
 
-    integer :: hi(16), ierr, u, nsteps, mode, istep, k
+    integer :: hi(16), ierr, u, nsteps, mode, istep, k, ip, I1
+    real(8), allocatable :: qout(:,:,:), mass0(:)
+    character(len=18) :: fnp11
+    character(len=3) :: s_layers
     real(8) :: t0, t1
     real(8) :: hd(8)
     character(len=512) :: fin, fout
@@ -139,6 +147,12 @@ program ref_driver
     psih_df = 0
     read(u) psih; read(u) dpsidx; read(u) dpsidy; read(u) wjac
     read(u) dpsidx_df; read(u) dpsidy_df; read(u) wjac_df
+    ! psih_df at the LGL nodes is the identity (read only by compute_conserved)
+    do I1 = 1, npoin
+        do ip = 1, npts
+            if (index_df(ip, I1) == I1) psih_df(ip, I1) = 1
+        end do
+    end do
     allocate(pbprime(npoin_q), pbprime_df(npoin), one_over_pbprime(npoin_q), one_over_pbprime_df(npoin))
     allocate(pbprime_face(2, nq, nface), pbprime_df_face(2, ngl, nface), one_over_pbprime_edge(nq, nface))
     allocate(coeff_pbpert_L(nq, nface), coeff_pbpert_R(nq, nface), coeff_pbub_LR(nq, nface))
@@ -168,6 +182,14 @@ program ref_driver
     read(u) ksiq_x; read(u) ksiq_y; read(u) etaq_x; read(u) etaq_y; read(u) jacq
     read(u) ksi_x; read(u) ksi_y; read(u) eta_x; read(u) eta_y; read(u) jac
 #endif
+    if (mode == 5) then
+        ! mode 5 trailer: the node coordinates (mod_grid coord, read by courant_mlswe), and the
+        ! single-rank gather plumbing of diagnostics / print_diagnostics_mlswe
+        read(u) coord
+        nproc = 1; irank = 0; npoin_g = npoin; npoin_l_max = npoin
+        allocate(npoin_l(1)); npoin_l(1) = npoin
+        lcheck_conserved = .true.
+    end if
     close(u)
     rhs = 0
 
@@ -230,6 +252,25 @@ program ref_driver
         call btp_bcl_coeffs_qdf(qf, qprime_df)
         call ti_barotropic_ssprk_mlswe(qb_df, qprime_df)
         call momentum_mass(q_df, qf, qprime_df, qb_df)
+    case (5)
+        ! the diagnostics of the time loop (mod_time_loop.F90:150-186, :257-268): initial layer
+        ! masses, nsteps of ti_rk_bcl, then print_diagnostics_mlswe with idone = 0 (stdout
+        ! report + mass_mlswe.cons line) and idone = 1 (final report + mlswe_FIN.txt)
+        allocate(qout(5, npoin, nlayers), mass0(nlayers))
+        call diagnostics(qout, q_df, qb_df, 0, 1)
+        do k = 1, nlayers
+            call compute_conserved(mass0(k), qout(1, :, k))
+        end do
+        do istep = 1, nsteps
+            call ti_rk_bcl(q_df, qb_df, qprime_df)
+        end do
+        call diagnostics(qout, q_df, qb_df, nsteps, 1)
+        write(s_layers, '(i3)') nlayers
+        fnp11 = '(i8,' // trim(adjustl(s_layers)) // '(e16.8,1x))'
+        open(unit=111, file='mass_mlswe.cons')
+        call print_diagnostics_mlswe(qout, qb_df, dt*nsteps, nsteps, dt, 0, mass0, nsteps, fnp11, 111)
+        close(111)
+        call print_diagnostics_mlswe(qout, qb_df, dt*nsteps, nsteps, dt, 1, mass0, nsteps, fnp11, 111)
     case default
         stop 'unknown mode'
     end select

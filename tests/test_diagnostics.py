@@ -61,6 +61,29 @@ def test_ci_check_on_reference_files():
     assert 1e-5 < rep[1]["h"][0] < 1e-2
 
 
+@pytest.mark.ref
+@pytest.mark.parametrize("name", ["bump10", "dg8L3q"])
+def test_diagnostics_match_reference_fortran(name, case_factory, tmp_path):
+    """The reference's own diagnostics (diagnostics.F90, compute_conserved.F90, courant.F90,
+    print_diagnostics.F90, run by oracle/_ref/ref_driver mode 5 after 2 steps) against
+    hnumo/diagnostics.py on the same state: the stdout reports (idone 0 and 1), the
+    mass_mlswe.cons line and mlswe_FIN.txt are identical byte for byte."""
+    import oracle as O
+    case = case_factory(name)
+    ref = O.run_reference(case, "diag", 2, workdir=str(tmp_path))
+    L = case.scalars["nlayers"]
+    qf0 = D.layer_fields(case, case.arrays["q_df"])
+    mass0 = [D.conserved_mass(case, qf0[0, :, k]) for k in range(L)]
+    qf = D.layer_fields(case, ref["q_df"])
+    t = 2 * case.scalars["dt"]
+    text0, cons, _ = D.print_diagnostics(case, qf, ref["qb_df"], t, 2, 0, mass0)
+    text1, _, fin = D.print_diagnostics(case, qf, ref["qb_df"], t, 2, 1, mass0)
+    out = ref["stdout"]
+    assert out[out.index(" =====") - 1:].lstrip("\n") == text0 + text1
+    assert (tmp_path / "mass_mlswe.cons").read_text() == cons + "\n"
+    assert (tmp_path / "mlswe_FIN.txt").read_text() == fin
+
+
 def test_conserved_mass_matches_layer_mass(case_factory):
     case = case_factory("bump10")
     q = case.arrays["q_df"]
