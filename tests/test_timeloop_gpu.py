@@ -2,8 +2,8 @@
 layers, dt 100 s, dt_btp 1.8 s, 10800 s = 108 baroclinic steps) through the time loop of
 hnumo/diagnostics.py (mod_time_loop.F90), checked as CI/bump/check.F90 checks the reference:
 per-layer mass loss <= 1e-12.  The h/u/v extrema are compared with the reference's own FIN
-files (tests/golden/*_mlswe_FIN.txt); those three files disagree with each other at the
-1e-3 level, so the comparison is reported, and bounded loosely."""
+files (tests/golden/*_mlswe_FIN.txt): the CI's file is matched to 1e-6 relative; the two
+Examples/ files disagree with it at the 1e-2 level and are only reported."""
 import io
 import os
 
@@ -24,11 +24,13 @@ def test_bump_ci_on_engine(case_factory, tmp_path):
     e.close()
     fin = (tmp_path / "mlswe_FIN.txt").read_text()
     print(fin)
-    best = None
+    worst = {}
     for name in FINS:
         ok, rep = D.ci_check(fin, open(os.path.join(GOLD, name)).read())
         assert ok, rep                                 # check.F90:58: mass loss <= 1e-12
-        worst = max(max(v) for r in rep.values() for k, v in r.items() if k != "mass_loss")
-        print(name, "max relative difference of the h/u/v extrema: %.3e" % worst)
-        best = worst if best is None else min(best, worst)
-    assert best < 0.1
+        worst[name] = max(max(v) for r in rep.values() for k, v in r.items() if k != "mass_loss")
+        print(name, "max relative difference of the h/u/v extrema: %.3e" % worst[name])
+    # the CI's own reference file (the one check.F90 reads): h/u/v extrema of both layers agree
+    # to 2e-7 relative after 108 steps (measured 1.8e-7; the Examples/ files are from other
+    # code versions and differ by ~1e-2)
+    assert worst[FINS[0]] < 1e-6
