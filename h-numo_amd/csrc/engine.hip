@@ -332,7 +332,6 @@ static void exchange_qb(hnumo_engine *e, double *qb) { exchange(e, qb, 4, 1, 0);
 static void exchange_qp(hnumo_engine *e, double *qp) { exchange(e, qp, 3, e->L, 3 * (size_t)e->npoin); }
 static void exchange_dpp(hnumo_engine *e) { exchange(e, e->dpp, 1, e->L, (size_t)e->npoin); }
 
-__global__ void epoch_bump_kernel(unsigned long long *epoch) { *epoch = *epoch + 1; }
 
 static void launch_copy(hnumo_engine *e, double *dst, const double *src, size_t n) {
   (void)hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, e->stream);
@@ -343,11 +342,36 @@ static void launch_avg(hnumo_engine *e, double *out, const double *a, const doub
   hipLaunchKernelGGL(average_kernel, dim3(std::max(blocks, 1)), dim3(256), 0, e->stream, out, a, b, n, stride);
 }
 
-static void zero_accumulators(hnumo_engine *e) {
-  (void)hipMemsetAsync(e->qacc, 0, sizeof(double) * QA_N * e->npq, e->stream);
-  (void)hipMemsetAsync(e->facc, 0, sizeof(double) * FA_N * 4 * (size_t)e->nelem * e->nq, e->stream);
-  (void)hipMemsetAsync(e->nacc, 0, sizeof(double) * NA_N * e->npoin, e->stream);
-  (void)hipMemsetAsync(e->gfacc, 0, sizeof(double) * 8 * 4 * (size_t)e->nelem * e->ngl, e->stream);
+// Sub-cycle prologue (mod_rk_mlswe.F90:45-72): zero the time averages, copy the state into
+// stage buffer 0 and bump the persistent kernel's epoch -- one launch instead of four memsets,
+// a copy and a one-thread kernel (each a graph node of ~4 us at this size).
+__global__ void subcycle_prologue_kernel(double *qacc, size_t nqa, double *facc, size_t nfa, double *nacc, size_t nna,
+                                         double *gfacc, size_t nga, double *qbuf0, const double *qb, size_t nqb,
+                                         unsigned long long *epoch) {
+  const size_t s = (size_t)gridDim.x * blockDim.x, t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (size_t i = t0; i < nqa; i += s) qacc[i] = 0.0;
+  for (size_t i = t0; i < nfa; i += s) facc[i] = 0.0;
+  for (size_t i = t0; i < nna; i += s) nacc[i] = 0.0;
+  for (size_t i = t0; i < nga; i += s) gfacc[i] = 0.0;
+  for (size_t i = t0; i < nqb; i += s) qbuf0[i] = qb[i];
+  if (epoch && t0 == 0) *epoch = *epoch + 1;
+}
+
+static void subcycle_prologue(hnumo_engine *e, const double *qb_state, unsigned long long *epoch) {
+  const size_t nqa = QA_N * (size_t)e->npq, nfa = FA_N * 4 * (size_t)e->nelem * e->nq;
+  const int blocks = (int)std::min<size_t>((nqa + 255) / 256, 2048);
+  hipLaunchKernelGGL(subcycle_prologue_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qacc, nqa, e->facc, nfa,
+                     e->nacc, NA_N * (size_t)e->npoin, e->gfacc, 8 * 4 * (size_t)e->nelem * e->ngl, e->qbuf[0],
+                     qb_state, 4 * (size_t)e->npoin, epoch);
+}
+
+// three device copies in one launch (ti_rk_bcl.F90:53-55)
+__global__ void copy3_kernel(double *d0, const double *s0, size_t n0, double *d1, const double *s1, size_t n1,
+                             double *d2, const double *s2, size_t n2) {
+  const size_t s = (size_t)gridDim.x * blockDim.x, t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (size_t i = t0; i < n0; i += s) d0[i] = s0[i];
+  for (size_t i = t0; i < n1; i += s) d1[i] = s1[i];
+  for (size_t i = t0; i < n2; i += s) d2[i] = s2[i];
 }
 
 static void launch_bcl_coeffs(hnumo_engine *e, const double *qp, double *qf) {
@@ -418,11 +442,9 @@ static bool use_persistent(const hnumo_engine *e) {
 
 // ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:19-151) on device state qb_state
 static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp, bool timed = false) {
-  zero_accumulators(e);
-  launch_copy(e, e->qbuf[0], qb_state, 4 * (size_t)e->npoin);
-  exchange_qb(e, e->qbuf[0]);
   const bool pers = use_persistent(e);
-  if (pers) hipLaunchKernelGGL(epoch_bump_kernel, dim3(1), dim3(1), 0, e->stream, e->epoch);
+  subcycle_prologue(e, qb_state, pers ? e->epoch : nullptr);
+  exchange_qb(e, e->qbuf[0]);
   DISPATCH(e, grad_trace(e, e->qbuf[0], e->gtrace[0], 0, e->nelem, pers ? e->gtr[0] : nullptr));
   const int K = e->K, NB = e->p.N_btp;
   int cur;
@@ -449,8 +471,7 @@ static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp,
   int nblk = 1024;
   hipLaunchKernelGGL(btp_finalize_kernel, dim3(nblk), dim3(256), 0, e->stream, e->qacc, e->facc, e->nacc, e->gfacc,
                      e->tau_wind_ave, e->tau_wind, e->npq, 4 * e->nelem * e->nq, e->npoin, 4 * e->nelem * e->ngl, NB,
-                     1.0 / (double)(K * NB));
-  launch_copy(e, qb_state, e->qbuf[cur], 4 * (size_t)e->npoin);
+                     1.0 / (double)(K * NB), qb_state, e->qbuf[cur]);
 }
 
 // the full ti_rk_bcl on device state (e->q, e->qb, e->qp)
@@ -461,9 +482,8 @@ static void launch_step(hnumo_engine *e) {
   launch_copy(e, e->qbp, e->qb, 4 * (size_t)e->npoin);
   launch_bcl_coeffs(e, e->qp, e->qf);
   launch_subcycle(e, e->qbp, e->qp);
-  launch_copy(e, e->q2, e->q, n3);
-  launch_copy(e, e->qp2, e->qp, n3);
-  launch_copy(e, e->qf2, e->qf, nf);
+  hipLaunchKernelGGL(copy3_kernel, dim3((int)std::min<size_t>((nf + 255) / 256, 2048)), dim3(256), 0, e->stream, e->q2,
+                     e->q, n3, e->qp2, e->qp, n3, e->qf2, e->qf, nf);
   DISPATCH(e, mass(e, e->qp2, e->qf2, e->q2));
   exchange_dpp(e);
   DISPATCH(e, cons(e, e->q2, nullptr, 0));
@@ -1056,7 +1076,7 @@ int hnumo_create_rhs_btp(hnumo_engine *eng, double *rhs, const double *qb_df, co
   HIPCHK(hipSetDevice(eng->device));
   int rc = upload_state(eng, nullptr, qb_df, qprime_df);
   if (rc) return rc;
-  zero_accumulators(eng);
+  subcycle_prologue(eng, eng->qb, nullptr);  // zeroed time averages (qbuf[0] is the rhs-only output slot)
   DISPATCH(eng, grad_trace(eng, eng->qb, eng->gtrace[0], 0, eng->nelem));
   StageArgs a{};
   a.m = eng->m;

@@ -1291,11 +1291,14 @@ __global__ void __launch_bounds__(64) grad_trace_kernel(DevMesh m, const double 
 
 // Normalisation of the time averages after the sub-cycle (mod_rk_mlswe.F90:124-149).
 // tau_wind_ave = (sum over N_btp of tau_wind) / N_btp, summed the same way as the reference.
+// It also copies the sub-cycle's result state into qb_state (one launch instead of two).
 __global__ void btp_finalize_kernel(double *qacc, double *facc, double *nacc, double *gfacc, double *tau_wind_ave,
                                     const double *tau_wind, int npq, int nfq, int npoin, int nfn, int N_btp,
-                                    double N_inv) {
+                                    double N_inv, double *qb_state, const double *qb_result) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
+  if (qb_state != qb_result)
+    for (size_t i = tid; i < (size_t)4 * npoin; i += stride) qb_state[i] = qb_result[i];
   for (size_t i = tid; i < (size_t)QA_N * npq; i += stride) qacc[i] = N_inv * qacc[i];
   for (size_t i = tid; i < (size_t)FA_N * nfq; i += stride) facc[i] = N_inv * facc[i];
   for (size_t i = tid; i < (size_t)NA_N * npoin; i += stride) nacc[i] = N_inv * nacc[i];
