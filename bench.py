@@ -9,13 +9,20 @@ per second, one element-update = one element advanced by one barotropic stage wi
 layers, EU/s = E * 2*N_btp*kstages / T_step.  Inputs are the analytic double-gyre initial
 condition (data: synthetic IC, no files).
 
-Multi-GPU (torch.distributed.run, one rank per GPU; weak scaling): the double gyre is
-enlarged to px*py blocks of 25x25 elements (same element size, rank grid 2x1, 2x2, 4x2)
-and each rank owns one block plus a one-element ghost layer (hnumo/partition.py); the
-engine refreshes ghost data from the owners over RCCL point-to-point (xGMI) at every
-exchange point of the step (csrc/engine.hip `exchange`).  value = element-updates of all
-ranks / max time over ranks.  If the RCCL halo cannot be set up on every rank, the ranks
-fall back to independent replicas and say so in config.parallelism.
+Workloads (BASELINE.json configs):
+  N=1   dg25L3  -- configs[1], the double gyre at 25x25 elements, N=4, 3 layers (the metric's
+                   1-GPU configuration); the line also carries "c4_single_gpu", the C4 mesh
+                   below on this one GPU (the strong-scaling base of the N>1 lines).
+  N>1   dg316L3 -- configs[3] (C4), the double gyre at 316x316 = 99,856 elements, N=4,
+                   3 layers, dt=40 s, dt_btp=2 s, split over the N GPUs (strong scaling:
+                   rank grid 2x1, 2x2, 4x2 of 158x316 / 158x158 / 79x158 element blocks).
+  --weak        -- labelled extra: N blocks of 25x25 elements (weak scaling).
+Multi-GPU runs one rank per GPU (torch.distributed.run); each rank owns one block plus a
+one-element ghost layer (hnumo/partition.py) whose data the engine refreshes from the owners
+over RCCL point-to-point (xGMI) at every exchange point of the step (csrc/engine.hip
+`exchange`).  value = element-updates of all ranks / max time over ranks.  If the RCCL halo
+cannot be set up (or fails) on any rank, the ranks fall back to independent replicas of the
+per-GPU block and say so in config.parallelism.
 """
 from __future__ import annotations
 
@@ -72,14 +79,43 @@ def cpu_baseline(case, steps: int):
             "sample": sample + f" of the C restatement (oracle/hnumo_oracle.c, -O2), {t:.2f} s"}
 
 
+def c4_single_gpu(steps: int = 3):
+    """The C4 mesh (dg316L3, 99,856 elements) on this one GPU: the base of the N>1 strong-scaling
+    lines (reported beside the N=1 configs[1] line)."""
+    import torch
+    from hnumo.case import build_case, make_config
+    from hnumo.engine import Engine
+    from hnumo.roofline import element_updates_per_step
+    case = build_case(make_config("dg316L3"), dense=False)
+    eng = Engine(case)
+    eng.set_resident(True)
+    q, qb, qp = eng.state()
+    eng.ti_rk_bcl(q, qb, qp)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng.bench_steps(steps)
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    k_ms = eng.time_stage_kernel(1)
+    from hnumo.roofline import HBM_PEAK_GBS, stage_bytes
+    eng.close()
+    ach = stage_bytes(case) / (k_ms * 1e-3) / 1e9
+    return {"workload": "dg316L3 (C4: 316x316 elements, N=4, 3 layers) on 1 GPU, per-stage launches",
+            "value": round(element_updates_per_step(case) * steps / t, 1), "unit": "element-updates/s",
+            "steps": steps, "ms_per_step": round(1e3 * t / steps, 3),
+            "stage_kernel_us": round(k_ms * 1e3, 2), "stage_kernel_frac": round(ach / HBM_PEAK_GBS, 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=None, help="default: 20 at N=1 (dg25L3), 5 at N>1 (C4)")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="dg25L3")
+    ap.add_argument("--config", default=None, help="default: dg25L3 at N=1, dg316L3 (C4) at N>1")
+    ap.add_argument("--weak", action="store_true", help="N>1: N blocks of the 1-GPU mesh (weak scaling)")
     ap.add_argument("--cpu-steps", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c4", action="store_true", help="N=1: skip the c4_single_gpu figure")
     ap.add_argument("--summation", default="reference", choices=["reference", "factored"],
                     help="stage summation order (hnumo_set_summation); only 'reference' meets the 1e-10 bar")
     args = ap.parse_args()
@@ -96,24 +132,35 @@ def main():
 
     from hnumo.case import build_case, make_config
     from hnumo.engine import Engine
-    from hnumo.roofline import HBM_PEAK_GBS, element_updates_per_step, stage_bytes
+    from hnumo.roofline import HBM_PEAK_GBS, element_updates_per_step, stage_bytes, step_bytes
 
-    base_cfg = make_config(args.config)
-    case = build_case(base_cfg, dense=False)         # the per-GPU block (roofline, workload name)
-    eng, parallelism = None, "single"
+    weak = world > 1 and args.weak
+    cfg_name = args.config or ("dg316L3" if world > 1 and not weak else "dg25L3")
+    steps = args.steps if args.steps is not None else (20 if world == 1 or weak else 5)
+    base_cfg = make_config(cfg_name)
+    eng, parallelism, scaling = None, "single", "weak"
+    case = None
     if world > 1:
         from hnumo.partition import partition, rank_grid
         px, py = rank_grid(world)
-        x0, x1 = base_cfg["xdims"]
-        y0, y1 = base_cfg["ydims"]
-        gcfg = make_config(args.config, nelx=base_cfg["nelx"] * px, nely=base_cfg["nely"] * py,
-                           xdims=(x0, x0 + (x1 - x0) * px), ydims=(y0, y0 + (y1 - y0) * py))
+        if weak:
+            x0, x1 = base_cfg["xdims"]
+            y0, y1 = base_cfg["ydims"]
+            gcfg = make_config(cfg_name, nelx=base_cfg["nelx"] * px, nely=base_cfg["nely"] * py,
+                               xdims=(x0, x0 + (x1 - x0) * px), ydims=(y0, y0 + (y1 - y0) * py))
+        else:
+            gcfg = base_cfg
+            scaling = "strong"
         gcase = build_case(gcfg, dense=False)
         obj = [Engine.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         err = None
         try:
-            eng = Engine(partition(gcase, world, rank), device=local_rank, comm_id=obj[0], summation=args.summation)
+            case = partition(gcase, world, rank)
+            eng = Engine(case, device=local_rank, comm_id=obj[0], summation=args.summation)
+            eng.set_resident(True)
+            q, qb, qp = eng.state()
+            eng.ti_rk_bcl(q, qb, qp)                 # first step: uploads, captures the graph, exchanges
         except Exception as exc:  # pragma: no cover - depends on the node
             err = f"{type(exc).__name__}: {exc}"
         bad = torch.tensor([1 if err else 0], device="cuda")
@@ -122,14 +169,29 @@ def main():
             if eng is not None:
                 eng.close()
             eng = None
+            if weak:
+                case = build_case(base_cfg, dense=False)
+            else:  # replicas of one rank's block (same per-GPU work, no exchange)
+                bx, by = gcfg["nelx"] // px, gcfg["nely"] // py
+                x0, x1 = gcfg["xdims"]
+                y0, y1 = gcfg["ydims"]
+                case = build_case(make_config(cfg_name, nelx=bx, nely=by, xdims=(x0, x0 + (x1 - x0) / px),
+                                              ydims=(y0, y0 + (y1 - y0) / py)), dense=False)
             parallelism = f"replicas{world} (RCCL halo unavailable: {err or 'on another rank'})"
         else:
-            parallelism = f"domain decomposition {px}x{py} x ({base_cfg['nelx']}x{base_cfg['nely']}), ghost halo over RCCL"
+            bx, by = gcfg["nelx"] // px, gcfg["nely"] // py
+            parallelism = (f"domain decomposition {px}x{py} blocks of {bx}x{by} elements "
+                           f"({gcfg['nelx']}x{gcfg['nely']} total), one-element ghost halo over RCCL p2p")
+        del gcase
     if eng is None:
+        if case is None:
+            case = build_case(base_cfg, dense=False)
         eng = Engine(case, device=local_rank, summation=args.summation)
-    eng.set_resident(True)
-    q, qb, qp = eng.state()
-    eng.ti_rk_bcl(q, qb, qp)                       # uploads the state, builds the graph
+        eng.set_resident(True)
+        q, qb, qp = eng.state()
+        eng.ti_rk_bcl(q, qb, qp)                   # uploads the state, builds the graph
+    else:
+        q, qb, qp = eng.state()
     if args.warmup > 1:
         eng.bench_steps(args.warmup - 1)
 
@@ -140,15 +202,21 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    _, k_ms, _ = eng.bench_steps(args.steps)         # synchronises the engine stream
+    _, k_ms, _ = eng.bench_steps(steps)               # synchronises the engine stream; checks the flags
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    eu_local = element_updates_per_step(case) * steps
     if dist is not None:
-        t = torch.tensor([elapsed], device="cuda")
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        n = torch.tensor([eu_local], device="cuda", dtype=torch.float64)
+        dist.all_reduce(n, op=dist.ReduceOp.SUM)
+        eu_total = float(n.item())
+    else:
+        eu_total = float(eu_local)
     path = eng.stage_path
     kname = "btp_subcycle_kernel" if path == "persistent" else "btp_stage_kernel"
     k_src = "graph event nodes around the corrector sub-cycle"
@@ -161,43 +229,62 @@ def main():
     if not (abs(qb).max() < 1e30):
         raise RuntimeError("non-finite state after benchmark")
 
-    eu = element_updates_per_step(case) * args.steps * world   # every rank owns one block of E elements
-    value = eu / elapsed
-    ms_per_step = 1e3 * elapsed / args.steps
+    value = eu_total / elapsed
+    ms_per_step = 1e3 * elapsed / steps
     sb = stage_bytes(case)
     roof = None
     if k_ms and k_ms > 0:
         achieved = sb / (k_ms * 1e-3) / 1e9
+        step_ach = step_bytes(case) * steps / elapsed / 1e9
+        E = case.scalars["nelem"]
+        limiter = ("latency: %d elements on 256 CUs (%.1f per CU), working set inside the 256 MiB Infinity "
+                   "Cache; profiles/ SQ counters: waves mostly waiting" % (E, E / 256.0)) if E < 4096 else \
+            "per-element latency x occupancy (3 workgroups/CU); HBM traffic below the algorithmic bytes"
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "limiter": limiter,
                 "kernel": kname, "kernel_avg_us": round(k_ms * 1e3, 3),
-                "algorithmic_bytes_per_launch": int(sb), "timing": k_src}
+                "algorithmic_bytes_per_launch": int(sb), "timing": k_src,
+                "step_achieved": round(step_ach, 1), "step_frac": round(step_ach / HBM_PEAK_GBS, 4),
+                "step_bytes": int(step_bytes(case)),
+                "step_model": "E*(2*N_btp*kstages*B_stage + B_bcl_step)/T_step per GPU (hnumo/roofline.py)"}
         pmc = os.path.join(REPO, "profiles", "pmc_btp_stage.json")
         if os.path.exists(pmc):
             try:
                 d = json.load(open(pmc))
-                if d.get("config") == args.config and d.get("kernel", "btp_stage_kernel") == kname:
+                if d.get("config") == cfg_name and d.get("kernel", "btp_stage_kernel") == kname:
                     roof["traffic"] = d["hbm_bytes_per_launch"]
+                    roof["traffic_source"] = pmc.replace(REPO + os.sep, "")
             except Exception:
                 pass
+    S = case.scalars
+    if world > 1 and not weak:
+        wl = (f"{cfg_name} (C4): double-gyre {base_cfg['nelx']}x{base_cfg['nely']} = "
+              f"{base_cfg['nelx'] * base_cfg['nely']} elements split over {world} GPUs")
+    else:
+        wl = f"{cfg_name}: double-gyre {base_cfg['nelx']}x{base_cfg['nely']} elements per GPU"
     out = {
         "metric": "DG element-updates/sec (all layers, per RK stage)",
-        "value": round(value, 1), "unit": "element-updates/s", "n_gpus": world, "steps": args.steps,
+        "value": round(value, 1), "unit": "element-updates/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic (analytic double-gyre IC)",
-        "config": {"workload": f"{args.config}: double-gyre {base_cfg['nelx']}x{base_cfg['nely']} elements per GPU, "
-                               f"N={case.scalars['ngl'] - 1}, {case.scalars['nlayers']} layers, "
-                               f"N_btp={case.scalars['N_btp']}, kstages={case.scalars['kstages']}",
-                   "elements": case.scalars["nelem"], "nlayers": case.scalars["nlayers"],
-                   "nop": case.scalars["ngl"] - 1, "parallelism": parallelism,
+        "scaling": scaling, "vs_baseline": None, "dtype": "f64", "data": "synthetic (analytic double-gyre IC)",
+        "config": {"workload": wl + f", N={S['ngl'] - 1}, {S['nlayers']} layers, "
+                               f"N_btp={S['N_btp']}, kstages={S['kstages']}",
+                   "elements": int(eu_total / steps / (2 * S["N_btp"] * S["kstages"])),
+                   "elements_per_gpu": int(eu_local / steps / (2 * S["N_btp"] * S["kstages"])),
+                   "nlayers": S["nlayers"], "nop": S["ngl"] - 1, "parallelism": parallelism,
                    "summation": args.summation, "stage_path": path},
         "roofline": roof,
     }
+    eng.close()
+    if rank == 0 and world == 1 and not args.no_c4 and args.config is None:
+        try:
+            out["c4_single_gpu"] = c4_single_gpu()
+        except Exception as exc:  # pragma: no cover - diagnostic only
+            out["c4_single_gpu"] = {"error": f"{type(exc).__name__}: {exc}"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(build_case(make_config(args.config)), args.cpu_steps)
+        out["cpu_baseline"] = cpu_baseline(build_case(make_config(cfg_name)), args.cpu_steps)
     if rank == 0:
         print(json.dumps(out))
-    eng.close()
     if dist is not None:
         dist.destroy_process_group()
 

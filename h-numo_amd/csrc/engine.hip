@@ -53,6 +53,7 @@ struct hnumo_engine {
   LocalGroup *group = nullptr;
   bool own_stream = true;
   std::string err;
+  std::string comm_err;  // first halo-transport failure (sticky until reported)
   hipStream_t stream = nullptr;
   DevMesh m{};
   hnumo_params p{};
@@ -273,23 +274,41 @@ __global__ void ghost_unpack_kernel(double *base, const double *buf, const int *
 
 // engines of one process joined by hnumo_local_group: a host barrier per exchange keeps
 // every engine's pack ahead of the copies and the copies ahead of the next pack (one stream)
+// An engine that fails (or is destroyed) aborts the group: every waiting engine wakes up,
+// stops exchanging and reports the abort (no thread is left waiting in a barrier).  The
+// group and its shared stream (created by engine 0) live until the last engine is destroyed.
 struct LocalGroup {
   std::vector<hnumo_engine *> eng;
   std::mutex mu;
   std::condition_variable cv;
-  int count = 0, gen = 0;
-  void barrier() {
+  int count = 0, gen = 0, refs = 0;
+  bool aborted = false;
+  hipStream_t stream = nullptr;
+  bool barrier() {
     std::unique_lock<std::mutex> lk(mu);
+    if (aborted) return false;
     int g = gen;
     if (++count == (int)eng.size()) {
       count = 0;
       gen++;
       cv.notify_all();
     } else {
-      cv.wait(lk, [&] { return gen != g; });
+      cv.wait(lk, [&] { return gen != g || aborted; });
     }
+    return !aborted;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(mu);
+    aborted = true;
+    cv.notify_all();
   }
 };
+
+// RCCL results are checked at every call; the first failure is kept (sticky) and turned into
+// HNUMO_ERR_DEVICE by run_steps -- a failed exchange must not pass as a good step
+static void nccl_check(hnumo_engine *e, ncclResult_t r, const char *what) {
+  if (r != ncclSuccess && e->comm_err.empty()) e->comm_err = std::string(what) + ": " + ncclGetErrorString(r);
+}
 
 // refresh the ghost elements' block of `base` from their owners
 static void exchange(hnumo_engine *e, double *base, int ncomp, int nblk, size_t stride) {
@@ -302,24 +321,27 @@ static void exchange(hnumo_engine *e, double *base, int ncomp, int nblk, size_t 
                          e->stream, n.sbuf, base, n.d_send, n.nsend, per, nblk, stride);
     }
   if (e->comm_mode == 2) {
-    (void)ncclGroupStart();
+    nccl_check(e, ncclGroupStart(), "ncclGroupStart");
     for (auto &n : e->nbh) {
-      if (n.nsend) (void)ncclSend(n.sbuf, (size_t)n.nsend * nblk * per, ncclDouble, n.rank, e->comm, e->stream);
-      if (n.nrecv) (void)ncclRecv(n.rbuf, (size_t)n.nrecv * nblk * per, ncclDouble, n.rank, e->comm, e->stream);
+      if (n.nsend)
+        nccl_check(e, ncclSend(n.sbuf, (size_t)n.nsend * nblk * per, ncclDouble, n.rank, e->comm, e->stream), "ncclSend");
+      if (n.nrecv)
+        nccl_check(e, ncclRecv(n.rbuf, (size_t)n.nrecv * nblk * per, ncclDouble, n.rank, e->comm, e->stream), "ncclRecv");
     }
-    (void)ncclGroupEnd();
+    nccl_check(e, ncclGroupEnd(), "ncclGroupEnd");
   } else {
     LocalGroup *g = e->group;
-    g->barrier();
+    if (!g->barrier()) return;
     for (auto &n : e->nbh) {
       if (!n.nrecv) continue;
       hnumo_engine *peer = g->eng[n.rank];
       for (auto &pn : peer->nbh)
-        if (pn.rank == e->rank)
-          (void)hipMemcpyAsync(n.rbuf, pn.sbuf, sizeof(double) * (size_t)n.nrecv * nblk * per, hipMemcpyDeviceToDevice,
-                               e->stream);
+        if (pn.rank == e->rank &&
+            hipMemcpyAsync(n.rbuf, pn.sbuf, sizeof(double) * (size_t)n.nrecv * nblk * per, hipMemcpyDeviceToDevice,
+                           e->stream) != hipSuccess)
+          e->comm_err = "local group: hipMemcpyAsync of a ghost block failed";
     }
-    g->barrier();
+    if (!g->barrier()) return;
   }
   for (auto &n : e->nbh)
     if (n.nrecv) {
@@ -526,6 +548,20 @@ void hnumo_engine_destroy(hnumo_engine *eng) {
   for (void *ptr : eng->allocs) (void)hipFree(ptr);
   if (eng->h_neg) (void)hipHostFree(eng->h_neg);
   if (eng->stream && eng->own_stream) (void)hipStreamDestroy(eng->stream);
+  if (LocalGroup *g = eng->group) {
+    // the destroyed engine cannot take part in exchanges any more; the last one out frees
+    // the group and the shared stream
+    g->abort();
+    bool last;
+    {
+      std::lock_guard<std::mutex> lk(g->mu);
+      last = --g->refs == 0;
+    }
+    if (last) {
+      if (g->stream) (void)hipStreamDestroy(g->stream);
+      delete g;
+    }
+  }
   if (eng->comm) (void)ncclCommDestroy(eng->comm);
   if (eng->ev0) (void)hipEventDestroy(eng->ev0);
   if (eng->ev1) (void)hipEventDestroy(eng->ev1);
@@ -956,7 +992,8 @@ static int download_state(hnumo_engine *eng, double *q, double *qb, double *qp) 
 // same launch sequence directly.
 static int ensure_graph(hnumo_engine *eng) {
   if (eng->graph_exec || eng->no_graph) return 0;
-  if (eng->comm_mode == 1) {
+  const char *ge = getenv("HNUMO_GRAPH");
+  if (eng->comm_mode == 1 || (ge && ge[0] == '0')) {
     eng->no_graph = true;
     return 0;
   }
@@ -971,7 +1008,33 @@ static int ensure_graph(hnumo_engine *eng) {
     eng->graph = nullptr;
     eng->graph_exec = nullptr;
     eng->no_graph = true;
+    // RCCL calls were recorded into the failed capture: this rank's point-to-point sequence
+    // can no longer be trusted to match its peers', so report instead of falling back
+    if (eng->comm_mode == 2)
+      return fail(eng, HNUMO_ERR_DEVICE,
+                  std::string("step graph capture with RCCL failed (") + hipGetErrorString(err) +
+                      "); rerun with HNUMO_GRAPH=0 for direct launches");
   }
+  if (!eng->comm_err.empty()) return fail(eng, HNUMO_ERR_DEVICE, eng->comm_err);
+  return 0;
+}
+
+// error bits of the device flag word (neg_flag): 1 negative thickness, 2 non-finite
+// state, 8 a persistent sub-cycle trace wait timed out (workgroups not co-resident)
+static int flag_error(hnumo_engine *eng, int flags) {
+  if (flags & 1) return fail(eng, HNUMO_ERR_NEGATIVE_THICKNESS, "Negative mass in thickness at some points");
+  if (flags & 2) return fail(eng, HNUMO_ERR_NONFINITE, "non-finite barotropic state");
+  if (flags & 8) return fail(eng, HNUMO_ERR_DEVICE, "persistent sub-cycle: a trace granule wait timed out");
+  return 0;
+}
+
+static int transport_error(hnumo_engine *eng) {
+  if (!eng->comm_err.empty()) {
+    std::string m = eng->comm_err;
+    eng->comm_err.clear();
+    return fail(eng, HNUMO_ERR_DEVICE, "halo exchange failed: " + m);
+  }
+  if (eng->group && eng->group->aborted) return fail(eng, HNUMO_ERR_DEVICE, "local exchange group aborted by another engine");
   return 0;
 }
 
@@ -994,10 +1057,8 @@ static int run_steps(hnumo_engine *eng, int nsteps) {
   HIPCHK(hipMemcpyAsync(eng->h_neg, eng->neg_flag, sizeof(int), hipMemcpyDeviceToHost, eng->stream));
   HIPCHK(hipStreamSynchronize(eng->stream));
   HIPCHK(hipGetLastError());
-  if (*eng->h_neg & 1) return fail(eng, HNUMO_ERR_NEGATIVE_THICKNESS, "Negative mass in thickness at some points");
-  if (*eng->h_neg & 2) return fail(eng, HNUMO_ERR_NONFINITE, "non-finite barotropic state");
-  if (*eng->h_neg & 8) return fail(eng, HNUMO_ERR_DEVICE, "persistent sub-cycle: a trace granule wait timed out");
-  return 0;
+  if ((rc = transport_error(eng))) return rc;
+  return flag_error(eng, *eng->h_neg);
 }
 
 int hnumo_ti_rk_bcl(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df) {
@@ -1235,11 +1296,18 @@ int hnumo_bench_steps(hnumo_engine *eng, int nsteps, double *ms_total, double *m
   HIPCHK(hipSetDevice(eng->device));
   int rc = ensure_graph(eng);
   if (rc) return rc;
+  HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
   HIPCHK(hipEventRecord(eng->ev0, eng->stream));
   rc = launch_steps(eng, nsteps);
   if (rc) return rc;
   HIPCHK(hipEventRecord(eng->ev1, eng->stream));
+  HIPCHK(hipMemcpyAsync(eng->h_neg, eng->neg_flag, sizeof(int), hipMemcpyDeviceToHost, eng->stream));
   HIPCHK(hipEventSynchronize(eng->ev1));
+  HIPCHK(hipStreamSynchronize(eng->stream));
+  HIPCHK(hipGetLastError());
+  // a timed run whose state went bad (or whose persistent hand-offs timed out) is no result
+  if ((rc = transport_error(eng))) return rc;
+  if ((rc = flag_error(eng, *eng->h_neg))) return rc;
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, eng->ev0, eng->ev1));
   if (ms_total) *ms_total = ms;
@@ -1276,8 +1344,12 @@ int hnumo_time_stage_kernel(hnumo_engine *eng, int nsubcycles, double *ms_kernel
     total += mk;
   }
   eng->kernel_events = ke;
+  HIPCHK(hipMemcpyAsync(eng->h_neg, eng->neg_flag, sizeof(int), hipMemcpyDeviceToHost, eng->stream));
   HIPCHK(hipStreamSynchronize(eng->stream));
   HIPCHK(hipGetLastError());
+  int rc = transport_error(eng);
+  if (!rc) rc = flag_error(eng, *eng->h_neg & 8);
+  if (rc) return rc;
   *ms_kernel_avg = total / ((double)nsubcycles * eng->p.N_btp * eng->K);
   return 0;
 }
@@ -1308,14 +1380,14 @@ int hnumo_local_group(hnumo_engine **engines, int n) {
       return HNUMO_ERR_INVALID;
   LocalGroup *g = new LocalGroup();
   g->eng.assign(engines, engines + n);
+  g->stream = engines[0]->stream;  // the group owns engine 0's stream from now on
+  g->refs = n;
   for (int i = 0; i < n; i++) {
     hnumo_engine *e = engines[i];
     (void)hipSetDevice(e->device);
-    if (i > 0) {
-      if (e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
-      e->stream = engines[0]->stream;
-      e->own_stream = false;
-    }
+    if (i > 0 && e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+    e->stream = g->stream;
+    e->own_stream = false;
     e->group = g;
     e->comm_mode = 1;
   }
@@ -1334,9 +1406,11 @@ int hnumo_group_ti_rk_bcl(hnumo_engine **engines, int n, double **q_df, double *
         rc[i] = upload_state(eng, q_df[i], qb_df[i], qprime_df[i]);
         eng->uploaded = true;
       }
-      int r = run_steps(eng, 1);
+      int r = rc[i] ? rc[i] : run_steps(eng, 1);
       if (!rc[i]) rc[i] = r;
       if (!rc[i] && !eng->resident) rc[i] = download_state(eng, q_df[i], qb_df[i], qprime_df[i]);
+      // a failing engine must not leave the others waiting in an exchange barrier
+      if (rc[i]) eng->group->abort();
     });
   for (auto &t : th) t.join();
   for (int i = 0; i < n; i++)

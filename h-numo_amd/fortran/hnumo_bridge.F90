@@ -22,7 +22,7 @@ module hnumo_bridge
     implicit none
     private
     public :: hnumo_bridge_init, hnumo_bridge_ti_rk_bcl, hnumo_bridge_fetch_averages, &
-        hnumo_bridge_finalize, hnumo_bridge_engine
+        hnumo_bridge_finalize, hnumo_bridge_engine, hnumo_bridge_sync
 
     type(c_ptr), save :: engine = c_null_ptr
 
@@ -137,6 +137,21 @@ contains
             stop
         end if
     end subroutine hnumo_bridge_ti_rk_bcl
+
+    ! Resident mode (hnumo_bridge_init(device, resident=.true.)) keeps q_df, qb_df, qprime_df
+    ! in HBM between steps and never writes the caller's arrays: call this before anything
+    ! on the host reads the state (diagnostics, snapshots, mlswe_FIN.txt, restart dumps --
+    ! mod_time_loop.F90:219-254), or those would see the state of the first step.
+    subroutine hnumo_bridge_sync(q_df, qb_df, qprime_df)
+        real(c_double), intent(inout) :: q_df(:, :, :), qb_df(:, :), qprime_df(:, :, :)
+        integer(c_int) :: rc
+        if (.not. c_associated(engine)) stop 'hnumo_bridge_sync: call hnumo_bridge_init first'
+        rc = hnumo_sync(engine, q_df, qb_df, qprime_df)
+        if (rc /= HNUMO_OK) then
+            print *, 'hnumo_sync: ', hnumo_last_error(engine)
+            stop
+        end if
+    end subroutine hnumo_bridge_sync
 
     ! copy the engine's time averages into the reference's mod_variables arrays
     subroutine hnumo_bridge_fetch_averages()

@@ -62,8 +62,15 @@ def lib():
     return _lib
 
 
-def _dp(a):
-    assert a.flags["F_CONTIGUOUS"] and a.dtype == np.float64
+def _dp(a, size=None, name="array"):
+    """Pointer to a float64 Fortran-contiguous array of exactly `size` elements (the C side
+    reads and writes fixed-size blocks, so a wrong shape must never reach it)."""
+    if not isinstance(a, np.ndarray) or a.dtype != np.float64 or not a.flags["F_CONTIGUOUS"]:
+        raise ValueError(f"{name}: need a Fortran-contiguous float64 numpy array")
+    if not a.flags["WRITEABLE"]:
+        raise ValueError(f"{name}: array is read-only")
+    if size is not None and a.size != size:
+        raise ValueError(f"{name}: {a.size} elements, expected {size}")
     return a.ctypes.data_as(C.POINTER(C.c_double))
 
 
@@ -106,21 +113,32 @@ class Engine:
         return (np.array(A["q_df"], order="F"), np.array(A["qb_df"], order="F"),
                 np.array(A["qprime_df"], order="F"))
 
+    # sizes of q_df(3,npoin,L), qb_df(4,npoin), qprime_df(3,npoin,L)
+    def _sizes(self):
+        d = self.dims
+        return 3 * d["npoin"] * d["nlayers"], 4 * d["npoin"], 3 * d["npoin"] * d["nlayers"]
+
+    def _state_ptrs(self, q, qb, qp):
+        nq, nb, np_ = self._sizes()
+        return _dp(q, nq, "q_df"), _dp(qb, nb, "qb_df"), _dp(qp, np_, "qprime_df")
+
     # = ti_rk_bcl (ti_rk_bcl.F90:9)
     def ti_rk_bcl(self, q, qb, qp):
-        self._check(lib().hnumo_ti_rk_bcl(self.h, _dp(q), _dp(qb), _dp(qp)))
+        self._check(lib().hnumo_ti_rk_bcl(self.h, *self._state_ptrs(q, qb, qp)))
 
     def btp_bcl_coeffs(self, qp):
-        self._check(lib().hnumo_btp_bcl_coeffs(self.h, _dp(qp)))
+        self._check(lib().hnumo_btp_bcl_coeffs(self.h, _dp(qp, self._sizes()[2], "qprime_df")))
 
     # = ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:19)
     def ti_barotropic_ssprk(self, qb, qp):
-        self._check(lib().hnumo_ti_barotropic_ssprk(self.h, _dp(qb), _dp(qp)))
+        _, nb, np_ = self._sizes()
+        self._check(lib().hnumo_ti_barotropic_ssprk(self.h, _dp(qb, nb, "qb_df"), _dp(qp, np_, "qprime_df")))
 
     # = create_rhs_btp (mod_rhs_btp.F90:28)
     def create_rhs_btp(self, qb, qp):
+        _, nb, np_ = self._sizes()
         rhs = np.zeros((3, self.dims["npoin"]), order="F")
-        self._check(lib().hnumo_create_rhs_btp(self.h, _dp(rhs), _dp(qb), _dp(qp)))
+        self._check(lib().hnumo_create_rhs_btp(self.h, _dp(rhs), _dp(qb, nb, "qb_df"), _dp(qp, np_, "qprime_df")))
         return rhs
 
     def field(self, name):
@@ -145,7 +163,7 @@ class Engine:
         self._check(lib().hnumo_set_resident(self.h, int(on)))
 
     def sync(self, q, qb, qp):
-        self._check(lib().hnumo_sync(self.h, _dp(q), _dp(qb), _dp(qp)))
+        self._check(lib().hnumo_sync(self.h, *self._state_ptrs(q, qb, qp)))
 
     def bench_steps(self, nsteps: int):
         t = C.c_double()
@@ -202,8 +220,11 @@ def local_group(engines):
 def group_ti_rk_bcl(engines, states):
     """One baroclinic step of every engine of a local group; states[i] = (q, qb, qp) arrays."""
     n = len(engines)
+    if len(states) != n:
+        raise ValueError("one (q, qb, qp) state per engine")
     arr = engines[0]._group
-    mk = lambda j: (C.POINTER(C.c_double) * n)(*[_dp(states[i][j]) for i in range(n)])
+    ptrs = [e._state_ptrs(*states[i]) for i, e in enumerate(engines)]
+    mk = lambda j: (C.POINTER(C.c_double) * n)(*[ptrs[i][j] for i in range(n)])
     rc = lib().hnumo_group_ti_rk_bcl(arr, n, mk(0), mk(1), mk(2))
     if rc:
         msgs = [lib().hnumo_last_error(e.h).decode() for e in engines]

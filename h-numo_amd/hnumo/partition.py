@@ -172,8 +172,8 @@ def partition(case: Case, nranks: int, rank: int) -> RankCase:
     for r in range(nranks):
         if r == rank:
             continue
-        gh_r = _ghosts(owner == r, el, er)
-        send = np.array([g2l[g] for g in owned if g in set(gh_r.tolist())], dtype=np.int64)
+        gh_r = set(_ghosts(owner == r, el, er).tolist())
+        send = np.array([g2l[g] for g in owned if g in gh_r], dtype=np.int64)
         recv = np.array([g2l[g] for g in ghosts if owner[g] == r], dtype=np.int64)
         if send.size or recv.size:
             neighbours.append(Neighbour(r, send, recv))

@@ -28,13 +28,50 @@ def stage_bytes_per_element(nop: int, faces_per_element: float) -> float:
     return 8.0 * (44 * P + 39 * Q + faces_per_element * (47 * n + 46 * m))
 
 
+def bcl_bytes_per_element(nop: int, nlayers: int, faces_per_element: float) -> float:
+    """Algorithmic bytes of the baroclinic part of ONE step per element (same counting rule,
+    per kernel family, predictor + corrector; P, Q, n, m as above, L layers):
+      btp_bcl_coeffs_qdf  elem: qprime in 3PL, dpp_graduv out 4PL, dpprime_visc out PL,
+                          Q_*/H_bcl out 4Q, btp_dpp_graduv + pbprime_visc out 5P
+                          face: qprime faces 6nL, graduv_dpp_face out 10nL, edge coeffs 4m,
+                          btp_graduv_dpp_face 10n
+      layer mass          elem: qprime 3PL, dp in/out 2PL, dp' out PL, ope/uvb averages 3Q,
+                          sum_layer_mass_flux 2Q;  face: qprime faces 6nL, face averages 6m,
+                          flux mL, sums 2m
+      consistency         elem: dp' PL, q 2PL, averages + sums 4Q;  face: dp' traces 2nL,
+                          averages + sums 4m, flux mL
+      layer momentum      elem: qprime 3PL, q in/out 6PL, qprime out 3PL, dpp_graduv 4PL,
+                          dpprime_visc PL, qb 4P, 10 quad averages 10Q, 7 nodal averages 7P;
+                          face: qprime faces 6nL, graduv_dpp_face 10nL, graduvb_face_ave 8n,
+                          12 face averages 12m, fluxes 4mL, LDG 2nL
+    i.e. per half-step 34PL + 23Q + 16P + F/E*(40nL + 6mL + 28m + 18n); twice per step.
+    About 1 % of the sub-cycle's 2*N_btp*kstages stages."""
+    n, m = nop + 1, 2 * nop + 1
+    P, Q, L = n * n, m * m, nlayers
+    half = 34 * P * L + 23 * Q + 16 * P + faces_per_element * (40 * n * L + 6 * m * L + 28 * m + 18 * n)
+    return 8.0 * 2 * half
+
+
+def owned_elements(case) -> int:
+    """Elements this engine advances (a RankCase's ghosts are excluded)."""
+    return int(getattr(case, "nelem_owned", 0) or case.scalars["nelem"])
+
+
 def stage_bytes(case) -> float:
-    """Algorithmic bytes of ONE btp_stage_kernel launch (all elements)."""
+    """Algorithmic bytes of ONE btp_stage_kernel launch (all owned elements)."""
     S = case.scalars
     E, F = S["nelem"], S["nface"]
-    return E * stage_bytes_per_element(S["ngl"] - 1, F / E)
+    return owned_elements(case) * stage_bytes_per_element(S["ngl"] - 1, F / E)
+
+
+def step_bytes(case) -> float:
+    """Algorithmic bytes of ONE baroclinic step: E*(2*N_btp*kstages*B_stage + B_bcl_step)."""
+    S = case.scalars
+    E, F = S["nelem"], S["nface"]
+    return stage_bytes(case) * 2 * S["N_btp"] * S["kstages"] + \
+        owned_elements(case) * bcl_bytes_per_element(S["ngl"] - 1, S["nlayers"], F / E)
 
 
 def element_updates_per_step(case) -> int:
     S = case.scalars
-    return S["nelem"] * 2 * S["N_btp"] * S["kstages"]
+    return owned_elements(case) * 2 * S["N_btp"] * S["kstages"]

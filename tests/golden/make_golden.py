@@ -8,6 +8,7 @@ Each fixture stores the sha256 of the input bundle, so a change to the setup cod
 detected instead of silently comparing against stale outputs.
 """
 import hashlib
+import json
 import os
 import sys
 import tempfile
@@ -32,6 +33,17 @@ GOLDEN = [
     ("dg25L3_step1", "dg25L3", "step", 1, 7),
     ("bump10q_step1", "bump10q", "step", 1, 1),
     ("dg8L3q_step1", "dg8L3q", "step", 1, 1),
+    # C3 at N=7 (8x8 elements: the 25x25 bundle's dense tables are ~0.5 GB)
+    ("dg8N7L3_step1", "dg25N7L3", "step", 1, 1, dict(nelx=8, nely=8)),
+    # branches the shipped namelists do not exercise: quadratic drag + no-slip
+    # walls, linear drag + beta plane + mixed walls, 3-layer lake, quad-point LDG + no-slip
+    ("bump10_b2ns_step1", "bump10", "step", 1, 1,
+     dict(botfr=2, cd=1e-3, visc=25.0, method_visc=3, y_boundary=(2, 2))),
+    ("bump10_mixed_step1", "bump10", "step", 1, 1,
+     dict(botfr=1, cd=1e-7, f0=1e-4, beta=1e-11, x_boundary=(2, 4))),
+    ("lake10L3_step1", "lake10", "step", 1, 1, dict(nlayers=3)),
+    ("bump10q_ns_step1", "bump10q", "step", 1, 1, dict(y_boundary=(2, 2), botfr=2, cd=1e-3)),
+    ("dg8L3q_mixed_step1", "dg8L3q", "step", 1, 1, dict(x_boundary=(2, 4))),
 ]
 FIELDS_KEPT = ["ope_ave", "H_ave", "Qu_ave", "btp_mass_flux_ave", "uvb_face_ave", "H_face_ave",
                "graduvb_ave", "Q_uu_dp", "H_bcl_edge", "btp_graduv_dpp_face"]
@@ -44,12 +56,24 @@ def bundle_hash(case, mode, nsteps):
         return hashlib.sha256(open(p, "rb").read()).hexdigest()
 
 
-def main():
-    for name, cfg, mode, nsteps, stride in GOLDEN:
-        case = build_case(make_config(cfg))
+def overrides_of(g) -> dict:
+    """Config overrides stored in a fixture (JSON; lists back to tuples)."""
+    if "overrides" not in g:
+        return {}
+    return {k: tuple(v) if isinstance(v, list) else v for k, v in json.loads(str(g["overrides"])).items()}
+
+
+def main(only=None):
+    for entry in GOLDEN:
+        name, cfg, mode, nsteps, stride = entry[:5]
+        ov = entry[5] if len(entry) > 5 else {}
+        if only and name not in only:
+            continue
+        case = build_case(make_config(cfg, **ov))
         out = O.run_reference(case, mode, nsteps)
         keep = {"bundle_sha256": np.array(bundle_hash(case, mode, nsteps)), "stride": np.array(stride),
-                "mode": np.array(mode), "nsteps": np.array(nsteps), "config": np.array(cfg)}
+                "mode": np.array(mode), "nsteps": np.array(nsteps), "config": np.array(cfg),
+                "overrides": np.array(json.dumps(ov))}
         if mode == "rhs":
             keep["rhs"] = out["rhs"]
         keep["qb_df"] = out["qb_df"][:, ::stride]
@@ -67,4 +91,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:] or None)

@@ -157,11 +157,19 @@ def test_shear_stress_reference_corrector_is_nonfinite(case_factory):
     e.close()
 
 
-@pytest.mark.parametrize("name", ["bump10_step2", "lake10_step1", "dg25_step1", "dg25L3_step1", "bump10q_step1",
-                                  "dg8L3q_step1"])
+GOLDEN_STEPS = ["bump10_step2", "lake10_step1", "dg25_step1", "dg25L3_step1", "bump10q_step1", "dg8L3q_step1",
+                "dg8N7L3_step1", "bump10_b2ns_step1", "bump10_mixed_step1", "lake10L3_step1", "bump10q_ns_step1",
+                "dg8L3q_mixed_step1"]
+
+
+@pytest.mark.parametrize("name", GOLDEN_STEPS)
 def test_engine_matches_reference_golden(name, case_factory, engines):
+    """The engine against the reference Fortran's own outputs (tests/golden, made by
+    tests/golden/make_golden.py), incl. N=7 and the branches the shipped namelists do not run:
+    quadratic drag (botfr=2), no-slip (2) and mixed walls, the 3-layer lake."""
+    from util import overrides_of
     g = dict(np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False))
-    case = case_factory(str(g["config"]))
+    case = case_factory(str(g["config"]), **overrides_of(g))
     e = get_engine(engines, case)
     q, qb, qp = e.state()
     for _ in range(int(g["nsteps"])):
@@ -170,6 +178,44 @@ def test_engine_matches_reference_golden(name, case_factory, engines):
     for k, a in [("q_df", q[:, ::s, :]), ("qprime_df", qp[:, ::s, :]), ("qb_df", qb[:, ::s])]:
         for v in range(a.shape[0]):
             assert rel(a[v], g[k][v]) < TOL, (k, v, rel(a[v], g[k][v]))
+    # the engine reproduces the reference arithmetic: the state is bit-identical
+    assert np.array_equal(q[:, ::s, :], g["q_df"]) and np.array_equal(qb[:, ::s], g["qb_df"])
+    assert np.array_equal(qp[:, ::s, :], g["qprime_df"])
+
+
+BRANCH_VARIANTS = {
+    "botfr2_noslip": ("bump10", dict(botfr=2, cd=1e-3, visc=25.0, method_visc=3, y_boundary=(2, 2))),
+    "beta_mixed": ("bump10", dict(botfr=1, cd=1e-7, f0=1e-4, beta=1e-11, x_boundary=(2, 4))),
+    "lake_L3": ("lake10", dict(nlayers=3)),
+    "quadldg_noslip_botfr2": ("bump10q", dict(y_boundary=(2, 2), botfr=2, cd=1e-3)),
+    "dg_L3_mixed": ("dg8L3q", dict(x_boundary=(2, 4))),
+    "dg_L3_noslip_botfr2": ("dg8L3q", dict(method_visc=3, botfr=2, cd=1e-3, x_boundary=(2, 2), y_boundary=(2, 2))),
+}
+
+
+@pytest.mark.parametrize("variant", sorted(BRANCH_VARIANTS))
+def test_branch_variants_bitwise(variant, case_factory):
+    """Shipped-code branches no shipped namelist runs (mod_rhs_btp.F90:163-168 quadratic drag;
+    mod_barotropic_terms.F90:89-90 / mod_laplacian_quad.F90 no-slip walls; mixed walls; a
+    3-layer lake): engine == oracle bit for bit over 2 baroclinic steps, every time average
+    included (the oracle is pinned to the reference on these, tests/test_oracle.py)."""
+    import oracle as O
+    from hnumo import bundle as B
+    from hnumo.engine import Engine
+    name, ov = BRANCH_VARIANTS[variant]
+    case = case_factory(name, **ov)
+    o = O.Oracle(case)
+    e = Engine(case)
+    q, qb, qp = o.state()
+    qe, qbe, qpe = e.state()
+    for _ in range(2):
+        o.ti_rk_bcl(q, qb, qp)
+        e.ti_rk_bcl(qe, qbe, qpe)
+    assert np.isfinite(q).all() and np.isfinite(qb).all()
+    assert np.array_equal(qe, q) and np.array_equal(qbe, qb) and np.array_equal(qpe, qp)
+    for f, _ in B.FIELDS:
+        assert np.array_equal(e.field(f), o.field(f)), f
+    e.close()
 
 
 def test_n7_step_parity(case_factory):

@@ -12,11 +12,17 @@ from util import layer_mass
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = os.path.join(HERE, "golden")
 GOLDEN = ["bump10_rhs", "bump10_btp", "bump10_step2", "lake10_step1", "dg25_step1", "dg25L3_step1",
-          "bump10q_step1", "dg8L3q_step1"]
+          "bump10q_step1", "dg8L3q_step1", "dg8N7L3_step1", "bump10_b2ns_step1", "bump10_mixed_step1",
+          "lake10L3_step1", "bump10q_ns_step1", "dg8L3q_mixed_step1"]
 
 
 def load(name):
     return dict(np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False))
+
+
+def golden_case(g, case_factory):
+    from util import overrides_of
+    return case_factory(str(g["config"]), **overrides_of(g))
 
 
 def bundle_hash(case, mode, nsteps):
@@ -27,12 +33,13 @@ def bundle_hash(case, mode, nsteps):
         return hashlib.sha256(open(p, "rb").read()).hexdigest()
 
 
-def test_basis_matches_reference_bitwise():
+@pytest.mark.parametrize("fixture,nop", [("bump10_rhs", 4), ("dg8N7L3_step1", 7)])
+def test_basis_matches_reference_bitwise(fixture, nop):
     """LGL nodes/weights and the interpolation/derivative tables equal the reference's
-    mod_basis_create output (mod_basis.F90:60-186) bit for bit."""
+    mod_basis_create output (mod_basis.F90:60-186) bit for bit, at N=4 and N=7."""
     from hnumo.basis import Basis
-    g = load("bump10_rhs")
-    b = Basis(4)
+    g = load(fixture)
+    b = Basis(nop)
     for k, v in [("xgl", b.xgl), ("wgl", b.wgl), ("xnq", b.xnq), ("wnq", b.wnq), ("psiq", b.psiq),
                  ("dpsiq", b.dpsiq), ("dpsi", b.dpsi)]:
         assert np.array_equal(g["ref_" + k], v), k
@@ -42,8 +49,8 @@ def test_basis_matches_reference_bitwise():
 def test_oracle_matches_golden(name, case_factory):
     import oracle as O
     g = load(name)
-    cfg, mode, nsteps, stride = str(g["config"]), str(g["mode"]), int(g["nsteps"]), int(g["stride"])
-    case = case_factory(cfg)
+    mode, nsteps, stride = str(g["mode"]), int(g["nsteps"]), int(g["stride"])
+    case = golden_case(g, case_factory)
     assert bundle_hash(case, mode, nsteps) == str(g["bundle_sha256"]), "setup inputs changed: regenerate golden"
     o = O.Oracle(case)
     q, qb, qp = o.state()

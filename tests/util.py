@@ -16,3 +16,11 @@ def layer_mass(case, q_df):
     A, S = case.arrays, case.scalars
     w = A["jac"].reshape(-1, order="F")
     return np.array([np.sum(w * (A["alpha"][k] / S["gravity"]) * q_df[0, :, k]) for k in range(S["nlayers"])])
+
+
+def overrides_of(g) -> dict:
+    """Config overrides stored in a golden fixture (JSON; lists back to tuples)."""
+    import json
+    if "overrides" not in g:
+        return {}
+    return {k: tuple(v) if isinstance(v, list) else v for k, v in json.loads(str(g["overrides"])).items()}
