@@ -95,6 +95,27 @@ struct hnumo_engine {
   unsigned long long *epoch = nullptr;        // tag epoch, bumped before every persistent sub-cycle
   StageArgs *d_stages[2] = {nullptr, nullptr};  // per-stage arguments: predictor (qp), corrector (qp2)
   int sub_final = 0;                          // qbuf index holding the sub-cycle result
+  // processor-face halo: the reference's own partition contract (face(8) = 0 faces listed per
+  // neighbour rank in nbh_send_recv; p4est.c:1686-1712, mod_parallel).  NS shared-face slots in
+  // list order; neighbour j owns slots [off, off+n).  Stage traces move between the trace
+  // buffers' send / receive slots (no packing); the baroclinic face exchanges pack side 1 of
+  // the listed faces and unpack the neighbour's into side 2.
+  bool face_halo = false;
+  int NS = 0;
+  struct FNbr {
+    int rank = -1, off = 0, n = 0;
+  };
+  std::vector<FNbr> fnb;
+  int *d_sface = nullptr;                    // [NS] local face of each shared slot
+  double *bx_sbuf = nullptr, *bx_rbuf = nullptr;  // [NS * per-face message] baroclinic exchanges
+  size_t bx_per_max = 0;
+  int *d_elB = nullptr, *d_elI = nullptr;    // elements with / without a processor face
+  int nB = 0, nI = 0;
+  double *cdef = nullptr;                    // consistency deficits [L][side][2][F*NQ]
+  hipStream_t stream2 = nullptr;             // boundary elements + trace transport (two-stream schedule)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_I = nullptr, ev_B[2] = {nullptr, nullptr};
+  // local exchange group, processor-face transport: device copies ordered by events
+  hipEvent_t ev_tsent = nullptr, ev_bpacked = nullptr, ev_bdone = nullptr;
   // method_visc == 1 (quad-point LDG, kernels_lapq.hip)
   bool lapq_on = false;
   double *dpq = nullptr;      // dpprime_visc_q [L][npoin_q]
@@ -115,17 +136,23 @@ static T *dalloc(hnumo_engine *eng, size_t n) {
   return (T *)ptr;
 }
 
+static void face_exchange_qf(hnumo_engine *e, double *qf, int nc);
+static void face_exchange_gdpp(hnumo_engine *e);
+static void face_exchange_cdef(hnumo_engine *e);
+
 // ------------------------------------------------------------------ kernel dispatch
 template <int NGL, int NQ>
 struct Launch {
   static constexpr int BSE = ((NQ * NQ + 63) / 64) * 64;
-  static void stage(hnumo_engine *e, const StageArgs &a) {
+  // one stage over the owned elements, or over the `n` elements of a.elist on stream `st`
+  static void stage(hnumo_engine *e, const StageArgs &a, int n = -1, hipStream_t st = nullptr) {
+    if (n < 0) n = e->nelem_owned;
+    if (!st) st = e->stream;
+    if (n == 0) return;
     if (e->summation == HNUMO_SUM_REFERENCE)
-      hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false>), dim3(e->nelem_owned), dim3(StageCfg<NGL, NQ, false>::BS),
-                         0, e->stream, a);
+      hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false>), dim3(n), dim3(StageCfg<NGL, NQ, false>::BS), 0, st, a);
     else
-      hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, true>), dim3(e->nelem_owned), dim3(StageCfg<NGL, NQ, true>::BS), 0,
-                         e->stream, a);
+      hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, true>), dim3(n), dim3(StageCfg<NGL, NQ, true>::BS), 0, st, a);
   }
   static void subcycle(hnumo_engine *e, const StageArgs *stages, int ns) {
     SubArgs sa{stages, ns, e->epoch};
@@ -153,16 +180,25 @@ struct Launch {
       hipLaunchKernelGGL((grad_trace_kernel<NGL, NQ>), dim3(n), dim3(64), 0, e->stream, e->m, qb, gt, e0, gtr,
                          e->epoch);
   }
+  // extract_qprime_df_face / extract_dprime_df_face + bcl_create_communicator (ti_rk_bcl.F90:43-44,
+  // :62, :75-76): processor faces take the neighbour's side 1 as their side 2
   static void extract(hnumo_engine *e, const double *qp, double *qf, int only_dp) {
     size_t n = (size_t)e->nface * NGL;
     hipLaunchKernelGGL((extract_face_kernel<NGL>), dim3((n + 255) / 256), dim3(256), 0, e->stream, e->m, qp, qf,
                        only_dp);
+    face_exchange_qf(e, qf, only_dp ? 1 : 3);
   }
   static void bcl_coeffs(hnumo_engine *e, const double *qp, const double *qf) {
     hipLaunchKernelGGL((bcl_coeffs_elem_kernel<NGL, NQ>), dim3(e->nelem), dim3(BSE), 0, e->stream, e->m, qp,
                        e->qcoef, e->ncoef, e->dpp_graduv, e->dpprime_visc, e->ecoef);
     hipLaunchKernelGGL((bcl_coeffs_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf,
                        e->dpp_graduv, e->dpprime_visc, e->fcoef, e->fncoef, e->gdpp_face, e->efcoef);
+    if (e->face_halo) {  // graduv_dpp_face halo (mod_barotropic_terms.F90:393) and its layer sums
+      face_exchange_gdpp(e);
+      if (e->NS)
+        hipLaunchKernelGGL((bcl_coeffs_proc_kernel<NGL, NQ>), dim3((e->NS * NGL + 63) / 64), dim3(64), 0, e->stream, e->m,
+                         e->gdpp_face, e->d_sface, e->NS, e->fncoef, e->efcoef);
+    }
     if (e->lapq_on)  // interpolate_dpp right after dpprime_visc is set (ti_rk_bcl.F90:48,67)
       hipLaunchKernelGGL((lapq_dpp_kernel<NGL, NQ>), dim3(std::min<size_t>(((size_t)e->L * e->npq + 255) / 256, 4096)),
                          dim3(256), 0, e->stream, e->m, e->dpprime_visc, e->dpq);
@@ -190,7 +226,13 @@ struct Launch {
   }
   static void cons(hnumo_engine *e, double *q, double *qp_out, int finalize_dp) {
     hipLaunchKernelGGL((cons_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, e->dpp,
-                       e->facc, e->slmf_face, e->fcons);
+                       e->facc, e->slmf_face, e->fcons, e->face_halo ? e->cdef : nullptr);
+    if (e->face_halo) {  // mass_deficit_mass_face halo (mod_layer_terms.F90:135)
+      face_exchange_cdef(e);
+      if (e->NS)
+        hipLaunchKernelGGL((cons_flux_proc_kernel<NQ>), dim3((e->NS * NQ + 63) / 64), dim3(64), 0, e->stream, e->m,
+                         e->cdef, e->d_sface, e->NS, e->fcons);
+    }
     hipLaunchKernelGGL((cons_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(BSE), 0, e->stream, e->m, e->dpp,
                        e->qacc, e->slmf, e->fcons, q, qp_out, finalize_dp);
   }
@@ -312,7 +354,7 @@ static void nccl_check(hnumo_engine *e, ncclResult_t r, const char *what) {
 
 // refresh the ghost elements' block of `base` from their owners
 static void exchange(hnumo_engine *e, double *base, int ncomp, int nblk, size_t stride) {
-  if (e->comm_mode == 0) return;
+  if (e->comm_mode == 0 || e->face_halo) return;
   const int per = e->P * ncomp;
   for (auto &n : e->nbh)
     if (n.nsend) {
@@ -353,6 +395,111 @@ static void exchange(hnumo_engine *e, double *base, int ncomp, int nblk, size_t 
 static void exchange_qb(hnumo_engine *e, double *qb) { exchange(e, qb, 4, 1, 0); }
 static void exchange_qp(hnumo_engine *e, double *qp) { exchange(e, qp, 3, e->L, 3 * (size_t)e->npoin); }
 static void exchange_dpp(hnumo_engine *e) { exchange(e, e->dpp, 1, e->L, (size_t)e->npoin); }
+
+// ------------------------------------------------------------------ processor-face exchanges
+// The peer engine of a local group holding rank r.
+static hnumo_engine *group_peer(hnumo_engine *e, int r) { return e->group->eng[r]; }
+static const hnumo_engine::FNbr *peer_entry(hnumo_engine *peer, int rank) {
+  for (auto &n : peer->fnb)
+    if (n.rank == rank) return &n;
+  return nullptr;
+}
+
+// Baroclinic face exchange on the engine stream (bcl_create_communicator,
+// create_rhs_communicator.F90:384-438): side 1 of every shared face -> the neighbour's side 2.
+// Face array element (side 1) of layer k, component c < nc, point p < nn of face f:
+// base[k*sk + c*sc + f*sf + p*sn]; side 2 at + s2.
+static void face_exchange(hnumo_engine *e, double *base, int nc, int nn, size_t sk, size_t sc, size_t sf, size_t sn,
+                          size_t s2) {
+  // (a rank without shared faces still takes part in a local group's barriers)
+  if (!e->face_halo || (e->NS == 0 && e->comm_mode != 1)) return;
+  const int L = e->L;
+  const size_t per = (size_t)L * nc * nn, tot = per * e->NS;
+  const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>((tot + 255) / 256, 1024));
+  if (e->comm_mode == 1) {  // local group: my previous message must have been read by every peer
+    for (auto &n : e->fnb) (void)hipStreamWaitEvent(e->stream, group_peer(e, n.rank)->ev_bdone, 0);
+  }
+  if (tot)
+    hipLaunchKernelGGL(face_pack_kernel, dim3(blocks), dim3(256), 0, e->stream, e->bx_sbuf, base, e->d_sface, e->NS,
+                       L, nc, nn, sk, sc, sf, sn);
+  if (e->comm_mode == 2) {
+    nccl_check(e, ncclGroupStart(), "ncclGroupStart");
+    for (auto &n : e->fnb) {
+      nccl_check(e, ncclSend(e->bx_sbuf + per * n.off, per * n.n, ncclDouble, n.rank, e->comm, e->stream), "ncclSend");
+      nccl_check(e, ncclRecv(e->bx_rbuf + per * n.off, per * n.n, ncclDouble, n.rank, e->comm, e->stream), "ncclRecv");
+    }
+    nccl_check(e, ncclGroupEnd(), "ncclGroupEnd");
+  } else {
+    (void)hipEventRecord(e->ev_bpacked, e->stream);
+    if (!e->group->barrier()) return;
+    for (auto &n : e->fnb) {
+      hnumo_engine *peer = group_peer(e, n.rank);
+      const hnumo_engine::FNbr *pn = peer_entry(peer, e->rank);
+      if (!pn || pn->n != n.n) {
+        e->comm_err = "local group: neighbour lists of two ranks disagree";
+        continue;
+      }
+      (void)hipStreamWaitEvent(e->stream, peer->ev_bpacked, 0);
+      if (hipMemcpyAsync(e->bx_rbuf + per * n.off, peer->bx_sbuf + per * pn->off, per * n.n * sizeof(double),
+                         hipMemcpyDeviceToDevice, e->stream) != hipSuccess)
+        e->comm_err = "local group: hipMemcpyAsync of a face message failed";
+    }
+    (void)hipEventRecord(e->ev_bdone, e->stream);
+    if (!e->group->barrier()) return;
+  }
+  if (tot)
+    hipLaunchKernelGGL(face_unpack_kernel, dim3(blocks), dim3(256), 0, e->stream, base, e->bx_rbuf, e->d_sface,
+                       e->NS, L, nc, nn, sk, sc, sf, sn, s2);
+}
+
+// qprime_df_face-like arrays qf(3,2,ngl,F,L) (QF macro): components [0,nc)
+static void face_exchange_qf(hnumo_engine *e, double *qf, int nc) {
+  const size_t F = e->nface, N = e->ngl;
+  face_exchange(e, qf, nc, e->ngl, F * N * 6, 1, N * 6, 6, 3);
+}
+// graduv_dpp_face [L][10][F*NGL]: components 0..4 (side 1) -> 5..9 (side 2)
+static void face_exchange_gdpp(hnumo_engine *e) {
+  face_exchange(e, e->gdpp_face, 5, e->ngl, 10 * e->FN, e->FN, e->ngl, 1, 5 * e->FN);
+}
+// mass_deficit_mass_face [L][side][2][F*NQ]
+static void face_exchange_cdef(hnumo_engine *e) {
+  face_exchange(e, e->cdef, 2, e->nq, 4 * e->FQ, e->FQ, e->nq, 1, 2 * e->FQ);
+}
+
+// Stage-trace exchange (btp_create_pre/postcommunicator + create_rhs_lap_pre/postcommunicator_df,
+// one message for both: qb(4) and grad(u_bar)(4) at the face nodes) on stream `st`: the send
+// slots [4E, 4E+NS) of trace buffer `tb` go to the neighbours' receive slots [4E+NS, 4E+2NS).
+static void trace_exchange(hnumo_engine *e, double *tb, hipStream_t st) {
+  if (!e->face_halo || (e->NS == 0 && e->comm_mode != 1)) return;
+  const size_t slot = 8 * (size_t)e->ngl, s0 = 4 * (size_t)e->nelem, r0 = s0 + e->NS;
+  if (e->comm_mode == 2) {
+    nccl_check(e, ncclGroupStart(), "ncclGroupStart");
+    for (auto &n : e->fnb) {
+      nccl_check(e, ncclSend(tb + (s0 + n.off) * slot, slot * n.n, ncclDouble, n.rank, e->comm, st), "ncclSend");
+      nccl_check(e, ncclRecv(tb + (r0 + n.off) * slot, slot * n.n, ncclDouble, n.rank, e->comm, st), "ncclRecv");
+    }
+    nccl_check(e, ncclGroupEnd(), "ncclGroupEnd");
+    return;
+  }
+  // local group: every engine runs the same stage sequence, so the peer's buffer of the same
+  // index holds the traces of the same stage
+  const int bi = tb == e->gtrace[0] ? 0 : 1;
+  (void)hipEventRecord(e->ev_tsent, st);
+  if (!e->group->barrier()) return;
+  for (auto &n : e->fnb) {
+    hnumo_engine *peer = group_peer(e, n.rank);
+    const hnumo_engine::FNbr *pn = peer_entry(peer, e->rank);
+    if (!pn || pn->n != n.n) {
+      e->comm_err = "local group: neighbour lists of two ranks disagree";
+      continue;
+    }
+    (void)hipStreamWaitEvent(st, peer->ev_tsent, 0);
+    if (hipMemcpyAsync(tb + (r0 + n.off) * slot, peer->gtrace[bi] + (4 * (size_t)peer->nelem + pn->off) * slot,
+                       slot * n.n * sizeof(double), hipMemcpyDeviceToDevice, st) != hipSuccess)
+      e->comm_err = "local group: hipMemcpyAsync of a trace message failed";
+  }
+  (void)e->group->barrier();
+}
 
 
 static void launch_copy(hnumo_engine *e, double *dst, const double *src, size_t n) {
@@ -475,6 +622,35 @@ static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp,
     DISPATCH(e, subcycle(e, e->d_stages[qp == e->qp ? 0 : 1], K * NB));
     if (timed && e->kernel_events) (void)hipEventRecord(e->evk1, e->stream);
     cur = e->sub_final;
+  } else if (e->face_halo) {
+    // Processor-face halo, two streams (the overlap of mod_rhs_btp.F90:40-46): elements with a
+    // processor face ("boundary", B) run on stream2, which then ships their new face traces to
+    // the neighbours; the interior elements (I) run on the engine stream meanwhile.  Stage s:
+    //   B_s waits for I_{s-1} (its interior neighbours' traces); the transport of stage s-1
+    //       precedes it on stream2;
+    //   I_s waits for B_{s-1} only -- never for the transport, which overlaps I_s.
+    trace_exchange(e, e->gtrace[0], e->stream);  // the sub-cycle input's traces (grad_trace above)
+    std::vector<StageArgs> st;
+    cur = stage_table(e, qp, st);
+    if (timed && e->kernel_events) (void)hipEventRecord(e->evk0, e->stream);
+    (void)hipEventRecord(e->ev_fork, e->stream);
+    (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
+    (void)hipEventRecord(e->ev_I, e->stream);
+    for (size_t i = 0; i < st.size(); i++) {
+      StageArgs a = st[i];
+      (void)hipStreamWaitEvent(e->stream2, e->ev_I, 0);
+      a.elist = e->d_elB;
+      DISPATCH(e, stage(e, a, e->nB, e->stream2));
+      (void)hipEventRecord(e->ev_B[i & 1], e->stream2);
+      if (a.write_trace) trace_exchange(e, a.trace_out, e->stream2);
+      if (i > 0) (void)hipStreamWaitEvent(e->stream, e->ev_B[(i - 1) & 1], 0);
+      a.elist = e->d_elI;
+      DISPATCH(e, stage(e, a, e->nI, e->stream));
+      (void)hipEventRecord(e->ev_I, e->stream);
+    }
+    (void)hipEventRecord(e->ev_join, e->stream2);
+    (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
+    if (timed && e->kernel_events) (void)hipEventRecord(e->evk1, e->stream);
   } else {
     std::vector<StageArgs> st;
     cur = stage_table(e, qp, st);
@@ -567,6 +743,10 @@ void hnumo_engine_destroy(hnumo_engine *eng) {
   if (eng->ev1) (void)hipEventDestroy(eng->ev1);
   if (eng->evk0) (void)hipEventDestroy(eng->evk0);
   if (eng->evk1) (void)hipEventDestroy(eng->evk1);
+  for (hipEvent_t ev : {eng->ev_fork, eng->ev_join, eng->ev_I, eng->ev_B[0], eng->ev_B[1], eng->ev_tsent,
+                        eng->ev_bpacked, eng->ev_bdone})
+    if (ev) (void)hipEventDestroy(ev);
+  if (eng->stream2) (void)hipStreamDestroy(eng->stream2);
   delete eng;
 }
 
@@ -581,13 +761,54 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   *out = eng;
   eng->device = device;
   if (!mesh || !st || !par) return fail(eng, HNUMO_ERR_INVALID, "null descriptor");
+  // multi-rank: the reference's processor-face lists (num_send_recv / nbh_send_recv), or the
+  // ghost-element lists (num_ghost_send / num_ghost_recv) -- one of the two
+  std::vector<int> sface;                 // processor-face halo: shared slot -> local face
+  std::vector<int> face_slot(mesh->nface > 0 ? mesh->nface : 0, -1);
   if (halo && halo->nranks > 1) {
     if (halo->rank < 0 || halo->rank >= halo->nranks) return fail(eng, HNUMO_ERR_INVALID, "bad rank");
-    if (halo->nelem_owned < 1 || halo->nelem_owned > mesh->nelem)
-      return fail(eng, HNUMO_ERR_INVALID, "nelem_owned must be in 1..nelem (owned elements first)");
-    for (int k = 0; k < halo->num_nbh; k++)
-      if (halo->num_send_recv && halo->num_send_recv[k] > 0)
-        return fail(eng, HNUMO_ERR_INVALID, "processor-face halos are not supported: use the ghost-element lists");
+    bool any_face = false, any_ghost = false;
+    for (int k = 0; k < halo->num_nbh; k++) {
+      if (halo->num_send_recv && halo->num_send_recv[k] > 0) any_face = true;
+      if ((halo->num_ghost_send && halo->num_ghost_send[k] > 0) || (halo->num_ghost_recv && halo->num_ghost_recv[k] > 0))
+        any_ghost = true;
+    }
+    if (any_face && any_ghost)
+      return fail(eng, HNUMO_ERR_INVALID, "give either processor-face lists or ghost-element lists, not both");
+    if (any_face) {
+      eng->face_halo = true;
+      if (halo->nelem_owned != 0 && halo->nelem_owned != mesh->nelem)
+        return fail(eng, HNUMO_ERR_INVALID, "processor-face halo: every local element is owned (nelem_owned = nelem)");
+      if (!halo->nbh_proc || !halo->num_send_recv || !halo->nbh_send_recv)
+        return fail(eng, HNUMO_ERR_INVALID, "processor-face halo needs nbh_proc, num_send_recv, nbh_send_recv");
+      size_t o = 0;
+      for (int k = 0; k < halo->num_nbh; k++) {
+        hnumo_engine::FNbr nb;
+        nb.rank = halo->nbh_proc[k] - 1;  // mod_parallel nbh_proc is 1-based (p4est.c:1357)
+        nb.off = (int)sface.size();
+        nb.n = halo->num_send_recv[k];
+        if (nb.rank < 0 || nb.rank >= halo->nranks || nb.rank == halo->rank)
+          return fail(eng, HNUMO_ERR_INVALID, "nbh_proc: bad neighbour rank (1-based ranks expected)");
+        if (nb.n < 0) return fail(eng, HNUMO_ERR_INVALID, "num_send_recv < 0");
+        for (int i = 0; i < nb.n; i++) {
+          const int f = halo->nbh_send_recv[o + i] - 1;
+          if (f < 0 || f >= mesh->nface) return fail(eng, HNUMO_ERR_INVALID, "nbh_send_recv: face id out of range");
+          if (mesh->face[8 * f + 7] != 0)
+            return fail(eng, HNUMO_ERR_INVALID, "nbh_send_recv lists a face whose face(8) is not 0 (not a processor face)");
+          if (face_slot[f] >= 0)
+            return fail(eng, HNUMO_ERR_INVALID,
+                        "a processor face is listed twice (non-conforming multiplicity > 1 is not supported)");
+          face_slot[f] = (int)sface.size();
+          sface.push_back(f);
+        }
+        o += nb.n;
+        eng->fnb.push_back(nb);
+      }
+      eng->NS = (int)sface.size();
+    } else {
+      if (halo->nelem_owned < 1 || halo->nelem_owned > mesh->nelem)
+        return fail(eng, HNUMO_ERR_INVALID, "nelem_owned must be in 1..nelem (owned elements first)");
+    }
   }
   if (par->method_visc == 1) {
     if (!mesh->imapl_q || !mesh->imapr_q) return fail(eng, HNUMO_ERR_INVALID, "method_visc==1 needs imapl_q/imapr_q");
@@ -611,7 +832,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   if (mesh->npoin != E * P || mesh->npoin_q != E * Q) return fail(eng, HNUMO_ERR_INVALID, "npoin/npoin_q mismatch");
   eng->nelem = E; eng->npoin = E * P; eng->npq = E * Q; eng->nface = F; eng->ngl = ngl; eng->nq = nq;
   eng->L = L; eng->P = P; eng->Q = Q; eng->K = par->kstages;
-  eng->nelem_owned = (halo && halo->nranks > 1) ? halo->nelem_owned : E;
+  eng->nelem_owned = (halo && halo->nranks > 1 && !eng->face_halo) ? halo->nelem_owned : E;
   const int EO = eng->nelem_owned;
   eng->FQ = (size_t)F * nq; eng->FN = (size_t)F * ngl;
   const size_t npoin = eng->npoin, npq = eng->npq, FQ = eng->FQ, FN = eng->FN;
@@ -625,8 +846,9 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     if (er > 0) {
       if (er > E) return fail(eng, HNUMO_ERR_INVALID, "face(8) out of range");
       ef[er - 1].push_back({f, 1});
-    } else if (er == 0) {
-      return fail(eng, HNUMO_ERR_INVALID, "processor faces need a halo (multi-rank) description");
+    } else if (er == 0 && face_slot[f] < 0) {
+      return fail(eng, HNUMO_ERR_INVALID,
+                  "face(8) = 0 (processor face) but the face is not in the halo's nbh_send_recv lists");
     }
   }
   auto lnode = [&](const int32_t *imap, int f, int n) {
@@ -654,6 +876,12 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
           if (ef[nb][k].first == f) enbr_lf[4 * e + lf] = k;
         for (int n = 0; n < ngl; n++)
           enbr_node[(4 * e + lf) * ngl + n] = nb * P + lnode(s == 0 ? mesh->imapr : mesh->imapl, f, n);
+      } else if (er == 0) {
+        // processor face: the stage writes this face's traces into send slot 4E + s of the
+        // trace buffer, i.e. "element" E + s/4, local face s%4
+        const int sl = face_slot[f];
+        enbr_e[4 * e + lf] = E + sl / 4;
+        enbr_lf[4 * e + lf] = sl % 4;
       }
     }
   for (int f = 0; f < F; f++) {
@@ -840,7 +1068,8 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   eng->qf = dalloc<double>(eng, 6 * FN * L); eng->qf2 = dalloc<double>(eng, 6 * FN * L);
   eng->dpp2 = dalloc<double>(eng, npoin * L);
   for (int i = 0; i < 4; i++) eng->qbuf[i] = dalloc<double>(eng, 4 * npoin);
-  for (int i = 0; i < 2; i++) eng->gtrace[i] = dalloc<double>(eng, (size_t)E * 32 * ngl);
+  // trace buffers: element slots [4E], then (processor-face halo) NS send + NS receive slots
+  for (int i = 0; i < 2; i++) eng->gtrace[i] = dalloc<double>(eng, (4 * (size_t)E + 2 * (size_t)eng->NS) * 8 * ngl);
   eng->qcoef = dalloc<double>(eng, QC_N * npq); eng->ncoef = dalloc<double>(eng, NC_N * npoin);
   eng->fcoef = dalloc<double>(eng, FC_N * FQ); eng->fncoef = dalloc<double>(eng, 10 * FN);
   eng->dpp_graduv = dalloc<double>(eng, 4 * npoin * L); eng->dpprime_visc = dalloc<double>(eng, npoin * L);
@@ -879,7 +1108,51 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   if (const char *sd = getenv("HNUMO_STAGE_DBG")) eng->stage_dbg = atoi(sd);
   if (const char *sp = getenv("HNUMO_STAGE_PROF"))
     if (sp[0] == '1') eng->stage_prof = dalloc<unsigned long long>(eng, (size_t)eng->nelem * 32);
-  if (halo && halo->nranks > 1) {
+  if (halo && halo->nranks > 1 && eng->face_halo) {
+    eng->rank = halo->rank;
+    eng->nranks = halo->nranks;
+    const int NS = eng->NS;
+    // trace source slot of every element face; boundary / interior element lists
+    std::vector<int> tsrc(4 * (size_t)E), elB, elI;
+    for (int e = 0; e < E; e++) {
+      bool bnd = false;
+      for (int lf = 0; lf < 4; lf++) {
+        const int f = efaces[4 * e + lf];
+        const bool proc = ebc[4 * e + lf] == 0;
+        tsrc[4 * e + lf] = proc ? 4 * E + NS + face_slot[f] : 4 * e + lf;
+        bnd |= proc;
+      }
+      (bnd ? elB : elI).push_back(e);
+    }
+    eng->nB = (int)elB.size();
+    eng->nI = (int)elI.size();
+    int *d_tsrc = dalloc<int>(eng, tsrc.size());
+    eng->d_sface = dalloc<int>(eng, NS);
+    eng->d_elB = dalloc<int>(eng, elB.size());
+    eng->d_elI = dalloc<int>(eng, elI.size());
+    eng->cdef = dalloc<double>(eng, 4 * FQ * L);
+    eng->bx_per_max = (size_t)L * std::max(5 * ngl, 2 * nq);
+    eng->bx_sbuf = dalloc<double>(eng, eng->bx_per_max * NS);
+    eng->bx_rbuf = dalloc<double>(eng, eng->bx_per_max * NS);
+    if (eng->alloc_failed) return fail(eng, HNUMO_ERR_DEVICE, "hipMalloc failed (halo buffers)");
+    HIPCHK(hipMemcpy(d_tsrc, tsrc.data(), tsrc.size() * sizeof(int), hipMemcpyHostToDevice));
+    if (NS) HIPCHK(hipMemcpy(eng->d_sface, sface.data(), NS * sizeof(int), hipMemcpyHostToDevice));
+    if (eng->nB) HIPCHK(hipMemcpy(eng->d_elB, elB.data(), elB.size() * sizeof(int), hipMemcpyHostToDevice));
+    if (eng->nI) HIPCHK(hipMemcpy(eng->d_elI, elI.data(), elI.size() * sizeof(int), hipMemcpyHostToDevice));
+    eng->m.etsrc = d_tsrc;
+    HIPCHK(hipStreamCreateWithFlags(&eng->stream2, hipStreamNonBlocking));
+    for (hipEvent_t *ev : {&eng->ev_fork, &eng->ev_join, &eng->ev_I, &eng->ev_B[0], &eng->ev_B[1], &eng->ev_tsent,
+                           &eng->ev_bpacked, &eng->ev_bdone})
+      HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    if (halo->comm_id) {  // RCCL point-to-point over xGMI
+      ncclUniqueId id;
+      static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
+      std::memcpy(&id, halo->comm_id, sizeof(id));
+      ncclResult_t nr = ncclCommInitRank(&eng->comm, halo->nranks, id, halo->rank);
+      if (nr != ncclSuccess) return fail(eng, HNUMO_ERR_DEVICE, std::string("ncclCommInitRank: ") + ncclGetErrorString(nr));
+      eng->comm_mode = 2;
+    }
+  } else if (halo && halo->nranks > 1) {
     eng->rank = halo->rank;
     eng->nranks = halo->nranks;
     size_t os = 0, orr = 0;
@@ -1139,6 +1412,7 @@ int hnumo_create_rhs_btp(hnumo_engine *eng, double *rhs, const double *qb_df, co
   if (rc) return rc;
   subcycle_prologue(eng, eng->qb, nullptr);  // zeroed time averages (qbuf[0] is the rhs-only output slot)
   DISPATCH(eng, grad_trace(eng, eng->qb, eng->gtrace[0], 0, eng->nelem));
+  trace_exchange(eng, eng->gtrace[0], eng->stream);
   StageArgs a{};
   a.m = eng->m;
   a.qb_in = eng->qb; a.qb0 = eng->qb; a.qb2 = eng->qb; a.qprime = eng->qp;
@@ -1378,16 +1652,23 @@ int hnumo_local_group(hnumo_engine **engines, int n) {
     if (!engines[i] || engines[i]->rank != i || engines[i]->nranks != n || engines[i]->comm_mode != 0 ||
         engines[i]->device != engines[0]->device)
       return HNUMO_ERR_INVALID;
+  for (int i = 0; i < n; i++)
+    if (engines[i]->face_halo != engines[0]->face_halo) return HNUMO_ERR_INVALID;
   LocalGroup *g = new LocalGroup();
   g->eng.assign(engines, engines + n);
-  g->stream = engines[0]->stream;  // the group owns engine 0's stream from now on
   g->refs = n;
+  // ghost-element halo: one shared stream orders every engine's packs, copies and unpacks;
+  // processor-face halo: each engine keeps its streams, the copies are ordered by events
+  const bool share = !engines[0]->face_halo;
+  if (share) g->stream = engines[0]->stream;  // the group owns engine 0's stream from now on
   for (int i = 0; i < n; i++) {
     hnumo_engine *e = engines[i];
     (void)hipSetDevice(e->device);
-    if (i > 0 && e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
-    e->stream = g->stream;
-    e->own_stream = false;
+    if (share) {
+      if (i > 0 && e->own_stream && e->stream) (void)hipStreamDestroy(e->stream);
+      e->stream = g->stream;
+      e->own_stream = false;
+    }
     e->group = g;
     e->comm_mode = 1;
   }

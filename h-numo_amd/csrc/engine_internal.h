@@ -12,7 +12,8 @@
 //   element->face    efaces[e][4], eside[e][4], ebc[e][4], efmap[e][4][NGL],
 //                    enbr_node[e][4][NGL], enbr_e[e][4], enbr_lf[e][4]
 //   face traces      trace[e][4][8][NGL]   (qb(4) and grad(u_bar)(4) of the neighbour at each
-//                    face node, written by the neighbour's stage into this element's slot)
+//                    face node, written by the neighbour's stage into this element's slot;
+//                    processor-face halo: + [NS] send slots + [NS] receive slots, see DevMesh)
 //
 // Element-major copies for the barotropic stage kernel (one contiguous record per element,
 // so a stage loads everything it needs with one round of async global->LDS copies):
@@ -109,6 +110,12 @@ struct DevMesh {
   int botfr;
   double ad, max_shear_dz;        // ad_mlswe, max_shear_dz (implicit vertical shear stress)
   int shear_corr;                 // hnumo_params.shear_corrector
+  // processor-face halo (NULL on a single rank / the ghost-element halo): per element and local
+  // face, the trace-buffer slot its neighbour trace arrives in -- e*4+lf, or for a processor
+  // face the receive slot 4E+NS+s of shared face s (the trace buffers are [4E + 2NS][8][NGL]:
+  // element slots, then the send slots the stage writes processor-face traces into, then the
+  // receive slots the transport fills)
+  const int *etsrc;
 };
 
 }  // namespace hnumo

@@ -359,9 +359,14 @@ __global__ void __launch_bounds__(64)
 // =============================================== consistency: face deficit fluxes
 // evaluate_consistency_face (mod_layer_terms.F90:57-137) + the upwind selection of
 // create_consistency_mass_flux (mod_create_rhs_mlswe.F90:1036-1115); dpp = dp'(npoin,L).
+// Processor-face halo (cdef != NULL): the side-1 deficits (m11, m21) of every face are kept in
+// cdef [L][side][2][F*NQ]; a processor face's side 2 is its neighbour's side 1, which only
+// arrives with the exchange (bcl_create_communicator at mod_layer_terms.F90:135), so its flux
+// is formed afterwards by cons_flux_proc_kernel.
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(64)
-    cons_flux_face_kernel(DevMesh m, const double *dpp, const double *facc, const double *slmf_face, double *fcons) {
+    cons_flux_face_kernel(DevMesh m, const double *dpp, const double *facc, const double *slmf_face, double *fcons,
+                          double *cdef) {
   const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L, npoin = m.npoin;
   __shared__ double s_psiq[NGL * NQ];
   for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
@@ -386,10 +391,83 @@ __global__ void __launch_bounds__(64)
       }
       double wl = ql / pbl, wr = qr / pbr;
       double m11 = wl * d1, m21 = wl * d2, m12 = wr * d1, m22 = wr * d2;
+      if (cdef) {
+        cdef[((size_t)k * 4 + 0) * FQ + fq] = m11;
+        cdef[((size_t)k * 4 + 1) * FQ + fq] = m21;
+        if (er == 0) continue;  // processor face: cons_flux_proc_kernel after the exchange
+      }
       double feu = (m11 * nxl > 0.0) ? m11 : m12;
       double fev = (m21 * nyl > 0.0) ? m21 : m22;
       fcons[(size_t)k * FQ + fq] = nxl * feu + nyl * fev;
     }
+  }
+}
+
+// create_consistency_mass_flux (mod_create_rhs_mlswe.F90:1036-1115) on the processor faces,
+// with side 2 = the neighbour's side-1 deficits received into cdef: one thread per
+// (shared face, quad point).
+template <int NQ>
+__global__ void cons_flux_proc_kernel(DevMesh m, const double *cdef, const int *sface, int NS, double *fcons) {
+  const int F = m.nface, L = m.L;
+  const size_t FQ = (size_t)F * NQ;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= NS * NQ) return;
+  const int f = sface[t / NQ], iq = t % NQ;
+  const size_t fq = (size_t)f * NQ + iq;
+  const double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
+  for (int k = 0; k < L; k++) {
+    const double m11 = cdef[((size_t)k * 4 + 0) * FQ + fq], m21 = cdef[((size_t)k * 4 + 1) * FQ + fq];
+    const double m12 = cdef[((size_t)k * 4 + 2) * FQ + fq], m22 = cdef[((size_t)k * 4 + 3) * FQ + fq];
+    const double feu = (m11 * nxl > 0.0) ? m11 : m12;
+    const double fev = (m21 * nyl > 0.0) ? m21 : m22;
+    fcons[(size_t)k * FQ + fq] = nxl * feu + nyl * fev;
+  }
+}
+
+// btp_graduv_dpp_face side 2 of the processor faces (mod_barotropic_terms.F90:395-407): the
+// layer sum of the received graduv_dpp_face (:393), into fncoef and the element-side copies.
+template <int NGL, int NQ>
+__global__ void bcl_coeffs_proc_kernel(DevMesh m, const double *gdpp_face, const int *sface, int NS, double *fncoef,
+                                       double *efcoef) {
+  const int F = m.nface, L = m.L;
+  const size_t FN = (size_t)F * NGL;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= NS * NGL) return;
+  const int f = sface[t / NGL], n = t % NGL;
+  const size_t fn = (size_t)f * NGL + n;
+  double bsum[5] = {0, 0, 0, 0, 0};
+  for (int k = 0; k < L; k++)
+    for (int c = 0; c < 5; c++) bsum[c] = bsum[c] + gdpp_face[((size_t)k * 10 + 5 + c) * FN + fn];
+  constexpr int EFC = 4 * NQ + 10 * NGL;
+  const int sl = m.fslotL[f];
+  for (int c = 0; c < 5; c++) {
+    fncoef[(size_t)(5 + c) * FN + fn] = bsum[c];
+    efcoef[(size_t)sl * EFC + 4 * NQ + (5 + c) * NGL + n] = bsum[c];
+  }
+}
+
+// Pack / unpack of a face array for the processor-face exchange (send_receive_bound.F90:272-327
+// pack_data_dg_*, create_rhs_dynamics_flux.F90:104-182 create_nbhs_face_*): for shared face s
+// (face sface[s]), layer k, component c < nc, point n < nn, element
+//   base[k*sk + c*sc + f*sf + n*sn]  (side 1)  ->  buf[((s*L + k)*nc + c)*nn + n]
+// and back into base[s2 + ...] (side 2).  The message of neighbour j is the slice of its
+// faces (contiguous in list order).
+__global__ void face_pack_kernel(double *buf, const double *base, const int *sface, int NS, int L, int nc, int nn,
+                                 size_t sk, size_t sc, size_t sf, size_t sn) {
+  const size_t n = (size_t)NS * L * nc * nn, st = (size_t)gridDim.x * blockDim.x;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += st) {
+    const int p = (int)(t % nn), c = (int)((t / nn) % nc), k = (int)((t / ((size_t)nn * nc)) % L);
+    const int s = (int)(t / ((size_t)nn * nc * L));
+    buf[t] = base[k * sk + c * sc + (size_t)sface[s] * sf + p * sn];
+  }
+}
+__global__ void face_unpack_kernel(double *base, const double *buf, const int *sface, int NS, int L, int nc, int nn,
+                                   size_t sk, size_t sc, size_t sf, size_t sn, size_t s2) {
+  const size_t n = (size_t)NS * L * nc * nn, st = (size_t)gridDim.x * blockDim.x;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += st) {
+    const int p = (int)(t % nn), c = (int)((t / nn) % nc), k = (int)((t / ((size_t)nn * nc)) % L);
+    const int s = (int)(t / ((size_t)nn * nc * L));
+    base[s2 + k * sk + c * sc + (size_t)sface[s] * sf + p * sn] = buf[t];
   }
 }
 

@@ -91,6 +91,9 @@ struct StageArgs {
   // [2][npoin]; the fused nodal LDG then only keeps its ope2/uvb averages (graduvb_ave and
   // graduvb_face_ave are not accumulated on that branch, mod_laplacian_quad.F90:125-223)
   const double *lapq;
+  // processor-face halo: the elements of this launch (block b runs element elist[b]; NULL:
+  // element b) -- the boundary / interior split of the two-stream schedule
+  const int *elist;
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -331,7 +334,15 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       glds_copy<BS>(a.qb_in + (size_t)e * 4 * P, s_qb, 8 * P, tid, rot);
       if (use_q0) glds_copy<BS>(a.qb0 + (size_t)e * 4 * P, s_q0, 8 * P, tid, rot);
       if (use_q2) glds_copy<BS>(a.qb2 + (size_t)e * 4 * P, s_q2, 8 * P, tid, rot);
-      glds_copy<BS>(a.trace_in + (size_t)e * 32 * NGL, s_tr, 2 * 32 * NGL, tid, rot);
+      if (m.etsrc) {
+        // processor-face halo: each face's neighbour trace from its own slot (the receive
+        // slot of a processor face); the slot ids are uniform, scalar loads
+#pragma unroll
+        for (int lf = 0; lf < 4; lf++)
+          glds_copy<BS>(a.trace_in + (size_t)m.etsrc[4 * e + lf] * 8 * NGL, s_tr + lf * 8 * NGL, 2 * 8 * NGL, tid, rot);
+      } else {
+        glds_copy<BS>(a.trace_in + (size_t)e * 32 * NGL, s_tr, 2 * 32 * NGL, tid, rot);
+      }
     }
     // qprime, the face statics and the face coefficients are constant over a sub-cycle
     // (persistent, not RES: the previous stage re-fetched them in E1, see there)
@@ -533,7 +544,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         // reference's node order (creat_btp_fluxes_qdf, mod_rhs_btp.F90:246-259)
         const int t = w - nint - 8 * NGL - P, part = t / (4 * NQ), lf = (t / NQ) & 3, iq = t % NQ;
         const int er = s_bc[lf];
-        if (part == 0 || er <= 0) {
+        if (part == 0 || er < 0) {  // (er == 0: processor face, the neighbour trace is received)
           const double *efn = s_ef + lf * C::FBLK + EF_N * NQ;
           double x[4][NGL], hv[NGL];
 #pragma unroll
@@ -585,7 +596,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       double fo[4], fr[4];
 #pragma unroll
       for (int c = 0; c < 4; c++) fo[c] = fi[c];
-      if (er > 0) {
+      if (er >= 0) {  // interior or processor face: the neighbour's trace
         double tv[4][NGL], hv[NGL];
 #pragma unroll
         for (int n = 0; n < NGL; n++) {
@@ -616,7 +627,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       const int p = s_map[lf * NGL + n];
       double own[4] = {s_qb[p * 4], s_qb[p * 4 + 1], s_qb[p * 4 + 2], s_qb[p * 4 + 3]};
       double oth[4];
-      if (er > 0) {
+      if (er >= 0) {
 #pragma unroll
         for (int c = 0; c < 4; c++) oth[c] = tr[c * NGL + n];
       } else {
@@ -829,7 +840,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     const double nxn = efn[EFN_NX * NGL + n], nyn = efn[EFN_NY * NGL + n], wq = efn[EFN_W * NGL + n];
     double own[4] = {s_grad[0 * P + p], s_grad[1 * P + p], s_grad[2 * P + p], s_grad[3 * P + p]};
     double oth[4];
-    if (er > 0) {
+    if (er >= 0) {  // interior or processor face (create_rhs_lap_postcommunicator_df)
 #pragma unroll
       for (int c = 0; c < 4; c++) oth[c] = tr[(4 + c) * NGL + n];
     } else {
@@ -1168,7 +1179,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     for (int t = tid; t < 4 * 8 * NGL; t += BS) {
       asm volatile("" ::: "memory");
       const int lf = t / (8 * NGL), c = (t / NGL) % 8, n = t % NGL;
-      if (s_bc[lf] <= 0) continue;
+      if (s_bc[lf] < 0) continue;  // (processor faces: into the face's send slot)
       const int p = s_map[lf * NGL + n];
       double val;
       if (c < 4) {
@@ -1207,7 +1218,8 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
     btp_stage_kernel(StageArgs a) {
   __shared__ double s_arena[StageCfg<NGL, NQ, SF>::ARENA];
   __shared__ unsigned long long s_prof[32];
-  stage_body<NGL, NQ, SF, false>(a, s_arena, s_prof, true, blockIdx.x, threadIdx.x);
+  stage_body<NGL, NQ, SF, false>(a, s_arena, s_prof, true, a.elist ? a.elist[blockIdx.x] : (int)blockIdx.x,
+                                  threadIdx.x);
 }
 
 // The whole barotropic sub-cycle (N_btp x kstages stages, ti_barotropic_ssprk_mlswe
@@ -1271,7 +1283,7 @@ __global__ void __launch_bounds__(64) grad_trace_kernel(DevMesh m, const double 
   __syncthreads();
   for (int t = tid; t < 4 * 8 * NGL; t += 64) {
     const int lf = t / (8 * NGL), c = (t / NGL) % 8, n = t % NGL;
-    if (s_er[EREC_BC + lf] <= 0) continue;
+    if (s_er[EREC_BC + lf] < 0) continue;  // (processor faces: into the face's send slot)
     const int p = s_er[EREC_MAP + lf * NGL + n];
     double val;
     if (c < 4) {

@@ -54,9 +54,14 @@ class HaloDesc(C.Structure):
 
 
 class Halo:
-    """HaloDesc for a hnumo.partition.RankCase (keeps the index arrays alive)."""
+    """HaloDesc for a multi-rank case (keeps the index arrays alive): a hnumo.facepart.FaceRankCase
+    (the reference's processor-face lists, mod_parallel) or a hnumo.partition.RankCase (ghost
+    elements)."""
 
     def __init__(self, rc, comm_id: bytes | None = None):
+        if getattr(rc, "halo_kind", None) == "faces":
+            self._faces(rc, comm_id)
+            return
         nb = rc.neighbours
         self.keep = {
             "nbh_proc": np.array([n.rank for n in nb], dtype=np.int32),
@@ -72,9 +77,23 @@ class Halo:
         h.rank, h.nranks, h.num_nbh, h.nelem_owned = rc.rank, rc.nranks, len(nb), rc.nelem_owned
         for k, v in self.keep.items():
             setattr(h, k, v.ctypes.data_as(_ip) if v.size else None)
+        self._comm(h, comm_id)
+        self.desc = h
+
+    def _comm(self, h, comm_id):
         if comm_id is not None:
             self.keep["comm_id"] = np.frombuffer(bytearray(comm_id), dtype=np.uint8).copy()
             h.comm_id = self.keep["comm_id"].ctypes.data_as(C.POINTER(C.c_ubyte))
+
+    def _faces(self, rc, comm_id):
+        from .facepart import halo_lists
+        nbh_proc, num, lst, _ = halo_lists(rc)
+        self.keep = {"nbh_proc": nbh_proc, "num_send_recv": num, "nbh_send_recv": lst}
+        h = HaloDesc()
+        h.rank, h.nranks, h.num_nbh, h.nelem_owned = rc.rank, rc.nranks, nbh_proc.size, rc.scalars["nelem"]
+        for k, v in self.keep.items():
+            setattr(h, k, v.ctypes.data_as(_ip) if v.size else None)
+        self._comm(h, comm_id)
         self.desc = h
 
 

@@ -78,6 +78,7 @@ def write_bundle(path: str, case, mode: str, nsteps: int = 1, metrics: bool = Fa
     hi = np.zeros(16, dtype="<i4")
     hi[:14] = [S["nelem"], S["npoin"], S["npoin_q"], S["nface"], S["ngl"], S["nq"], S["nlayers"],
                S["ngl"] - 1, S["kstages"], S["N_btp"], S["method_visc"], S["botfr"], nsteps, MODES[mode]]
+    hi[14] = 1 if getattr(case, "halo_kind", None) == "faces" else 0      # halo trailer present
     hd = np.zeros(8, dtype="<f8")
     hd[:7] = [S["dt"], S["dt_btp"], S["visc"], S["cd"], S["ad"], S["gravity"], S["max_shear_dz"]]
     with open(path, "wb") as fh:
@@ -89,6 +90,13 @@ def write_bundle(path: str, case, mode: str, nsteps: int = 1, metrics: bool = Fa
             want = shape_of(shp, d)
             assert a.size == int(np.prod(want)), (name, a.shape, want)
             fh.write(np.asarray(a, dtype="<" + dt).ravel(order="F").tobytes())
+        if hi[14]:
+            # processor-face halo (mod_parallel): num_nbh, nbh_proc, num_send_recv, nbh_send_recv
+            from .facepart import halo_lists
+            nbh_proc, num, lst, _ = halo_lists(case)
+            fh.write(np.array([nbh_proc.size, lst.size], dtype="<i4").tobytes())
+            for a in (nbh_proc, num, lst):
+                fh.write(np.asarray(a, dtype="<i4").tobytes())
 
 
 def read_outputs(path: str, case, mode: str) -> dict:

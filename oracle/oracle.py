@@ -140,3 +140,38 @@ def run_reference(case, mode: str, nsteps: int = 1, workdir: str | None = None, 
             os.remove(f)
         os.rmdir(tmp)
     return out
+
+
+MPIEXEC = os.environ.get("HNUMO_MPIEXEC", "/opt/conda/bin/mpiexec")
+
+
+def run_reference_mpi(parts, mode: str, nsteps: int = 1) -> list:
+    """Run the reference Fortran under `mpiexec -n len(parts)` on a processor-face partition
+    (hnumo.facepart.face_partition, one FaceRankCase per rank): every rank reads its own bundle
+    and the reference's own MPI halo exchange runs.  Returns the outputs of every rank."""
+    if not os.path.exists(REF_DRIVER):
+        raise FileNotFoundError(REF_DRIVER)
+    tmp = tempfile.mkdtemp(prefix="hnumo_refmpi_")
+    fin, fout = os.path.join(tmp, "bundle.bin"), os.path.join(tmp, "out.bin")
+    for r, pc in enumerate(parts):
+        _bundle.write_bundle(f"{fin}.{r}", pc, mode, nsteps)
+
+    def _stack():
+        import resource
+        resource.setrlimit(resource.RLIMIT_STACK, (resource.RLIM_INFINITY, resource.RLIM_INFINITY))
+
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [MPIEXEC, "-launcher", "fork", "-n", str(len(parts)), REF_DRIVER, fin, fout]
+    r = subprocess.run(cmd, env=env, cwd=tmp, preexec_fn=_stack, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       text=True, timeout=3600)
+    if r.returncode != 0:
+        raise RuntimeError(f"mpiexec ref_driver failed ({r.returncode}): {r.stdout[-2000:]} {r.stderr[-2000:]}")
+    outs = []
+    for k, pc in enumerate(parts):
+        o = _bundle.read_outputs(f"{fout}.{k}", pc, mode)
+        o["stdout"] = r.stdout
+        outs.append(o)
+    for f in os.listdir(tmp):
+        os.remove(os.path.join(tmp, f))
+    os.rmdir(tmp)
+    return outs

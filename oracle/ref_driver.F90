@@ -8,8 +8,10 @@
 ! The reference's own start-up (p4est mesh, netCDF output, namelists) is not used:
 ! this program fills the module globals the path reads (SURVEY.md §8b) directly from
 ! the bundle -- the same arrays the CPU oracle and the HIP engine receive through
-! include/hnumo_engine.h.  It is single-rank (num_nbh = 0), so the reference's MPI
-! halo routines run with empty neighbour lists.
+! include/hnumo_engine.h.  On one rank (num_nbh = 0) the reference's MPI halo routines run
+! with empty neighbour lists; under `mpiexec -n R` every rank reads its own bundle of a
+! processor-face partition (<bundle>.<rank>, with mod_parallel's neighbour lists) and the
+! reference's own halo exchange (send_receive_bound / create_rhs_communicator) runs over MPI.
 !
 ! usage: ref_driver <bundle.bin> <outputs.bin>
 !
@@ -66,7 +68,8 @@ program ref_driver
 
     implicit none
 
-    integer :: hi(16), ierr, u, nsteps, mode, istep, k, ip, I1
+    integer :: hi(16), ierr, u, nsteps, mode, istep, k, ip, I1, myrank, nprocs, nhalo(2)
+    character(len=16) :: rsuf
     real(8), allocatable :: qout(:,:,:), mass0(:)
     character(len=18) :: fnp11
     character(len=3) :: s_layers
@@ -82,8 +85,16 @@ program ref_driver
     real(8), allocatable :: ref_psiq(:,:), ref_dpsiq(:,:), ref_psi(:,:), ref_dpsi(:,:)
 
     call mpi_init(ierr)
+    call mpi_comm_rank(mpi_comm_world, myrank, ierr)
+    call mpi_comm_size(mpi_comm_world, nprocs, ierr)
     call get_command_argument(1, fin)
     call get_command_argument(2, fout)
+    if (nprocs > 1) then
+        ! one bundle per rank (<bundle>.<rank>, a processor-face partition, hnumo/facepart.py)
+        write(rsuf, '(I0)') myrank
+        fin = trim(fin) // '.' // trim(rsuf)
+        fout = trim(fout) // '.' // trim(rsuf)
+    end if
     open(newunit=u, file=trim(fin), access='stream', form='unformatted', status='old')
     read(u) hi
     read(u) hd
@@ -190,17 +201,30 @@ program ref_driver
         allocate(npoin_l(1)); npoin_l(1) = npoin
         lcheck_conserved = .true.
     end if
+    ! ---- halo plumbing (mod_parallel, mod_mpi_communicator, mod_ref): empty on one rank; the
+    ! processor-face lists of p4est (p4est.c:1343-1412) when the bundle carries them
+    num_nbh = 0
+    nboun = 0
+    if (hi(15) == 1) then
+        read(u) nhalo
+        num_nbh = nhalo(1); nboun = nhalo(2)
+        allocate(nbh_proc(num_nbh), num_send_recv(num_nbh), nbh_send_recv(nboun), nbh_send_recv_multi(nboun))
+        read(u) nbh_proc; read(u) num_send_recv; read(u) nbh_send_recv
+        nbh_send_recv_multi = 1                  ! conforming faces (p4est.c:1707)
+        do k = 1, nboun
+            face_type(nbh_send_recv(k)) = 2      ! processor face (p4est.c:1691)
+        end do
+    else
+        allocate(num_send_recv(0), nbh_send_recv(0), nbh_send_recv_multi(0), nbh_proc(0))
+    end if
     close(u)
     rhs = 0
-
-    ! ---- single-rank halo plumbing (mod_parallel, mod_mpi_communicator, mod_ref)
-    num_nbh = 0
-    allocate(num_send_recv(0), nbh_send_recv(0), nbh_send_recv_multi(0), nbh_proc(0))
-    allocate(ireq(0), status(MPI_STATUS_SIZE, 0))
-    allocate(q_send(4, ngl, 0), q_recv(4, ngl, 0), recv_data_dg(0), send_data_dg(0))
-    allocate(lap_q_recv_df1(4, ngl, 0), lap_q_send_df1(4, ngl, 0))
-    allocate(lap_recv_data_dg_df1(0), lap_send_data_dg_df1(0))
-    allocate(recv_data_dg_quad(0), send_data_dg_quad(0))
+    allocate(ireq(2 * num_nbh), status(MPI_STATUS_SIZE, 2 * num_nbh))   ! mod_mpi_communicator_create
+    ! mod_ref_create's halo buffers (mod_ref.F90:82-118)
+    allocate(q_send(4, ngl, nboun), q_recv(4, ngl, nboun), recv_data_dg(4 * ngl * nboun), send_data_dg(4 * ngl * nboun))
+    allocate(lap_q_recv_df1(4, ngl, nboun), lap_q_send_df1(4, ngl, nboun))
+    allocate(lap_recv_data_dg_df1(4 * ngl * nboun), lap_send_data_dg_df1(4 * ngl * nboun))
+    allocate(recv_data_dg_quad(4 * nq * nboun), send_data_dg_quad(4 * nq * nboun))
     nmessage = 6
 
     ! ---- mod_variables

@@ -56,6 +56,35 @@ def bundle_hash(case, mode, nsteps):
         return hashlib.sha256(open(p, "rb").read()).hexdigest()
 
 
+# Multi-rank: the reference run under mpiexec on a processor-face partition (hnumo/facepart.py;
+# the reference's own halo exchange over MPI).  (name, config, overrides, nranks, order, nsteps)
+GOLDEN_MPI = [
+    ("bump10_mpi3m_step2", "bump10", {}, 3, "morton", 2),
+    ("lake10_mpi2b_step1", "lake10", {}, 2, "block", 1),
+    ("dg8L3_mpi2b_step2", "dg8L3q", dict(method_visc=3), 2, "block", 2),
+    ("dg8L3_mpi4m_step2", "dg8L3q", dict(method_visc=3), 4, "morton", 2),
+]
+
+
+def make_mpi(only=None):
+    from hnumo.facepart import face_partition
+    for name, cfg, ov, R, order, nsteps in GOLDEN_MPI:
+        if only and name not in only:
+            continue
+        case = build_case(make_config(cfg, **ov))
+        parts = [face_partition(case, R, r, order) for r in range(R)]
+        outs = O.run_reference_mpi(parts, "step", nsteps)
+        keep = {"config": np.array(cfg), "overrides": np.array(json.dumps(ov)), "nranks": np.array(R),
+                "order": np.array(order), "nsteps": np.array(nsteps), "mode": np.array("step")}
+        for r, (pc, o) in enumerate(zip(parts, outs)):
+            keep[f"bundle_sha256_r{r}"] = np.array(bundle_hash(pc, "step", nsteps))
+            for k in ("q_df", "qb_df", "qprime_df"):
+                keep[f"{k}_r{r}"] = o[k]
+        path = os.path.join(HERE, name + ".npz")
+        np.savez_compressed(path, **keep)
+        print(name, os.path.getsize(path))
+
+
 def overrides_of(g) -> dict:
     """Config overrides stored in a fixture (JSON; lists back to tuples)."""
     if "overrides" not in g:
@@ -91,4 +120,8 @@ def main(only=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or None)
+    args = sys.argv[1:]
+    if args and args[0] == "mpi":
+        make_mpi(args[1:] or None)
+    else:
+        main(args or None)
