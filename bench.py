@@ -17,12 +17,14 @@ Workloads (BASELINE.json configs):
                    3 layers, dt=40 s, dt_btp=2 s, split over the N GPUs (strong scaling:
                    rank grid 2x1, 2x2, 4x2 of 158x316 / 158x158 / 79x158 element blocks).
   --weak        -- labelled extra: N blocks of 25x25 elements (weak scaling).
-Multi-GPU runs one rank per GPU (torch.distributed.run); each rank owns one block plus a
-one-element ghost layer (hnumo/partition.py) whose data the engine refreshes from the owners
-over RCCL point-to-point (xGMI) at every exchange point of the step (csrc/engine.hip
-`exchange`).  value = element-updates of all ranks / max time over ranks.  If the RCCL halo
-cannot be set up (or fails) on any rank, the ranks fall back to independent replicas of the
-per-GPU block and say so in config.parallelism.
+Multi-GPU runs one rank per GPU (torch.distributed.run).  Each rank holds one block of the
+brick partitioned the way h-NUMO itself partitions -- processor faces (hnumo/facepart.py,
+p4est.c:1686-1712): the reference's halo contract, with the stage traces exchanged over RCCL
+point-to-point (xGMI) on a second stream while the interior elements run (csrc/engine.hip
+`trace_exchange`, the overlap of mod_rhs_btp.F90:40-46).  --halo ghost uses the one-element
+ghost layer of hnumo/partition.py instead.  value = element-updates of all ranks / max time
+over ranks.  If the RCCL halo cannot be set up (or fails) on any rank, the ranks fall back to
+independent replicas of the per-GPU block and say so in config.parallelism.
 """
 from __future__ import annotations
 
@@ -113,6 +115,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default=None, help="default: dg25L3 at N=1, dg316L3 (C4) at N>1")
     ap.add_argument("--weak", action="store_true", help="N>1: N blocks of the 1-GPU mesh (weak scaling)")
+    ap.add_argument("--halo", default="faces", choices=["faces", "ghost"],
+                    help="N>1: processor faces (the reference's contract) or a one-element ghost layer")
     ap.add_argument("--cpu-steps", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c4", action="store_true", help="N=1: skip the c4_single_gpu figure")
@@ -156,7 +160,11 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         err = None
         try:
-            case = partition(gcase, world, rank)
+            if args.halo == "faces":
+                from hnumo.facepart import face_partition
+                case = face_partition(gcase, world, rank, "block")
+            else:
+                case = partition(gcase, world, rank)
             eng = Engine(case, device=local_rank, comm_id=obj[0], summation=args.summation)
             eng.set_resident(True)
             q, qb, qp = eng.state()
@@ -180,8 +188,10 @@ def main():
             parallelism = f"replicas{world} (RCCL halo unavailable: {err or 'on another rank'})"
         else:
             bx, by = gcfg["nelx"] // px, gcfg["nely"] // py
+            how = ("processor-face halo (reference contract) over RCCL p2p, traces on a 2nd stream overlapped with "
+                   "interior elements" if args.halo == "faces" else "one-element ghost halo over RCCL p2p")
             parallelism = (f"domain decomposition {px}x{py} blocks of {bx}x{by} elements "
-                           f"({gcfg['nelx']}x{gcfg['nely']} total), one-element ghost halo over RCCL p2p")
+                           f"({gcfg['nelx']}x{gcfg['nely']} total), {how}")
         del gcase
     if eng is None:
         if case is None:

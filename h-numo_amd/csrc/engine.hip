@@ -1140,7 +1140,12 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     if (eng->nB) HIPCHK(hipMemcpy(eng->d_elB, elB.data(), elB.size() * sizeof(int), hipMemcpyHostToDevice));
     if (eng->nI) HIPCHK(hipMemcpy(eng->d_elI, elI.data(), elI.size() * sizeof(int), hipMemcpyHostToDevice));
     eng->m.etsrc = d_tsrc;
-    HIPCHK(hipStreamCreateWithFlags(&eng->stream2, hipStreamNonBlocking));
+    // the boundary elements and their transport are the critical path of the stage chain:
+    // their stream gets the highest priority, so their workgroups dispatch ahead of the
+    // interior launch's
+    int prio_lo = 0, prio_hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    HIPCHK(hipStreamCreateWithPriority(&eng->stream2, hipStreamNonBlocking, prio_hi));
     for (hipEvent_t *ev : {&eng->ev_fork, &eng->ev_join, &eng->ev_I, &eng->ev_B[0], &eng->ev_B[1], &eng->ev_tsent,
                            &eng->ev_bpacked, &eng->ev_bdone})
       HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
@@ -1265,8 +1270,12 @@ static int download_state(hnumo_engine *eng, double *q, double *qb, double *qp) 
 // same launch sequence directly.
 static int ensure_graph(hnumo_engine *eng) {
   if (eng->graph_exec || eng->no_graph) return 0;
+  // RCCL engines replay direct launches unless HNUMO_GRAPH=1: capturing RCCL point-to-point
+  // into a graph cannot be exercised on a one-GPU box, and at the multi-GPU sizes (~1e4
+  // elements per GPU, ~0.2 ms per stage) the host issues a stage's launches faster than the
+  // GPU runs them
   const char *ge = getenv("HNUMO_GRAPH");
-  if (eng->comm_mode == 1 || (ge && ge[0] == '0')) {
+  if (eng->comm_mode == 1 || (ge && ge[0] == '0') || (eng->comm_mode == 2 && !(ge && ge[0] == '1'))) {
     eng->no_graph = true;
     return 0;
   }

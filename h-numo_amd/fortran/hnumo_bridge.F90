@@ -16,7 +16,7 @@
 ! message.
 module hnumo_bridge
 
-    use iso_c_binding, only: c_int, c_int32_t, c_double, c_ptr, c_null_ptr, c_loc, c_associated
+    use iso_c_binding, only: c_int, c_int32_t, c_double, c_ptr, c_null_ptr, c_loc, c_associated, c_char
     use hnumo_engine_c
 
     implicit none
@@ -59,7 +59,9 @@ contains
             pbprime_df_face, one_over_pbprime_edge, coeff_pbpert_L, coeff_pbpert_R, coeff_pbub_LR, &
             coeff_mass_pbub_L, coeff_mass_pbub_R, coeff_mass_pbpert_LR, alpha_mlswe, tau_wind, &
             coriolis_quad, grad_zbot_quad, zbot_df, zbot_face, fdt2_bcl, a_bcl, b_bcl, ssprk_a, ssprk_beta, N_btp
-        use mod_parallel, only: num_nbh
+        use mod_parallel, only: num_nbh, nbh_proc, num_send_recv, nbh_send_recv, nbh_send_recv_multi
+        use mod_mpi_utilities, only: irank, numproc
+        use mpi
         integer, intent(in) :: device
         logical, intent(in), optional :: resident
 
@@ -71,8 +73,36 @@ contains
         integer(c_int32_t), allocatable, target :: imaplq1(:, :, :), imaprq1(:, :, :)
         real(c_double), allocatable, target :: nv1(:, :, :), nvq1(:, :, :), jf1(:, :), jfq1(:, :)
         integer(c_int) :: rc
+        ! multi-rank: mod_parallel's processor-face lists as they are, plus an RCCL id from rank 0
+        type(hnumo_halo_desc), target :: halo
+        integer(c_int32_t), allocatable, target :: h_proc(:), h_num(:), h_list(:)
+        character(kind=c_char), allocatable, target :: comm_id(:)
+        type(c_ptr) :: halo_p
+        integer :: ierr
 
-        if (num_nbh > 0) stop 'hnumo_bridge: processor faces need the RCCL halo (not in this build)'
+        if (hnumo_abi_version() /= HNUMO_ABI_EXPECTED) stop 'hnumo_bridge: libhnumo_engine ABI version mismatch'
+        halo_p = c_null_ptr
+        if (numproc > 1) then
+            if (num_nbh > 0) then
+                if (any(nbh_send_recv_multi(1:sum(num_send_recv(1:num_nbh))) /= 1)) &
+                    stop 'hnumo_bridge: non-conforming processor faces are not supported'
+            end if
+            allocate(h_proc(max(num_nbh, 1)), h_num(max(num_nbh, 1)), h_list(max(sum(num_send_recv(1:num_nbh)), 1)))
+            allocate(comm_id(128))
+            h_proc(1:num_nbh) = nbh_proc(1:num_nbh)                ! 1-based ranks, as p4est fills them
+            h_num(1:num_nbh) = num_send_recv(1:num_nbh)
+            h_list(1:sum(num_send_recv(1:num_nbh))) = nbh_send_recv(1:sum(num_send_recv(1:num_nbh)))
+            if (irank == 0) then
+                rc = hnumo_rccl_unique_id(comm_id)
+                if (rc /= HNUMO_OK) stop 'hnumo_bridge: hnumo_rccl_unique_id failed'
+            end if
+            call mpi_bcast(comm_id, 128, MPI_CHARACTER, 0, MPI_COMM_WORLD, ierr)
+            halo%rank = irank; halo%nranks = numproc; halo%num_nbh = num_nbh
+            halo%nbh_proc = c_loc(h_proc); halo%num_send_recv = c_loc(h_num); halo%nbh_send_recv = c_loc(h_list)
+            halo%comm_id = c_loc(comm_id)
+            halo%nelem_owned = nelem
+            halo_p = c_loc(halo)
+        end if
         face8 = face(1:8, 1:nface)
         imapl1 = imapl(:, :, 1, :)
         imapr1 = imapr(:, :, 1, :)
@@ -113,7 +143,7 @@ contains
         par%shear_corrector = HNUMO_SHEAR_CORRECTOR_REFERENCE   ! the reference's semantics (hnumo_engine.h)
         par%N_btp = N_btp; par%kstages = kstages; par%method_visc = method_visc; par%botfr = botfr
 
-        rc = hnumo_engine_create(mesh, st, par, c_null_ptr, int(device, c_int), engine)
+        rc = hnumo_engine_create(mesh, st, par, halo_p, int(device, c_int), engine)
         if (rc /= HNUMO_OK) then
             print *, 'hnumo_engine_create failed: ', hnumo_last_error(engine)
             stop 'hnumo_bridge_init'

@@ -17,7 +17,7 @@ module hnumo_engine_c
         HNUMO_ERR_NONFINITE = 2, HNUMO_ERR_DEVICE = 3, HNUMO_ERR_INVALID = 4
     integer(c_int32_t), parameter, public :: HNUMO_SHEAR_CORRECTOR_REFERENCE = 0, &
         HNUMO_SHEAR_CORRECTOR_PREDICTED = 1
-    integer(c_int), parameter, public :: HNUMO_ABI_EXPECTED = 3   ! must equal hnumo_abi_version()
+    integer(c_int), parameter, public :: HNUMO_ABI_EXPECTED = 5   ! must equal hnumo_abi_version()
     integer(c_int), parameter, public :: HNUMO_SUM_REFERENCE = 0, HNUMO_SUM_FACTORED = 1
 
     ! = hnumo_mesh_desc (mod_grid, mod_face, mod_basis, mod_metrics; optional dense tables)
@@ -82,7 +82,7 @@ module hnumo_engine_c
     public :: hnumo_engine_create, hnumo_engine_destroy, hnumo_abi_version, hnumo_ti_rk_bcl, &
         hnumo_ti_barotropic_ssprk, hnumo_btp_bcl_coeffs, hnumo_create_rhs_btp, hnumo_get_field_c, &
         hnumo_set_resident, hnumo_sync, hnumo_last_error_c, hnumo_last_error, hnumo_get_field, &
-        hnumo_set_summation, hnumo_get_summation, hnumo_stage_path
+        hnumo_set_summation, hnumo_get_summation, hnumo_stage_path, hnumo_rccl_unique_id
 
     interface
         integer(c_int) function hnumo_engine_create(mesh, statics, params, halo, device, eng) &
@@ -104,6 +104,12 @@ module hnumo_engine_c
         integer(c_int) function hnumo_abi_version() bind(C, name='hnumo_abi_version')
             import :: c_int
         end function hnumo_abi_version
+
+        ! 128-byte RCCL unique id for hnumo_halo_desc%comm_id (made on one rank, broadcast)
+        integer(c_int) function hnumo_rccl_unique_id(out128) bind(C, name='hnumo_rccl_unique_id')
+            import :: c_int, c_char
+            character(kind=c_char), intent(out) :: out128(128)
+        end function hnumo_rccl_unique_id
 
         type(c_ptr) function hnumo_last_error_c(eng) bind(C, name='hnumo_last_error')
             import :: c_ptr

@@ -63,7 +63,7 @@ program ref_driver
     use mod_grid, only: coord
     use mod_global_grid, only: npoin_g
     use mod_parallel, only: nproc, npoin_l, npoin_l_max
-    use mod_mpi_utilities, only: irank
+    use mod_mpi_utilities, only: irank, numproc
     use mod_input, only: lcheck_conserved
 
     implicit none
@@ -87,6 +87,7 @@ program ref_driver
     call mpi_init(ierr)
     call mpi_comm_rank(mpi_comm_world, myrank, ierr)
     call mpi_comm_size(mpi_comm_world, nprocs, ierr)
+    irank = myrank; numproc = nprocs            ! what initialize_mpi_util sets (mod_mpi_utilities.F90:43-49)
     call get_command_argument(1, fin)
     call get_command_argument(2, fout)
     if (nprocs > 1) then
