@@ -57,7 +57,21 @@ FIELDS = [
     ("sum_layer_mass_flux_face", "2,nq,nface"),
 ]
 
-MODES = {"rhs": 1, "btp": 2, "step": 3, "predict": 4, "diag": 5}
+MODES = {"rhs": 1, "btp": 2, "step": 3, "predict": 4, "diag": 5, "setup": 6}
+TEST_CASE_ID = {"bump": 1, "lakeAtrest": 2, "double-gyre": 3}
+
+# outputs of mode "setup" (oracle/ref_driver.F90 mode 6: the reference's own start-up routines)
+SETUP_OUT = [
+    ("q_df", "3,npoin,nlayers"), ("qb_df", "4,npoin"), ("qprime_df", "3,npoin,nlayers"), ("pbprime", "npoin_q"),
+    ("pbprime_df", "npoin"), ("pbprime_face", "2,nq,nface"), ("pbprime_df_face", "2,ngl,nface"),
+    ("one_over_pbprime", "npoin_q"), ("one_over_pbprime_df", "npoin"), ("one_over_pbprime_edge", "nq,nface"),
+    ("coeff_pbpert_L", "nq,nface"), ("coeff_pbpert_R", "nq,nface"), ("coeff_pbub_LR", "nq,nface"),
+    ("coeff_mass_pbub_L", "nq,nface"), ("coeff_mass_pbub_R", "nq,nface"), ("coeff_mass_pbpert_LR", "nq,nface"),
+    ("alpha", "nlayers"), ("zbot_df", "npoin"), ("zbot_face", "2,nq,nface"), ("grad_zbot_quad", "2,npoin_q"),
+    ("tau_wind", "2,npoin_q"), ("coriolis_quad", "npoin_q"), ("fdt2_bcl", "npoin"), ("a_bcl", "npoin"),
+    ("b_bcl", "npoin"), ("ssprk_a", "kstages,3"), ("ssprk_beta", "kstages"), ("N_btp", "1"), ("dt_btp", "1"),
+    ("gravity", "1"),
+]
 
 
 def dims(case) -> dict:
@@ -79,17 +93,25 @@ def write_bundle(path: str, case, mode: str, nsteps: int = 1, metrics: bool = Fa
     hi[:14] = [S["nelem"], S["npoin"], S["npoin_q"], S["nface"], S["ngl"], S["nq"], S["nlayers"],
                S["ngl"] - 1, S["kstages"], S["N_btp"], S["method_visc"], S["botfr"], nsteps, MODES[mode]]
     hi[14] = 1 if getattr(case, "halo_kind", None) == "faces" else 0      # halo trailer present
+    if mode == "setup":
+        hi[15] = TEST_CASE_ID[case.cfg["test_case"]]
     hd = np.zeros(8, dtype="<f8")
     hd[:7] = [S["dt"], S["dt_btp"], S["visc"], S["cd"], S["ad"], S["gravity"], S["max_shear_dz"]]
     with open(path, "wb") as fh:
         fh.write(hi.tobytes())
         fh.write(hd.tobytes())
         trailer = (METRIC_ARRAYS if metrics else []) + ([("coord", "f8", "3,npoin")] if mode == "diag" else [])
+        if mode == "setup":
+            trailer = METRIC_ARRAYS[:5] + [("coord", "f8", "3,npoin")]
         for name, dt, shp in BUNDLE_ARRAYS + trailer:
             a = np.asarray(case.arrays[name])
             want = shape_of(shp, d)
             assert a.size == int(np.prod(want)), (name, a.shape, want)
             fh.write(np.asarray(a, dtype="<" + dt).ravel(order="F").tobytes())
+        if mode == "setup":
+            c = case.cfg
+            sp = [c["xdims"][0], c["xdims"][1], c["ydims"][0], c["ydims"][1], c["f0"], c["beta"]]
+            fh.write(np.asarray(sp, dtype="<f8").tobytes())
         if hi[14]:
             # processor-face halo (mod_parallel): num_nbh, nbh_proc, num_send_recv, nbh_send_recv
             from .facepart import halo_lists
@@ -127,5 +149,19 @@ def read_outputs(path: str, case, mode: str) -> dict:
     take("ref_dpsiq", (ngl, nq))
     take("ref_psi", (ngl, ngl))
     take("ref_dpsi", (ngl, ngl))
+    assert off == raw.size, (off, raw.size)
+    return out
+
+
+def read_setup_outputs(path: str, case) -> dict:
+    """Outputs of the reference harness in mode "setup" (SETUP_OUT order)."""
+    d = dims(case)
+    raw = np.fromfile(path, dtype="<f8")
+    off, out = 0, {}
+    for name, shp in SETUP_OUT:
+        s = shape_of(shp, d)
+        n = int(np.prod(s))
+        out[name] = raw[off:off + n].reshape(s, order="F").copy()
+        off += n
     assert off == raw.size, (off, raw.size)
     return out

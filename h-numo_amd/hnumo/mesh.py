@@ -70,8 +70,11 @@ class BrickMesh:
         sl = np.concatenate([slv, slh]); sr = np.concatenate([srv, srh])
         nface = el.size
         self.nface = nface
-        # NUMA-style local face ids (face(5:6)); informational only on this path
-        lid = np.array([4, 2, 1, 3], dtype=np.int32)
+        # NUMA local face ids (face(5:6)) of a 2-D mesh in the xy plane: p4est faces x-, x+, y-, y+
+        # -> transform {4,5,2,3} + 1 (p4est.c:1551-1574, ORIENT = 2 when nglx, ngly > 1,
+        # mod_p4est.F90:263-271), i.e. ksi = -/+1 -> 5/6, eta = -/+1 -> 3/4; the set-up routines
+        # loop over face points by them (mod_grid_get_face_nq, mod_grid.F90:475-491)
+        lid = np.array([5, 6, 3, 4], dtype=np.int32)
         face = np.zeros((8, nface), dtype=np.int32, order="F")
         face[4] = lid[sl]
         face[5] = np.where(sr >= 0, lid[np.maximum(sr, 0)], 0)

@@ -37,7 +37,7 @@ program ref_driver
     use hnumo_bridge, only: hnumo_bridge_init, hnumo_bridge_ti_rk_bcl, hnumo_bridge_fetch_averages, &
         hnumo_bridge_finalize
 #endif
-    use mod_constants, only: gravity
+    use mod_constants, only: gravity, mod_constants_create
     use mod_initial, only: psih, dpsidx, dpsidy, indexq, wjac, psih_df, dpsidx_df, dpsidy_df, &
         index_df, wjac_df, pbprime, pbprime_df, one_over_pbprime, one_over_pbprime_df, &
         pbprime_face, pbprime_df_face, one_over_pbprime_edge, coeff_pbpert_L, coeff_pbpert_R, &
@@ -64,7 +64,12 @@ program ref_driver
     use mod_global_grid, only: npoin_g
     use mod_parallel, only: nproc, npoin_l, npoin_l_max
     use mod_mpi_utilities, only: irank, numproc
-    use mod_input, only: lcheck_conserved
+    use mod_input, only: lcheck_conserved, test_case, xdims, ydims, f0, beta
+    use mod_initial, only: kvector
+    use mod_metrics, only: ksiq_x, ksiq_y, etaq_x, etaq_y, jacq
+    use mod_initial_mlswe, only: compute_reference_edge_variables, bot_topo_derivatives, &
+        wind_stress_coriolis, ssprk_coefficients
+    use mod_Tensorproduct, only: compute_gradient_quad
 
     implicit none
 
@@ -83,8 +88,12 @@ program ref_driver
     integer :: nl, nelem_in, npoin_in, npoin_q_in, nface_in, ngl_in, nq_in, nop_in
     real(8), allocatable :: ref_xgl(:), ref_wgl(:), ref_xnq(:), ref_wnq(:)
     real(8), allocatable :: ref_psiq(:,:), ref_dpsiq(:,:), ref_psi(:,:), ref_dpsi(:,:)
+    ! mode 6 (the reference's own set-up routines)
+    real(8) :: sp(6)
+    real(8), allocatable :: oop_face(:,:,:), pb_edge(:,:), oop_df_face(:,:,:), tw_df(:,:), z_if(:,:), zbot_q(:)
 
     call mpi_init(ierr)
+    call mod_constants_create()                 ! pi, earth_radius (amain.F90:171)
     call mpi_comm_rank(mpi_comm_world, myrank, ierr)
     call mpi_comm_size(mpi_comm_world, nprocs, ierr)
     irank = myrank; numproc = nprocs            ! what initialize_mpi_util sets (mod_mpi_utilities.F90:43-49)
@@ -193,6 +202,23 @@ program ref_driver
     allocate(eta_y(ngl, ngl, 1, nelem), jac(ngl, ngl, 1, nelem))
     read(u) ksiq_x; read(u) ksiq_y; read(u) etaq_x; read(u) etaq_y; read(u) jacq
     read(u) ksi_x; read(u) ksi_y; read(u) eta_x; read(u) eta_y; read(u) jac
+#else
+    if (mode == 6) then
+        ! mode 6 trailer: quad-point metrics (compute_gradient_quad), node coordinates, and the
+        ! namelist values the set-up routines read (xdims, ydims, f0, beta; test_case id hi(16))
+        allocate(ksiq_x(nq, nq, 1, nelem), ksiq_y(nq, nq, 1, nelem), etaq_x(nq, nq, 1, nelem))
+        allocate(etaq_y(nq, nq, 1, nelem), jacq(nq, nq, 1, nelem))
+        read(u) ksiq_x; read(u) ksiq_y; read(u) etaq_x; read(u) etaq_y; read(u) jacq
+        read(u) coord
+        read(u) sp
+        xdims = sp(1:2); ydims = sp(3:4); f0 = sp(5); beta = sp(6)
+        select case (hi(16))
+        case (1); test_case = 'bump'
+        case (2); test_case = 'lakeAtrest'
+        case (3); test_case = 'double-gyre'
+        case default; stop 'mode 6: unknown test case id'
+        end select
+    end if
 #endif
     if (mode == 5) then
         ! mode 5 trailer: the node coordinates (mod_grid coord, read by courant_mlswe), and the
@@ -296,6 +322,41 @@ program ref_driver
         call print_diagnostics_mlswe(qout, qb_df, dt*nsteps, nsteps, dt, 0, mass0, nsteps, fnp11, 111)
         close(111)
         call print_diagnostics_mlswe(qout, qb_df, dt*nsteps, nsteps, dt, 1, mass0, nsteps, fnp11, 111)
+    case (6)
+        ! The reference's own start-up of the MLSWE fields, in mod_initial_create's order
+        ! (mod_initial.F90:159-183) on the harness mesh: initial_conditions (ICs, pbprime at
+        ! nodes / quad points / faces and the reciprocals), compute_reference_edge_variables
+        ! (the wave-speed edge coefficients), bot_topo_derivatives (zbot, zbot_face),
+        ! compute_gradient_quad (grad_zbot_quad), N_btp, wind_stress_coriolis (wind, Coriolis,
+        ! implicit-Coriolis coefficients), ssprk_coefficients.  Pins hnumo/case.py (a18).
+        allocate(kvector(3, npoin))
+        allocate(oop_face(2, nq, nface), pb_edge(nq, nface), oop_df_face(2, ngl, nface))
+        allocate(tw_df(2, npoin), z_if(npoin, nlayers + 1), zbot_q(npoin_q))
+        ! initial_conditions accumulates into its never-zeroed automatic array
+        ! one_plus_eta_temp (initial_conditions.F90:43,382), which the reference build's
+        ! -finit-real=zero starts at 0 (SURVEY Appendix B.12): zero the stack it will occupy
+        call zero_stack(64 * (npoin + npoin_q) * (nlayers + 2))
+        call initial_conditions(q_df, pbprime, pbprime_df, pbprime_face, one_over_pbprime, oop_face, pb_edge, &
+            one_over_pbprime_edge, one_over_pbprime_df, qb_df, qprime_df, alpha_mlswe, oop_df_face, &
+            pbprime_df_face, zbot_df, tw_df, z_if)
+        call compute_reference_edge_variables(coeff_pbpert_L, coeff_pbpert_R, coeff_pbub_LR, &
+            coeff_mass_pbub_L, coeff_mass_pbub_R, coeff_mass_pbpert_LR, pbprime_face, alpha_mlswe)
+        zbot_q = 0   ! bot_topo_derivatives accumulates into zbot unzeroed (SURVEY Appendix B.12)
+        call bot_topo_derivatives(zbot_q, zbot_face, zbot_df)
+        call compute_gradient_quad(grad_zbot_quad, zbot_df)
+        N_btp = ceiling(dt / dt_btp)
+        dt_btp = dt / real(N_btp)
+        call wind_stress_coriolis(tau_wind, coriolis_df, coriolis_quad, fdt_bcl, fdt2_bcl, a_bcl, b_bcl, tw_df)
+        call ssprk_coefficients(ssprk_a, ssprk_beta)
+        open(newunit=u, file=trim(fout), access='stream', form='unformatted', status='replace')
+        write(u) q_df, qb_df, qprime_df, pbprime, pbprime_df, pbprime_face, pbprime_df_face
+        write(u) one_over_pbprime, one_over_pbprime_df, one_over_pbprime_edge
+        write(u) coeff_pbpert_L, coeff_pbpert_R, coeff_pbub_LR, coeff_mass_pbub_L, coeff_mass_pbub_R
+        write(u) coeff_mass_pbpert_LR, alpha_mlswe, zbot_df, zbot_face, grad_zbot_quad, tau_wind
+        write(u) coriolis_quad, fdt2_bcl, a_bcl, b_bcl, ssprk_a, ssprk_beta, real(N_btp, 8), dt_btp, gravity
+        close(u)
+        call mpi_finalize(ierr)
+        stop
     case default
         stop 'unknown mode'
     end select
@@ -322,6 +383,14 @@ contains
         ref_xgl = xgl; ref_wgl = wgl; ref_xnq = xnq; ref_wnq = wnq
         ref_psiq = psiq; ref_dpsiq = dpsiq; ref_psi = psi; ref_dpsi = dpsi
     end subroutine write_basis_later
+
+    ! a zero-filled stack region below the caller's frame, for the next call's uninitialised
+    ! automatic arrays (volatile: the stores are not optimised away)
+    subroutine zero_stack(n)
+        integer, intent(in) :: n
+        real(8), volatile :: buf(n)
+        buf = 0
+    end subroutine zero_stack
 
     ! accumulators are zeroed by ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:45-72); a lone
     ! create_rhs_btp call (mode 1) needs the same starting point.

@@ -85,6 +85,33 @@ def make_mpi(only=None):
         print(name, os.path.getsize(path))
 
 
+# a18: the reference's own set-up routines (ref_driver mode 6: initial_conditions,
+# compute_reference_edge_variables, bot_topo_derivatives, compute_gradient_quad,
+# wind_stress_coriolis, ssprk_coefficients) -- every table hnumo/case.py builds.
+# (name, config, overrides, stride of the stored flattened arrays)
+GOLDEN_SETUP = [
+    ("setup_bump10", "bump10", {}, 1),
+    ("setup_lake10L3", "lake10", dict(nlayers=3), 1),
+    ("setup_dg25", "dg25", {}, 5),
+    ("setup_dg8N7", "dg25", dict(nelx=8, nely=8, nop=7, dt=180.0, dt_btp=9.0), 2),
+]
+
+
+def make_setup(only=None):
+    for name, cfg, ov, stride in GOLDEN_SETUP:
+        if only and name not in only:
+            continue
+        case = build_case(make_config(cfg, **ov))
+        out = O.run_reference(case, "setup", 1)
+        keep = {"config": np.array(cfg), "overrides": np.array(json.dumps(ov)), "stride": np.array(stride),
+                "bundle_sha256": np.array(bundle_hash(case, "setup", 1))}
+        for k, _ in B.SETUP_OUT:
+            keep["ref_" + k] = np.asarray(out[k]).reshape(-1, order="F")[::stride]
+        path = os.path.join(HERE, name + ".npz")
+        np.savez_compressed(path, **keep)
+        print(name, os.path.getsize(path))
+
+
 def overrides_of(g) -> dict:
     """Config overrides stored in a fixture (JSON; lists back to tuples)."""
     if "overrides" not in g:
@@ -123,5 +150,7 @@ if __name__ == "__main__":
     args = sys.argv[1:]
     if args and args[0] == "mpi":
         make_mpi(args[1:] or None)
+    elif args and args[0] == "setup":
+        make_setup(args[1:] or None)
     else:
         main(args or None)
