@@ -88,6 +88,7 @@ struct hnumo_engine {
   int summation = HNUMO_SUM_REFERENCE;        // hnumo_set_summation
   unsigned long long *stage_prof = nullptr;  // HNUMO_STAGE_PROF=1: per-element phase clocks
   int stage_dbg = 0;                         // HNUMO_STAGE_DBG: diagnostic phase switches (timing only)
+  int stage_nb = 0;                          // per-stage kernel arena sizing (StageCfg NB; HNUMO_STAGE_NB)
   // persistent sub-cycle (btp_subcycle_kernel): allowed per summation mode when every element's
   // workgroup fits on the device at once (and HNUMO_PERSISTENT != 0); used on single-rank engines
   bool persistent_ok[2] = {false, false};
@@ -149,6 +150,18 @@ struct Launch {
     if (n < 0) n = e->nelem_owned;
     if (!st) st = e->stream;
     if (n == 0) return;
+    if constexpr (NGL == 5) {
+      if (e->summation == HNUMO_SUM_REFERENCE && e->stage_nb == 5) {
+        hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, 5>), dim3(n), dim3(StageCfg<NGL, NQ, false, 5>::BS), 0,
+                           st, a);
+        return;
+      }
+      if (e->summation == HNUMO_SUM_REFERENCE && e->stage_nb == 4) {
+        hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, 4>), dim3(n), dim3(StageCfg<NGL, NQ, false, 4>::BS), 0,
+                           st, a);
+        return;
+      }
+    }
     if (e->summation == HNUMO_SUM_REFERENCE)
       hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false>), dim3(n), dim3(StageCfg<NGL, NQ, false>::BS), 0, st, a);
     else
@@ -1106,6 +1119,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   if (const char *sm = getenv("HNUMO_SUMMATION"))
     eng->summation = (sm[0] == 'r' || sm[0] == '0') ? HNUMO_SUM_REFERENCE : HNUMO_SUM_FACTORED;
   if (const char *sd = getenv("HNUMO_STAGE_DBG")) eng->stage_dbg = atoi(sd);
+  if (const char *sn = getenv("HNUMO_STAGE_NB")) eng->stage_nb = atoi(sn);
   if (const char *sp = getenv("HNUMO_STAGE_PROF"))
     if (sp[0] == '1') eng->stage_prof = dalloc<unsigned long long>(eng, (size_t)eng->nelem * 32);
   if (halo && halo->nranks > 1 && eng->face_halo) {

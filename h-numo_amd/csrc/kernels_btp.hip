@@ -41,6 +41,17 @@
 #ifndef HNUMO_RES
 #define HNUMO_RES 0
 #endif
+// Reference-order volume integral without term buffers ("on the fly", OTF) from this NGL on:
+// one thread per (component v, node p) computes its terms T(v,p,q) itself, in quad order, as
+// it sums them.  Same terms, same order, same bits as the chunked term buffers; no [3P][Q]
+// LDS staging (46 KB at N=7) and one D phase instead of NCH+1 -- at N=7 the chunked arena
+// allows one workgroup per CU.
+#ifndef HNUMO_OTF_MIN_NGL
+#define HNUMO_OTF_MIN_NGL 8
+#endif
+#ifndef HNUMO_OTF_UNROLL
+#define HNUMO_OTF_UNROLL 5
+#endif
 namespace hnumo {
 
 // A trace value with the tag of the stage it is for: one 16-byte write-through store makes
@@ -117,11 +128,15 @@ __device__ __forceinline__ void glds_copy(const void *g, void *l, int ndw, int t
   rot = (rot + nch) % NW;
 }
 
-template <int NGL, int NQ, bool SF = false>
+// NBK: workgroups per CU the LDS arena is sized for (0: 3 for 256-thread blocks, the persistent
+// sub-cycle's need at 625 elements).  The per-stage kernel on large meshes (every CU busy for
+// many rounds) is also built for NBK = 4, 5: a smaller arena (fewer quad rows per term chunk,
+// more D phases) buys more resident elements per CU to hide latency with.
+template <int NGL, int NQ, bool SF = false, int NBK = 0>
 struct StageCfg {
   static constexpr int P = NGL * NGL, Q = NQ * NQ;
   static constexpr int BS = (Q <= 25) ? 128 : 256;
-  static constexpr int MINW = (BS == 256) ? 3 : 4;          // waves/SIMD wanted
+  static constexpr int MINW = NBK ? NBK * BS / 256 : ((BS == 256) ? 3 : 4);  // waves/SIMD wanted
   static constexpr int NBLK_CU = (MINW * 4 * 64) / BS;      // resident blocks per CU wanted
   static constexpr int BUDGET = (163840 / NBLK_CU - 512) / 8;  // LDS doubles per block
   static constexpr int ERS = EREC_SIZE(NGL), ERSD = (ERS + 1) / 2;
@@ -156,7 +171,8 @@ struct StageCfg {
   static constexpr int RC0 = (TAV / (3 * P) - 1) / NQ;  // largest RC with 3P*((RC*NQ)|1) <= TAV
   static constexpr int RCM = RC0 < 1 ? 1 : (RC0 > NQ ? NQ : RC0);
   static constexpr int NCH = (NQ + RCM - 1) / RCM, RC = (NQ + NCH - 1) / NCH, QC = RC * NQ;
-  static constexpr int QCP = QC | 1, TSZ = 3 * P * QCP;
+  static constexpr bool OTF = !SF && NGL >= HNUMO_OTF_MIN_NGL;
+  static constexpr int QCP = QC | 1, TSZ = OTF ? 0 : 3 * P * QCP;
   static constexpr int TB0 = RES ? 0 : (TSZ > B_SIZE ? TSZ : B_SIZE), TB1 = RES ? TSZ : 0;
   // SF: first-pass contraction partials U, W [3][2][NGL][NQ] (C1 runs the LDG face fluxes)
   static constexpr int UWSZ = 3 * 2 * NGL * NQ, B_UW = RES ? 0 : B_SIZE;
@@ -277,10 +293,10 @@ __device__ __forceinline__ void for_tasks(int tid, int o, int n, F &&f) {
 // first stage on; the data other workgroups (or this one, earlier in the launch) wrote --
 // the state buffers and the neighbour traces -- move with sc1 (L2-coherent, write-through)
 // register loads and stores (MI355X_MICROARCH.md, inter-workgroup visibility).
-template <int NGL, int NQ, bool SF, bool PERSIST, class ARGS>
+template <int NGL, int NQ, bool SF, bool PERSIST, class ARGS, int NB = 0>
 __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsigned long long *s_prof,
                                            bool first, const int e, const int tid, unsigned long long ep = 0) {
-  using C = StageCfg<NGL, NQ, SF>;
+  using C = StageCfg<NGL, NQ, SF, NB>;
   constexpr int P = C::P, Q = C::Q, BS = C::BS, NCH = C::NCH, QC = C::QC, QCP = C::QCP;
   const auto &m = a.m;
   const int npoin = m.npoin;
@@ -983,6 +999,50 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     }
     LDS_BARRIER();
     STAGE_MARK(7);
+  } else if constexpr (C::OTF) {
+    // D (OTF): thread (v, p) sums rhs(v,p) = sum_q T(v,p,q) in quad order, computing each term
+    // as it goes (create_rhs_btp_volume_qdf, mod_rhs_btp.F90:194-206):
+    //   T(0) = wq*(dhdx*udp + dhdy*vdp), T(1) = wq*(hi*scx + dhdx*A + quv*dhdy),
+    //   T(2) = wq*(hi*scy + dhdx*quv + dhdy*B)
+    // written uniformly as T = wq*((hi*s1 + dhdx*s2) + s3*dhdy) with s1 = 0 for v = 0: the
+    // extra (hi*0) adds a signed zero, which leaves any non-zero partial sum unchanged, and a
+    // zero term can only differ in the sign of zero -- added to a sum that starts at +0 it
+    // changes nothing (round-to-nearest never produces -0 from +0 + x).  Then the face
+    // projections; qq and the LDG face fluxes run beside; the Laplacian after the barrier.
+    auto otf_task = [&](int t, bool) {
+      const int v = t / P, p = t % P, i = p % NGL, j = p / NGL;
+      const int r1 = v == 2 ? 5 : 2, r2 = v == 0 ? 0 : (v == 1 ? 3 : 4), r3 = v == 0 ? 1 : (v == 1 ? 4 : 6);
+      const bool z1 = v == 0;
+      const double *Q1 = s_qv + r1 * Q, *Q2 = s_qv + r2 * Q, *Q3 = s_qv + r3 * Q;
+      const double *Wq = s_qk + QE_W * Q, *Ex = s_qk + QE_EX * Q, *Ey = s_qk + QE_EY * Q;
+      const double *Nx = s_qk + QE_NX * Q, *Ny = s_qk + QE_NY * Q;
+      const double *Pi = s_psiq + i * NQ, *DPi = s_dpsiq + i * NQ, *Pj = s_psiq + j * NQ, *DPj = s_dpsiq + j * NQ;
+      double acc = 0.0;
+#pragma unroll 1
+      for (int jq = 0; jq < NQ; jq++) {
+        const double pj = Pj[jq], dpj = DPj[jq];
+        const int q0 = jq * NQ;
+#pragma unroll HNUMO_OTF_UNROLL
+        for (int iq = 0; iq < NQ; iq++) {
+          const int q = q0 + iq;
+          const double pi = Pi[iq], dpi = DPi[iq];
+          const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
+          const double dhdx = h_e * Ex[q] + h_n * Nx[q];
+          const double dhdy = h_e * Ey[q] + h_n * Ny[q];
+          const double s1 = z1 ? 0.0 : Q1[q];
+          acc = acc + Wq[q] * ((hi * s1 + dhdx * Q2[q]) + Q3[q] * dhdy);
+        }
+      }
+      s_rhs[v * P + p] = face_proj(v, p, acc);
+    };
+    for_tasks<BS>(tid, 0, 3 * P, otf_task);
+    for_tasks<BS>(tid, 3 * P, P, [&](int t, bool) { qq_task(t); });
+    for_tasks<BS>(tid, 4 * P, 4 * NGL, ldg_task);
+    LDS_BARRIER();
+    STAGE_MARK(6);
+    for_tasks<BS>(tid, 0, 2 * P, [&](int t, bool) { lap_task(t / P, t % P); });
+    LDS_BARRIER();
+    STAGE_MARK(7);
   } else {
     // D0 .. D_NCH: weak-form terms T(v,p,q) of quad-row chunk k computed in parallel into
     // term buffer k&1 (create_rhs_btp_volume_qdf, mod_rhs_btp.F90:194-206: rhs(v,I) +=
@@ -1213,13 +1273,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   }
 }
 
-template <int NGL, int NQ, bool SF>
-__global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ, SF>::MINW))
+template <int NGL, int NQ, bool SF, int NB = 0>
+__global__ void __launch_bounds__((StageCfg<NGL, NQ, SF, NB>::BS), (StageCfg<NGL, NQ, SF, NB>::MINW))
     btp_stage_kernel(StageArgs a) {
-  __shared__ double s_arena[StageCfg<NGL, NQ, SF>::ARENA];
+  __shared__ double s_arena[StageCfg<NGL, NQ, SF, NB>::ARENA];
   __shared__ unsigned long long s_prof[32];
-  stage_body<NGL, NQ, SF, false>(a, s_arena, s_prof, true, a.elist ? a.elist[blockIdx.x] : (int)blockIdx.x,
-                                  threadIdx.x);
+  stage_body<NGL, NQ, SF, false, StageArgs, NB>(a, s_arena, s_prof, true,
+                                                a.elist ? a.elist[blockIdx.x] : (int)blockIdx.x, threadIdx.x);
 }
 
 // The whole barotropic sub-cycle (N_btp x kstages stages, ti_barotropic_ssprk_mlswe
