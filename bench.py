@@ -40,35 +40,72 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "h-numo_amd"))
 
 
-def cpu_baseline(case, steps: int):
-    """Time the reference Fortran itself (oracle/_ref/ref_driver, built from the
-    reference sources in the build container) on this host, 1 rank/1 core; fall back to
-    the C restatement (oracle) if the binary cannot run here."""
+def _run_reference(parts_or_case, steps: int, nranks: int):
+    """Time the reference Fortran (oracle/_ref/ref_driver, built from the reference sources in
+    the build container): one process on core 0, or `mpiexec -n nranks` on a processor-face
+    partition (the reference's own MPI halo exchange), one rank per core.  Returns seconds
+    (max over ranks of the reference's own MPI_Wtime around the step loop) or None."""
     from hnumo import bundle as B
-    from hnumo.roofline import element_updates_per_step
-    eus = element_updates_per_step(case) * steps
     ref = os.path.join(REPO, "oracle", "_ref", "ref_driver")
-    sample = f"{case.cfg['name']} ({case.scalars['nelem']} elements, N={case.scalars['ngl'] - 1}, " \
-             f"L={case.scalars['nlayers']}), {steps} baroclinic steps"
-    if os.path.exists(ref):
-        try:
-            with tempfile.TemporaryDirectory() as d:
-                fin, fout = os.path.join(d, "b.bin"), os.path.join(d, "o.bin")
-                B.write_bundle(fin, case, "step", steps)
+    if not os.path.exists(ref):
+        return None
 
-                def _stack():
-                    import resource
-                    resource.setrlimit(resource.RLIMIT_STACK, (resource.RLIM_INFINITY, resource.RLIM_INFINITY))
+    def _stack():
+        import resource
+        resource.setrlimit(resource.RLIMIT_STACK, (resource.RLIM_INFINITY, resource.RLIM_INFINITY))
 
-                env = dict(os.environ, OMP_NUM_THREADS="1")
-                r = subprocess.run(["taskset", "-c", "0", ref, fin, fout], cwd=d, env=env, preexec_fn=_stack,
-                                   capture_output=True, text=True, timeout=600)
-                if r.returncode == 0:
-                    t = [float(line.split()[1]) for line in r.stdout.splitlines() if line.startswith("REF_TIME")][0]
-                    return {"value": eus / t, "unit": "element-updates/s", "cores": 1, "kind": "reference",
-                            "sample": sample + f" of the reference Fortran (amdflang -O2), {t:.2f} s"}
-        except Exception as exc:  # pragma: no cover - diagnostic only
-            print(f"[bench] reference baseline failed: {exc}", file=sys.stderr)
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    with tempfile.TemporaryDirectory() as d:
+        fin, fout = os.path.join(d, "b.bin"), os.path.join(d, "o.bin")
+        if nranks == 1:
+            B.write_bundle(fin, parts_or_case, "step", steps)
+            cmd = ["taskset", "-c", "0", ref, fin, fout]
+        else:
+            for r, pc in enumerate(parts_or_case):
+                B.write_bundle(f"{fin}.{r}", pc, "step", steps)
+            cmd = [os.environ.get("HNUMO_MPIEXEC", "/opt/conda/bin/mpiexec"), "-launcher", "fork", "-bind-to", "core",
+                   "-n", str(nranks), ref, fin, fout]
+        r = subprocess.run(cmd, cwd=d, env=env, preexec_fn=_stack, capture_output=True, text=True, timeout=900)
+        if r.returncode != 0:
+            print(f"[bench] reference run failed ({r.returncode}): {r.stderr[-500:]}", file=sys.stderr)
+            return None
+        t = [float(line.split()[1]) for line in r.stdout.splitlines() if line.startswith("REF_TIME")]
+        return max(t) if t else None
+
+
+def cpu_baseline(case, steps: int, cores: int):
+    """The reference Fortran timed on this host: `cores` MPI ranks (one per core) on a Morton
+    processor-face partition of the same workload -- the reference's own multi-rank path --
+    and, beside it, one rank on one core.  Falls back to the C restatement (oracle, 1 core)."""
+    from hnumo.facepart import face_partition
+    from hnumo.roofline import element_updates_per_step
+    eu = element_updates_per_step(case)
+    S = case.scalars
+    sample = f"{case.cfg['name']} ({S['nelem']} elements, N={S['ngl'] - 1}, L={S['nlayers']})"
+    out = None
+    try:
+        one = _run_reference(case, steps, 1)
+        many_steps = steps * max(1, cores // 2)
+        many = None
+        if cores > 1:
+            parts = [face_partition(case, cores, r, "morton") for r in range(cores)]
+            many = _run_reference(parts, many_steps, cores)
+        if many:
+            out = {"value": eu * many_steps / many, "unit": "element-updates/s", "cores": cores, "kind": "reference",
+                   "sample": sample + f", {many_steps} baroclinic steps of the reference Fortran (amdflang -O2) under "
+                                      f"mpiexec -n {cores} (Morton processor-face partition, its own MPI halo), "
+                                      f"one rank per core: {many:.2f} s"}
+        if one:
+            single = {"value": eu * steps / one, "cores": 1,
+                      "sample": sample + f", {steps} baroclinic steps, 1 rank on core 0: {one:.2f} s"}
+            if out:
+                out["single_core"] = single
+            else:
+                out = dict(single, unit="element-updates/s", kind="reference")
+    except Exception as exc:  # pragma: no cover - diagnostic only
+        print(f"[bench] reference baseline failed: {exc}", file=sys.stderr)
+    if out:
+        return out
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     o = O.Oracle(case)
@@ -77,8 +114,8 @@ def cpu_baseline(case, steps: int):
     for _ in range(steps):
         o.ti_rk_bcl(q, qb, qp)
     t = time.perf_counter() - t0
-    return {"value": eus / t, "unit": "element-updates/s", "cores": 1, "kind": "port",
-            "sample": sample + f" of the C restatement (oracle/hnumo_oracle.c, -O2), {t:.2f} s"}
+    return {"value": eu * steps / t, "unit": "element-updates/s", "cores": 1, "kind": "port",
+            "sample": sample + f", {steps} baroclinic steps of the C restatement (oracle/hnumo_oracle.c, -O2), {t:.2f} s"}
 
 
 def c4_single_gpu(steps: int = 3):
@@ -118,6 +155,8 @@ def main():
     ap.add_argument("--halo", default="faces", choices=["faces", "ghost"],
                     help="N>1: processor faces (the reference's contract) or a one-element ghost layer")
     ap.add_argument("--cpu-steps", type=int, default=8)
+    ap.add_argument("--cpu-cores", type=int, default=16,
+                    help="MPI ranks (= host cores) of the reference CPU baseline (the GPU box's share is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c4", action="store_true", help="N=1: skip the c4_single_gpu figure")
     ap.add_argument("--summation", default="reference", choices=["reference", "factored"],
@@ -292,7 +331,8 @@ def main():
         except Exception as exc:  # pragma: no cover - diagnostic only
             out["c4_single_gpu"] = {"error": f"{type(exc).__name__}: {exc}"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(build_case(make_config(cfg_name)), args.cpu_steps)
+        ncores = max(1, min(args.cpu_cores, len(os.sched_getaffinity(0))))
+        out["cpu_baseline"] = cpu_baseline(build_case(make_config(cfg_name)), args.cpu_steps, ncores)
     if rank == 0:
         print(json.dumps(out))
     if dist is not None:
