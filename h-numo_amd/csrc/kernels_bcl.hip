@@ -68,23 +68,40 @@ __device__ __forceinline__ double weak_div(const double *s_psiq, const double *s
   return acc;
 }
 
-// face terms of one face onto node p: acc -/+ (wq*hi)*flux(iq), quad order (left: -, right: +)
+// Face terms of one face onto node p: acc -/+ (wq*hi)*flux(iq), quad order (left: -, right: +),
+// from the element's own face data staged in LDS: s_fw[lf][NQ] (w of the face quad points)
+// and s_fx[lf][NQ] (the flux), lf = the element's local face.
 template <int NGL, int NQ>
-__device__ __forceinline__ double face_terms(const double *s_psiq, const int *s_map, const int *s_face,
-                                             const int *s_side, const double *fw, const double *flux, size_t fstride,
-                                             int p, double acc) {
+__device__ __forceinline__ double face_terms_lds(const double *s_psiq, const int *s_map, const int *s_side,
+                                                 const double *s_fw, const double *s_fx, int p, double acc) {
+  // (not unrolled: a node lies on at most two faces, and the unrolled search with its loads
+  // hoisted costs hundreds of registers)
+#pragma unroll 1
   for (int lf = 0; lf < 4; lf++)
+#pragma unroll 1
     for (int n = 0; n < NGL; n++) {
       if (s_map[lf * NGL + n] != p) continue;
-      const size_t b = (size_t)s_face[lf] * NQ;
       const bool left = s_side[lf] == 0;
+#pragma unroll
       for (int iq = 0; iq < NQ; iq++) {
-        const double c = fw[b + iq] * s_psiq[n * NQ + iq] * flux[b + iq];
+        const double c = s_fw[lf * NQ + iq] * s_psiq[n * NQ + iq] * s_fx[lf * NQ + iq];
         acc = left ? acc - c : acc + c;
       }
     }
-  (void)fstride;
   return acc;
+}
+
+// Stage an element's face data into LDS with the element's other loads (the element kernels
+// otherwise read it from global memory inside their ordered sums, one round trip per face):
+// dst[c][lf][NQ] = src[c*cstride + face(lf)*NQ + iq] for c < nc (before the first barrier,
+// after s_face is set -- it is read from global memory here).
+template <int NQ>
+__device__ __forceinline__ void stage_face_quads(double *dst, const double *src, size_t cstride, int nc,
+                                                 const int *efaces_e, int tid, int bs) {
+  for (int t = tid; t < nc * 4 * NQ; t += bs) {
+    const int c = t / (4 * NQ), lf = (t / NQ) % 4, iq = t % NQ;
+    dst[t] = src[c * cstride + (size_t)efaces_e[lf] * NQ + iq];
+  }
 }
 
 // ===================================================================== face traces
@@ -486,12 +503,15 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
   __shared__ double s_qm[5][Q];             // e_x, e_y, n_x, n_y, w
   __shared__ double s_f[MAXL][2][Q];        // udp, vdp per layer
   __shared__ double s_adv[MAXL][P];
+  __shared__ double s_fw[4 * NQ], s_fx[MAXL][4 * NQ];  // face weights, layer mass fluxes of the 4 faces
   __shared__ int s_map[4 * NGL], s_face[4], s_side[4];
   load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
   if (tid < 4) {
     s_face[tid] = m.efaces[e * 4 + tid];
     s_side[tid] = m.eside[e * 4 + tid];
   }
+  stage_face_quads<NQ>(s_fw, m.fstat + FS_W * (size_t)F * NQ, 0, 1, m.efaces + e * 4, tid, BS);
+  stage_face_quads<NQ>(&s_fx[0][0], fmass, (size_t)F * NQ, L, m.efaces + e * 4, tid, BS);
   for (int t = tid; t < 4 * NGL; t += BS) s_map[t] = m.efmap[e * 4 * NGL + t];
   for (int t = tid; t < L * 3 * P; t += BS) {
     int k = t / (3 * P), r = t % (3 * P);
@@ -531,8 +551,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     const int k = t / P, p = t % P, i = p % NGL, j = p / NGL;
     double acc = weak_div<NGL, NQ>(s_psiq, s_dpsiq, s_qm[0], s_qm[1], s_qm[2], s_qm[3], s_qm[4], s_f[k][0], s_f[k][1],
                                    i, j, 0.0);
-    acc = face_terms<NGL, NQ>(s_psiq, s_map, s_face, s_side, m.fstat + FS_W * (size_t)F * NQ,
-                              fmass + (size_t)k * F * NQ, 0, p, acc);
+    acc = face_terms_lds<NGL, NQ>(s_psiq, s_map, s_side, s_fw, s_fx[k], p, acc);
     const size_t I = (size_t)e * P + p;
     double adv = m.nstat[NS_MINV * (size_t)npoin + I] * acc;
     double v = q[((size_t)k * npoin + I) * 3] + m.dt * adv;
@@ -565,12 +584,15 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
   __shared__ double s_qm[5][Q];
   __shared__ double s_f[MAXL][2][Q];
   __shared__ double s_new[MAXL][P];
+  __shared__ double s_fw[4 * NQ], s_fx[MAXL][4 * NQ];  // face weights, consistency fluxes of the 4 faces
   __shared__ int s_map[4 * NGL], s_face[4], s_side[4];
   load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
   if (tid < 4) {
     s_face[tid] = m.efaces[e * 4 + tid];
     s_side[tid] = m.eside[e * 4 + tid];
   }
+  stage_face_quads<NQ>(s_fw, m.fstat + FS_W * (size_t)F * NQ, 0, 1, m.efaces + e * 4, tid, BS);
+  stage_face_quads<NQ>(&s_fx[0][0], fcons, (size_t)F * NQ, L, m.efaces + e * 4, tid, BS);
   for (int t = tid; t < 4 * NGL; t += BS) s_map[t] = m.efmap[e * 4 * NGL + t];
   for (int t = tid; t < L * P; t += BS) s_d[t / P][t % P] = dpp[(size_t)(t / P) * npoin + (size_t)e * P + t % P];
   for (int t = tid; t < 5 * Q; t += BS) {
@@ -598,8 +620,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     const int k = t / P, p = t % P, i = p % NGL, j = p / NGL;
     double acc = weak_div<NGL, NQ>(s_psiq, s_dpsiq, s_qm[0], s_qm[1], s_qm[2], s_qm[3], s_qm[4], s_f[k][0], s_f[k][1],
                                    i, j, 0.0);
-    acc = face_terms<NGL, NQ>(s_psiq, s_map, s_face, s_side, m.fstat + FS_W * (size_t)F * NQ,
-                              fcons + (size_t)k * F * NQ, 0, p, acc);
+    acc = face_terms_lds<NGL, NQ>(s_psiq, s_map, s_side, s_fw, s_fx[k], p, acc);
     const size_t I = (size_t)e * P + p;
     double v = q[((size_t)k * npoin + I) * 3] + m.dt * m.nstat[NS_MINV * (size_t)npoin + I] * acc;
     q[((size_t)k * npoin + I) * 3] = v;
@@ -841,6 +862,9 @@ __global__ void __launch_bounds__(256, 2)
   __shared__ double s_G[MAXL][6][Q];       // source_x, Hq+uu, uv, source_y, vu, Hq+vv
   __shared__ double s_qq[MAXL][4][P];      // LDG volume fluxes per layer
   __shared__ double s_r[MAXL][4][P];       // rhs_mom(2) and lap(2) per layer
+  __shared__ double s_fw[4 * NQ];          // face quad weights of the 4 faces
+  __shared__ double s_fm[MAXL][2][4 * NQ]; // momentum face terms of this element's side, per face
+  __shared__ double s_fl[MAXL][2][4 * NGL];// layer LDG face fluxes at the face nodes
   __shared__ int s_map[4 * NGL], s_face[4], s_side[4], s_bc[4];
 
   // quad-point scalars for the layer-coupling task of quad point tid, in flight during
@@ -862,6 +886,19 @@ __global__ void __launch_bounds__(256, 2)
     s_bc[tid] = m.ebc[e * 4 + tid];
   }
   for (int t = tid; t < 4 * NGL; t += BS) s_map[t] = m.efmap[e * 4 * NGL + t];
+  // the element's face data (Apply_layers_fluxes' lifts, the LDG face fluxes), staged with the
+  // other loads: momL or momR by the element's side of each face
+  stage_face_quads<NQ>(s_fw, m.fstat + FS_W * (size_t)F * NQ, 0, 1, m.efaces + e * 4, tid, BS);
+  for (int t = tid; t < L * 2 * 4 * NQ; t += BS) {
+    const int ko = t / (4 * NQ), lf = (t / NQ) % 4, iq = t % NQ;
+    const int f = m.efaces[e * 4 + lf];
+    const double *src = m.eside[e * 4 + lf] == 0 ? momL : momR;
+    (&s_fm[0][0][0])[t] = src[(size_t)ko * F * NQ + (size_t)f * NQ + iq];
+  }
+  for (int t = tid; t < L * 2 * 4 * NGL; t += BS) {
+    const int ko = t / (4 * NGL), lf = (t / NGL) % 4, n = t % NGL;
+    (&s_fl[0][0][0])[t] = lapf[(size_t)ko * F * NGL + (size_t)m.efaces[e * 4 + lf] * NGL + n];
+  }
   for (int t = tid; t < L * 3 * P; t += BS) {
     int k = t / (3 * P), r = t % (3 * P);
     s_qp[k][r % 3][r / 3] = qp_in[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
@@ -1055,10 +1092,12 @@ __global__ void __launch_bounds__(256, 2)
         const double dy = both ? ey_ + ny_ : (mid ? ey_ : ny_);
         acc = acc - s_nm[4][sn] * (dx * s_qq[k][2 * c][sn] + dy * s_qq[k][2 * c + 1][sn]);
       }
+#pragma unroll 1
       for (int lf = 0; lf < 4; lf++)
+#pragma unroll 1
         for (int n = 0; n < NGL; n++)
           if (s_map[lf * NGL + n] == p) {
-            const double v = lapf[((size_t)k * 2 + c) * F * NGL + (size_t)s_face[lf] * NGL + n];
+            const double v = s_fl[k][c][lf * NGL + n];
             acc = s_side[lf] == 0 ? acc + v : acc - v;
           }
       s_r[k][2 + c][p] = acc;
@@ -1087,18 +1126,7 @@ __global__ void __launch_bounds__(256, 2)
         acc = acc + term;
       }
     }
-    const double *fw = m.fstat + FS_W * (size_t)F * NQ;
-    for (int lf = 0; lf < 4; lf++)
-      for (int n = 0; n < NGL; n++) {
-        if (s_map[lf * NGL + n] != p) continue;
-        const size_t b = (size_t)s_face[lf] * NQ;
-        const bool left = s_side[lf] == 0;
-        const double *src = (left ? momL : momR) + ((size_t)k * 2 + o) * F * NQ;
-        for (int iq = 0; iq < NQ; iq++) {
-          const double c = fw[b + iq] * s_psiq[n * NQ + iq] * src[b + iq];
-          acc = left ? acc - c : acc + c;
-        }
-      }
+    acc = face_terms_lds<NGL, NQ>(s_psiq, s_map, s_side, s_fw, s_fm[k][o], p, acc);
     s_r[k][o][p] = acc;
   }
   __syncthreads();
