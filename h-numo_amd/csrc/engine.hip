@@ -123,6 +123,9 @@ struct hnumo_engine {
   double *lq_flux = nullptr;  // LDG fluxes at the quad points [L][E][4][Q] (barotropic: layer block 0)
   double *lapq = nullptr;     // Laplacians [L][2][npoin] (barotropic: [2][npoin])
   int *fqLR = nullptr;        // [2][F][NQ] element-local quad point of each face quad point, left | right
+  // bottom-layer qprime at the quad points, interpolated once per sub-cycle (StageArgs::qpq;
+  // botfr != 0; HNUMO_QPQ=0: every stage interpolates, for A/B timing)
+  double *qpq = nullptr;      // [E][3][Q]
 };
 
 template <typename T>
@@ -608,6 +611,8 @@ static int stage_table(hnumo_engine *e, const double *qp, std::vector<StageArgs>
       a.save_q2 = K == 5 && ik == 2;
       a.err = e->neg_flag;
       a.lapq = e->lapq_on ? e->lapq : nullptr;
+      a.qpq = e->qpq;
+      a.qpq_mode = stage == 0 ? 1 : 2;
       out_args.push_back(a);
       gt = 1 - gt;
       cur = out;
@@ -1120,6 +1125,10 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     eng->summation = (sm[0] == 'r' || sm[0] == '0') ? HNUMO_SUM_REFERENCE : HNUMO_SUM_FACTORED;
   if (const char *sd = getenv("HNUMO_STAGE_DBG")) eng->stage_dbg = atoi(sd);
   if (const char *sn = getenv("HNUMO_STAGE_NB")) eng->stage_nb = atoi(sn);
+  {
+    const char *qv = getenv("HNUMO_QPQ");
+    if (par->botfr && !(qv && atoi(qv) == 0)) eng->qpq = dalloc<double>(eng, (size_t)E * 3 * eng->nq * eng->nq);
+  }
   if (const char *sp = getenv("HNUMO_STAGE_PROF"))
     if (sp[0] == '1') eng->stage_prof = dalloc<unsigned long long>(eng, (size_t)eng->nelem * 32);
   if (halo && halo->nranks > 1 && eng->face_halo) {

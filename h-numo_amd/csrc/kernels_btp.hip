@@ -52,6 +52,14 @@
 #ifndef HNUMO_OTF_UNROLL
 #define HNUMO_OTF_UNROLL 5
 #endif
+// Face fluxes in D0 on the last wave, neighbour traces checked there (StageCfg::FD0).  Off:
+// measured slower at dg25L3 (15.4 against 14.5 us per persistent stage, bitwise unchanged) --
+// checking the traces one phase (B) later shortened the trace wait by only ~0.5k of ~5k clocks,
+// while the last wave's serial poll + face + LDG work lengthened D0 by ~2k: the wait is the
+// neighbours' stage-to-stage skew, not a fixed hand-off latency that later checking could hide.
+#ifndef HNUMO_FD0
+#define HNUMO_FD0 0
+#endif
 namespace hnumo {
 
 // A trace value with the tag of the stage it is for: one 16-byte write-through store makes
@@ -105,6 +113,11 @@ struct StageArgs {
   // processor-face halo: the elements of this launch (block b runs element elist[b]; NULL:
   // element b) -- the boundary / interior split of the two-stream schedule
   const int *elist;
+  // bottom-layer qprime at the quad points (pp, up, vp; mod_rhs_btp.F90:146-152), constant over a
+  // sub-cycle: [E][3][Q] scratch (NULL: interpolated by every stage).  qpq_mode 1: this stage
+  // interpolates and stores them (a sub-cycle's first stage), 2: loads them (the later stages)
+  double *qpq;
+  int qpq_mode;
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -168,7 +181,12 @@ struct StageCfg {
   // exact: term chunks of RC quad rows, two buffers of [3P][QCP] (odd pitch against bank
   // conflicts), as many rows as the LDS budget allows
   static constexpr int TAV = (BUDGET - O_B) / 2;
-  static constexpr int RC0 = (TAV / (3 * P) - 1) / NQ;  // largest RC with 3P*((RC*NQ)|1) <= TAV
+  static constexpr int rc_fit(int tav) {  // largest RC with 3P*((RC*NQ)|1) <= TAV (0 if none)
+    int rc = NQ;
+    while (rc > 0 && 3 * P * ((rc * NQ) | 1) > tav) rc--;
+    return rc;
+  }
+  static constexpr int RC0 = rc_fit(TAV);
   static constexpr int RCM = RC0 < 1 ? 1 : (RC0 > NQ ? NQ : RC0);
   static constexpr int NCH = (NQ + RCM - 1) / RCM, RC = (NQ + NCH - 1) / NCH, QC = RC * NQ;
   static constexpr bool OTF = !SF && NGL >= HNUMO_OTF_MIN_NGL;
@@ -184,6 +202,13 @@ struct StageCfg {
   // chunks) the face fluxes run in B and the traces are polled after the interpolation.
   static constexpr bool LATE = HNUMO_LATE && RES && !SF && NCH >= 3;
   static constexpr int KP = NCH - 3;
+  // FD0 (exact, chunked D, not LATE): the face fluxes run in D0 on the last wave, beside the first
+  // chunk's terms, followed by the LDG face fluxes (qq moves to D1: FPRE's face-quad traces share
+  // its LDS).  The persistent kernel's last wave issues the neighbour-trace granule loads before
+  // A2 and checks them only there, one phase (B) later than after A2: more of the hand-off latency
+  // hides behind the element's own work, and only one wave waits for it.
+  static constexpr bool FD0 = HNUMO_FD0 && !SF && !LATE && !OTF && NCH >= 2 && 4 * NQ <= 64 && 4 * NGL <= 64;
+  static constexpr int NGR = (32 * NGL + 63) / 64;  // granules per lane of the polling wave
   // B task ranges: quad points [0,Q) | face points [OF,OF+4NQ) (early only) | nodal grad
   // [OG,OG+P) | LDG face nodes [OL,OL+4NGL) (SF: C1), on their own
   // waves when they fit
@@ -207,13 +232,16 @@ struct StageCfg {
 // taken from the LDS table with a zero slot at index NGL*NGL: on the node itself both are
 // present and A*e + B*n is the reference's full expression, elsewhere the missing half adds
 // a signed zero (x + 0 == x), so the sums are the reference's without selects or branches.
+// (Written with selects only: short-circuit conditions here compiled to exec-mask branches per
+// term, ~25 VALU + 10 SALU per term.)
 template <int NGL>
 __device__ __forceinline__ void nz_coef(int r, int i, int j, int &mm, int &n, int &ia, int &ib) {
-  const bool row = (r >= j) && (r < j + NGL);
-  mm = row ? j : (r < j ? r : r - NGL + 1);
-  n = row ? r - j : i;
-  ia = row ? n * NGL + i : NGL * NGL;
-  ib = (!row || n == i) ? mm * NGL + j : NGL * NGL;
+  const int d = r - j;
+  const bool row = (unsigned)d < (unsigned)NGL;
+  mm = min(r, j) + max(d - NGL + 1, 0);
+  n = row ? d : i;
+  ia = row ? d * NGL + i : NGL * NGL;
+  ib = (row & (d != i)) ? NGL * NGL : mm * NGL + j;
 }
 
 // grad of u_bar at node (i,j) along one metric pair: sum over source nodes (mm,n) of
@@ -313,6 +341,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   double *s_u = S + C::O_UV, *s_v = s_u + P;  // u_bar = qb(3)/qb(1), v_bar = qb(4)/qb(1) at the nodes
   double *s_wn = S + C::O_WN;      // [4][2][NGL] face-node normals (wall fix)
   double *s_qv = S + C::O_QV;      // [NQV][Q] (see StageCfg)
+  double *s_pq = s_qv + 4 * Q;     // [3][Q] bottom-layer pp, up, vp (exact, A2 -> B)
   double *s_y = S + C::O_Y;        // SF: [NYV][NGL][NQ] interpolation partials
   double *s_grad = S + C::O_GR, *s_qq = S + C::O_QQ;  // [4][P]
   double *s_fq = S + C::O_FQ;      // [4][NQ][4]: wq, flux, H_kx+flux_x, H_ky+flux_y
@@ -337,6 +366,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   STAGE_MARK(0);
   if (a.prof && tid == 0) s_prof[22] = 0;
   const bool use_q0 = !a.rhs_only && a.a1 != 0.0, use_q2 = !a.rhs_only && a.a3 != 0.0;
+  const int qpm = (SF || !m.botfr || !a.qpq) ? 0 : a.qpq_mode;  // see StageArgs::qpq
   {
     int rot = 0;
     if (!PERSIST || first) {
@@ -363,7 +393,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     // qprime, the face statics and the face coefficients are constant over a sub-cycle
     // (persistent, not RES: the previous stage re-fetched them in E1, see there)
     if (!PERSIST || first) {
-      if (m.botfr) glds_copy<BS>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
+      if (m.botfr && qpm != 2)
+        glds_copy<BS>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
       glds_copy<BS>(m.efstat + (size_t)e * 4 * C::FBLK, s_ef, 2 * 4 * C::FBLK, tid, rot);
       glds_copy<BS>(a.efcoef + (size_t)e * 4 * C::EFC, s_ec, 2 * 4 * C::EFC, tid, rot);
     }
@@ -385,7 +416,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   // (The time averages are never read here: every stage adds its values with a global
   // float64 atomic add, which rounds exactly as acc = acc + x and, one stage per launch,
   // keeps the reference's summation order.)
-  constexpr int NST = QE_N - QE_KEEP, NPRE = NST + 4;
+  constexpr int NST = QE_N - QE_KEEP, NPRE = NST + 7;
   double pre[NPRE];
   auto load_pre = [&]() {
     if (tid < Q) {
@@ -395,6 +426,11 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       const double *eco = a.ecoef + (size_t)e * C::ECO + tid;
 #pragma unroll
       for (int k = 0; k < 4; k++) pre[NST + k] = eco[k * Q];
+      if (qpm == 2) {
+        const double *qq = a.qpq + (size_t)e * 3 * Q + tid;
+#pragma unroll
+        for (int k = 0; k < 3; k++) pre[NST + 4 + k] = qq[k * Q];
+      }
     }
   };
   if (!PERSIST || first) {
@@ -470,13 +506,59 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       if (a.prof) atomicMax(&s_prof[22], clock64() - c0);  // longest trace wait of the stage
     }
   };
-  if constexpr (!LATE) issue_granule();
+  // FD0: the last wave loads every granule of the element (NGR per lane) now and checks them in
+  // D0 (poll_wave), before the face fluxes it runs there
+  constexpr bool FD0 = C::FD0;
+  granule_u4 gxr[C::NGR];
+  auto issue_granules_wave = [&]() {
+    if constexpr (PERSIST && FD0) {
+      if (tid >= BS - 64) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(a.gtr_in + (size_t)e * 32 * NGL), 0, 32 * NGL * (int)sizeof(TraceGranule), 0x00020000);
+#pragma unroll
+        for (int k = 0; k < C::NGR; k++)  // (past the record: the buffer bound returns zeros)
+          gxr[k] = __builtin_amdgcn_raw_buffer_load_b128(r, ((tid & 63) + 64 * k) * (int)sizeof(TraceGranule), 0, 16);
+      }
+    }
+  };
+  auto poll_wave = [&]() {
+    if constexpr (PERSIST && FD0) {
+      const unsigned long long want = (ep << 20) | a.tag_in;
+      const unsigned long long c0 = a.prof ? clock64() : 0;
+#pragma unroll
+      for (int k = 0; k < C::NGR; k++) {
+        const int t = (tid & 63) + 64 * k;
+        if (t >= 32 * NGL || s_bc[t / (8 * NGL)] <= 0) continue;  // no neighbour writes this slot
+        double v = __builtin_bit_cast(double, ((unsigned long long)gxr[k][1] << 32) | gxr[k][0]);
+        unsigned long long tag = ((unsigned long long)gxr[k][3] << 32) | gxr[k][2];
+        unsigned spins = 0;
+        while (tag != want && !(a.dbg & 16)) {
+          __builtin_amdgcn_s_sleep(1);
+          ld_granule(a.gtr_in + (size_t)e * 32 * NGL + t, v, tag);
+          if (++spins > (1u << 20)) {  // never expected: report instead of hanging the GPU
+            atomicOr(a.err, 8);
+            break;
+          }
+        }
+        s_tr[t] = v;
+      }
+      if (a.prof) atomicMax(&s_prof[22], clock64() - c0);
+    }
+  };
+  if constexpr (FD0)
+    issue_granules_wave();
+  else if constexpr (!LATE)
+    issue_granule();
   {
-    const int ng = m.botfr ? 3 : 2;
+    // persistent, after the first stage: the wall normals and u_bar, v_bar of this state are in
+    // LDS already (E1 formed u_bar, v_bar of the new state); qpm == 2: pp, up, vp are loaded
+    const bool full = !PERSIST || first;
+    const int ng = (m.botfr && qpm != 2) ? 3 : 2;
     constexpr int TPG = SF ? NQ * NGL : Q;  // tasks per group
     const int nint = ng * TPG;
+    const int T_WN = nint + (full ? 8 * NGL : 0), T_UV = T_WN + (full ? P : 0);
     constexpr int NFP = C::FPRE ? 8 * NQ : 0;  // face-quad pre-interpolation tasks (own | ghost side)
-    for (int w = tid; w < nint + 8 * NGL + P + NFP; w += BS) {
+    for (int w = tid; w < T_UV + NFP; w += BS) {
       asm volatile("" ::: "memory");
       if (w < nint) {
         const int g = w / TPG, r = w % TPG;
@@ -542,23 +624,23 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
                 x1 = x1 + hi * s_qp[ip * 3 + 1];
                 x2 = x2 + hi * s_qp[ip * 3 + 2];
               }
-            s_qv[4 * Q + q] = x0;
-            s_qv[5 * Q + q] = x1;
-            s_qv[6 * Q + q] = x2;
+            s_pq[0 * Q + q] = x0;
+            s_pq[1 * Q + q] = x1;
+            s_pq[2 * Q + q] = x2;
           }
         }
-      } else if (w < nint + 8 * NGL) {
+      } else if (w < T_WN) {
         const int t = w - nint, lf = t / (2 * NGL), c = (t / NGL) & 1, n = t % NGL;
         s_wn[t] = s_ef[lf * C::FBLK + EF_N * NQ + (c ? EFN_NY : EFN_NX) * NGL + n];
-      } else if (w < nint + 8 * NGL + P) {
-        const int p = w - nint - 8 * NGL;
+      } else if (w < T_UV) {
+        const int p = w - T_WN;
         s_u[p] = s_qb[p * 4 + 2] / s_qb[p * 4];
         s_v[p] = s_qb[p * 4 + 3] / s_qb[p * 4];
       } else if constexpr (C::FPRE) {
         // face lf, quad iq: own-side traces (part 0), or on a physical boundary the ghost state
         // of btp_extract_df (mod_barotropic_terms.F90:75-91) (part 1), interpolated in the
         // reference's node order (creat_btp_fluxes_qdf, mod_rhs_btp.F90:246-259)
-        const int t = w - nint - 8 * NGL - P, part = t / (4 * NQ), lf = (t / NQ) & 3, iq = t % NQ;
+        const int t = w - T_UV, part = t / (4 * NQ), lf = (t / NQ) & 3, iq = t % NQ;
         const int er = s_bc[lf];
         if (part == 0 || er < 0) {  // (er == 0: processor face, the neighbour trace is received)
           const double *efn = s_ef + lf * C::FBLK + EF_N * NQ;
@@ -592,7 +674,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       }
     }
   }
-  if constexpr (!LATE) poll_traces();  // (the granule was issued before the interpolation)
+  if constexpr (!LATE && !FD0) poll_traces();  // (the granule was issued before the interpolation)
   LDS_BARRIER();
   STAGE_MARK(1);
 
@@ -741,10 +823,20 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         dpp = s_qv[1 * Q + q];
         udp = s_qv[2 * Q + q];
         vdp = s_qv[3 * Q + q];
-        if (m.botfr) {
-          pp = s_qv[4 * Q + q];
-          up = s_qv[5 * Q + q];
-          vp = s_qv[6 * Q + q];
+        if (qpm == 2) {
+          pp = pre[NST + 4];
+          up = pre[NST + 5];
+          vp = pre[NST + 6];
+        } else if (m.botfr) {
+          pp = s_pq[0 * Q + q];
+          up = s_pq[1 * Q + q];
+          vp = s_pq[2 * Q + q];
+          if (qpm == 1) {
+            double *qq = a.qpq + (size_t)e * 3 * Q + q;
+            qq[0] = pp;
+            qq[Q] = up;
+            qq[2 * Q] = vp;
+          }
         }
       }
       const double cor = pre[QE_COR - QE_KEEP];
@@ -804,15 +896,20 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         s_qv[5 * Q + q] = sc_y;
         s_qv[6 * Q + q] = Hq + qv;
       }
-    } else if (!LATE && w >= C::OF && w < C::OF + 4 * NQ) {
+    } else if (!LATE && !FD0 && w >= C::OF && w < C::OF + 4 * NQ) {
       face_task(w - C::OF);
     } else if (w >= C::OG && w < C::OL) {
       const int p = w - C::OG, i = p % NGL, j = p / NGL;
       double g[4];
-      nodal_grad4<NGL>(s_dpsi, i, j, s_ns[NE_EX * P + p], s_ns[NE_EY * P + p], s_ns[NE_NX * P + p],
-                       s_ns[NE_NY * P + p], s_u, s_v, g);
+      if (PERSIST && !first) {  // formed by the previous stage's E2 for this same state
 #pragma unroll
-      for (int c = 0; c < 4; c++) s_grad[c * P + p] = g[c];
+        for (int c = 0; c < 4; c++) g[c] = s_grad[c * P + p];
+      } else {
+        nodal_grad4<NGL>(s_dpsi, i, j, s_ns[NE_EX * P + p], s_ns[NE_EY * P + p], s_ns[NE_NX * P + p],
+                         s_ns[NE_NY * P + p], s_u, s_v, g);
+#pragma unroll
+        for (int c = 0; c < 4; c++) s_grad[c * P + p] = g[c];
+      }
       if (a.accumulate) {
         if (!a.lapq)
 #pragma unroll
@@ -919,15 +1016,16 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       double L_[9][LB];
 #pragma unroll
       for (int r = r0; r < r0 + LB && r < NT; r++) {
-        const bool mid = (r >= j) && (r < j + NGL);
-        const int jj = mid ? j : (r < j ? r : r - NGL + 1);
-        const int ii = mid ? r - j : i;
+        const int d = r - j;
+        const bool mid = (unsigned)d < (unsigned)NGL;
+        const int jj = min(r, j) + max(d - NGL + 1, 0);
+        const int ii = mid ? d : i;
         const int s = jj * NGL + ii;
         const int b = r - r0;
         // HE_DF(i,j,ii,jj) = dpsi(i,ii) on the row (jj==j), HN_DF(i,j,ii,jj) = dpsi(j,jj) on
         // the column (ii==i), the zero slot elsewhere (see nz_coef)
-        L_[0][b] = s_dpsi[mid ? i * NGL + ii : NGL * NGL];
-        L_[1][b] = s_dpsi[(!mid || ii == i) ? j * NGL + jj : NGL * NGL];
+        L_[0][b] = s_dpsi[mid ? i * NGL + d : NGL * NGL];
+        L_[1][b] = s_dpsi[(mid & (d != i)) ? NGL * NGL : j * NGL + jj];
         L_[2][b] = s_ns[NE_EX * P + s];
         L_[3][b] = s_ns[NE_EY * P + s];
         L_[4][b] = s_ns[NE_NX * P + s];
@@ -1147,9 +1245,16 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       if (LATE && k == C::KP) issue_granule();
       for_tasks<BS>(tid, 0, WT, [&](int t, bool) { term_task(k, t); });
       if (k >= 1 && !((a.dbg & 4) && k == NCH)) for_tasks<BS>(tid, OSUM, P, [&](int t, bool) { sum_task(k - 1, t); });
-      if (k == 0) {
-        for_tasks<BS>(tid, WT, P, [&](int t, bool) { qq_task(t); });
-        if (!LATE) for_tasks<BS>(tid, C::OL, 4 * NGL, ldg_task);
+      if (k == (FD0 ? 1 : 0)) for_tasks<BS>(tid, WT, P, [&](int t, bool) { qq_task(t); });
+      if (k == 0 && !LATE && !FD0) for_tasks<BS>(tid, C::OL, 4 * NGL, ldg_task);
+      if (FD0 && k == 0 && tid >= BS - 64) {
+        // the last wave: neighbour traces (persistent: checked now), face fluxes, LDG fluxes;
+        // its own LDS writes of the traces are complete before its lanes read them
+        poll_wave();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int t = tid & 63; t < 4 * NQ; t += 64) face_task(t);
+        asm volatile("" ::: "memory");
+        for (int t = tid & 63; t < 4 * NGL; t += 64) ldg_task(t, false);
       }
       if (LATE && k == C::KP + 1) {
         for_tasks<BS>(tid, C::OFD, 4 * NQ, [&](int t, bool) { face_task(t); });
@@ -1171,7 +1276,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   if constexpr (PERSIST && !C::RES) {
     if (a.write_trace) {  // a next stage follows
       int rot = 0;
-      if (m.botfr) glds_copy<BS>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
+      if (m.botfr && qpm == 0) glds_copy<BS>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
       glds_copy<BS>(m.efstat + (size_t)e * 4 * C::FBLK, s_ef, 2 * 4 * C::FBLK, tid, rot);
       glds_copy<BS>(a.efcoef + (size_t)e * 4 * C::EFC, s_ec, 2 * 4 * C::EFC, tid, rot);
     }
@@ -1226,6 +1331,21 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     s_v[p] = qn[3] / qn[0];
   }
   if (a.rhs_only) return;
+  if (a.write_trace) {
+    // grad(u_bar) of the new state at every node, once (the sums B's nodal task forms): the
+    // traces below read it, and the persistent kernel's next stage takes it as its own.  The
+    // nodes' u_bar, v_bar were written by this same wave (P <= 64).
+    static_assert(P <= 64, "E1 and the nodal gradients run on wave 0");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (tid < P) {
+      const int p = tid, i = p % NGL, j = p / NGL;
+      double g[4];
+      nodal_grad4<NGL>(s_dpsi, i, j, s_ns[NE_EX * P + p], s_ns[NE_EY * P + p], s_ns[NE_NX * P + p],
+                       s_ns[NE_NY * P + p], s_u, s_v, g);
+#pragma unroll
+      for (int c = 0; c < 4; c++) s_grad[c * P + p] = g[c];
+    }
+  }
   LDS_BARRIER();
   STAGE_MARK(4);
 
@@ -1241,14 +1361,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       const int lf = t / (8 * NGL), c = (t / NGL) % 8, n = t % NGL;
       if (s_bc[lf] < 0) continue;  // (processor faces: into the face's send slot)
       const int p = s_map[lf * NGL + n];
-      double val;
-      if (c < 4) {
-        val = s_qn[p * 4 + c];
-      } else {
-        const int cg = c - 4, i = p % NGL, j = p / NGL;
-        const double ex = s_ns[((cg & 1) ? NE_EY : NE_EX) * P + p], nx = s_ns[((cg & 1) ? NE_NY : NE_NX) * P + p];
-        val = nodal_grad<NGL>(s_dpsi, i, j, ex, nx, (cg >> 1) ? s_v : s_u);
-      }
+      const double val = c < 4 ? s_qn[p * 4 + c] : s_grad[(c - 4) * P + p];
       const size_t slot = (((size_t)s_nbe[lf] * 4 + s_nblf[lf]) * 8 + c) * NGL + n;
       if constexpr (PERSIST)
         st_granule(a.gtr_out + slot, val, (ep << 20) | a.tag_out);
