@@ -1231,6 +1231,50 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
 #pragma unroll
       for (int v = 0; v < 3; v++) s_rhs[v * P + p] = acc[v];
     };
+    // the last chunk, one thread per (v, p) (one chain each, a third of the face-lift chain of
+    // sum_task): rhs(v,p) += T(v,p,q) over the chunk, then the face projections of component v,
+    // the same adds in the same order as sum_task
+    auto sum_last_v = [&](int v, int p) {
+      constexpr int kc = NCH - 1, nq_k = Q - kc * QC;
+      double acc = kc == 0 ? 0.0 : s_rhs[v * P + p];
+      const double *T = tbuf(kc) + (v * P + p) * QCP;
+      constexpr int SBK = 9;
+#pragma unroll 1
+      for (int q0 = 0; q0 < nq_k; q0 += SBK) {
+        double tv[SBK];
+#pragma unroll
+        for (int qi = 0; qi < SBK; qi++) tv[qi] = q0 + qi < nq_k ? T[q0 + qi] : 0.0;
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int qi = 0; qi < SBK; qi++)
+          if (q0 + qi < nq_k) acc = acc + tv[qi];
+      }
+      if (!(a.dbg & 1)) {
+#pragma unroll
+        for (int kf = 0; kf < 2; kf++) {
+          asm volatile("" ::: "memory");
+          const int r = s_pf[2 * p + kf];
+          if (r < 0) continue;
+          const int lf = r / NGL, n = r % NGL;
+          const double sg = s_side[lf] == 0 ? -1.0 : 1.0;
+          const double *fq = s_fq + lf * NQ * 4;
+          double c[NQ], fw[NQ], ps[NQ];
+#pragma unroll
+          for (int iq = 0; iq < NQ; iq++) {
+            fw[iq] = fq[iq * 4];
+            ps[iq] = s_psiq[n * NQ + iq];
+            c[iq] = fq[iq * 4 + 1 + v];
+          }
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int iq = 0; iq < NQ; iq++) acc = acc + sg * ((fw[iq] * ps[iq]) * c[iq]);
+        }
+      }
+      s_rhs[v * P + p] = acc;
+    };
+    // (the Laplacian from thread 0 in the last phase, these after it)
+    constexpr int OSV = ((2 * P + 63) / 64) * 64;
+    constexpr bool VSPLIT = OSV + 3 * P <= BS;
     // lanes: terms from 0, the sums on the last wave when they fit beside the terms, qq
     // after the terms (D0), the Laplacian from 0 in the last phase (no terms there).  Face
     // fluxes and LDG face fluxes: LATE, in chunk phase KP+1 past the terms (the persistent
@@ -1244,7 +1288,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       const int WT = (k < NCH) ? ((k == NCH - 1) ? (Q - k * QC) : QC) * NGL : 0;  // term tasks
       if (LATE && k == C::KP) issue_granule();
       for_tasks<BS>(tid, 0, WT, [&](int t, bool) { term_task(k, t); });
-      if (k >= 1 && !((a.dbg & 4) && k == NCH)) for_tasks<BS>(tid, OSUM, P, [&](int t, bool) { sum_task(k - 1, t); });
+      if (k >= 1 && k < NCH) for_tasks<BS>(tid, OSUM, P, [&](int t, bool) { sum_task(k - 1, t); });
+      if (k == NCH && !(a.dbg & 4)) {
+        if constexpr (VSPLIT)
+          for_tasks<BS>(tid, OSV, 3 * P, [&](int t, bool) { sum_last_v(t / P, t % P); });
+        else
+          for_tasks<BS>(tid, OSUM, P, [&](int t, bool) { sum_task(k - 1, t); });
+      }
       if (k == (FD0 ? 1 : 0)) for_tasks<BS>(tid, WT, P, [&](int t, bool) { qq_task(t); });
       if (k == 0 && !LATE && !FD0) for_tasks<BS>(tid, C::OL, 4 * NGL, ldg_task);
       if (FD0 && k == 0 && tid >= BS - 64) {
