@@ -92,6 +92,7 @@ struct hnumo_engine {
   // persistent sub-cycle (btp_subcycle_kernel): allowed per summation mode when every element's
   // workgroup fits on the device at once (and HNUMO_PERSISTENT != 0); used on single-rank engines
   bool persistent_ok[2] = {false, false};
+  bool regacc[2] = {false, false};           // persistent kernel keeps the averages in registers
   TraceGranule *gtr[2] = {nullptr, nullptr};  // tagged face traces of the persistent sub-cycle
   unsigned long long *epoch = nullptr;        // tag epoch, bumped before every persistent sub-cycle
   StageArgs *d_stages[2] = {nullptr, nullptr};  // per-stage arguments: predictor (qp), corrector (qp2)
@@ -189,6 +190,8 @@ struct Launch {
     (void)hipGetLastError();
     e->persistent_ok[0] = (long)nb0 * ncu >= e->nelem_owned;
     e->persistent_ok[1] = (long)nb1 * ncu >= e->nelem_owned;
+    e->regacc[0] = StageCfg<NGL, NQ, false>::REGACC;
+    e->regacc[1] = StageCfg<NGL, NQ, true>::REGACC;
   }
   // face traces of elements [e0, e0+n) into their neighbours' slots
   static void grad_trace(hnumo_engine *e, const double *qb, double *gt, int e0, int n, TraceGranule *gtr = nullptr) {
@@ -542,12 +545,14 @@ __global__ void subcycle_prologue_kernel(double *qacc, size_t nqa, double *facc,
   if (epoch && t0 == 0) *epoch = *epoch + 1;
 }
 
-static void subcycle_prologue(hnumo_engine *e, const double *qb_state, unsigned long long *epoch) {
-  const size_t nqa = QA_N * (size_t)e->npq, nfa = FA_N * 4 * (size_t)e->nelem * e->nq;
-  const int blocks = (int)std::min<size_t>((nqa + 255) / 256, 2048);
+// (zero_acc false: the persistent kernel writes every average itself, StageCfg::REGACC)
+static void subcycle_prologue(hnumo_engine *e, const double *qb_state, unsigned long long *epoch, bool zero_acc) {
+  const size_t z = zero_acc ? 1 : 0;
+  const size_t nqa = z * QA_N * (size_t)e->npq, nfa = z * FA_N * 4 * (size_t)e->nelem * e->nq;
+  const int blocks = (int)std::min<size_t>((std::max<size_t>(nqa, 4 * (size_t)e->npoin) + 255) / 256, 2048);
   hipLaunchKernelGGL(subcycle_prologue_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qacc, nqa, e->facc, nfa,
-                     e->nacc, NA_N * (size_t)e->npoin, e->gfacc, 8 * 4 * (size_t)e->nelem * e->ngl, e->qbuf[0],
-                     qb_state, 4 * (size_t)e->npoin, epoch);
+                     e->nacc, z * NA_N * (size_t)e->npoin, e->gfacc, z * 8 * 4 * (size_t)e->nelem * e->ngl,
+                     e->qbuf[0], qb_state, 4 * (size_t)e->npoin, epoch);
 }
 
 // three device copies in one launch (ti_rk_bcl.F90:53-55)
@@ -613,6 +618,7 @@ static int stage_table(hnumo_engine *e, const double *qp, std::vector<StageArgs>
       a.lapq = e->lapq_on ? e->lapq : nullptr;
       a.qpq = e->qpq;
       a.qpq_mode = stage == 0 ? 1 : 2;
+      a.n_inv = 1.0 / (double)(K * NB);
       out_args.push_back(a);
       gt = 1 - gt;
       cur = out;
@@ -630,7 +636,9 @@ static bool use_persistent(const hnumo_engine *e) {
 // ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:19-151) on device state qb_state
 static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp, bool timed = false) {
   const bool pers = use_persistent(e);
-  subcycle_prologue(e, qb_state, pers ? e->epoch : nullptr);
+  // persistent with register averages: the kernel writes them, zeroed and scaled as below
+  const bool racc = pers && e->regacc[e->summation] && !(e->stage_dbg & 32);
+  subcycle_prologue(e, qb_state, pers ? e->epoch : nullptr, !racc);
   exchange_qb(e, e->qbuf[0]);
   DISPATCH(e, grad_trace(e, e->qbuf[0], e->gtrace[0], 0, e->nelem, pers ? e->gtr[0] : nullptr));
   const int K = e->K, NB = e->p.N_btp;
@@ -687,7 +695,7 @@ static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp,
   int nblk = 1024;
   hipLaunchKernelGGL(btp_finalize_kernel, dim3(nblk), dim3(256), 0, e->stream, e->qacc, e->facc, e->nacc, e->gfacc,
                      e->tau_wind_ave, e->tau_wind, e->npq, 4 * e->nelem * e->nq, e->npoin, 4 * e->nelem * e->ngl, NB,
-                     1.0 / (double)(K * NB), qb_state, e->qbuf[cur]);
+                     1.0 / (double)(K * NB), qb_state, e->qbuf[cur], racc ? 0 : 1);
 }
 
 // the full ti_rk_bcl on device state (e->q, e->qb, e->qp)
@@ -1442,7 +1450,7 @@ int hnumo_create_rhs_btp(hnumo_engine *eng, double *rhs, const double *qb_df, co
   HIPCHK(hipSetDevice(eng->device));
   int rc = upload_state(eng, nullptr, qb_df, qprime_df);
   if (rc) return rc;
-  subcycle_prologue(eng, eng->qb, nullptr);  // zeroed time averages (qbuf[0] is the rhs-only output slot)
+  subcycle_prologue(eng, eng->qb, nullptr, true);  // zeroed time averages (qbuf[0] is the rhs-only output slot)
   DISPATCH(eng, grad_trace(eng, eng->qb, eng->gtrace[0], 0, eng->nelem));
   trace_exchange(eng, eng->gtrace[0], eng->stream);
   StageArgs a{};

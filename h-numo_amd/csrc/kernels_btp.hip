@@ -118,6 +118,7 @@ struct StageArgs {
   // interpolates and stores them (a sub-cycle's first stage), 2: loads them (the later stages)
   double *qpq;
   int qpq_mode;
+  double n_inv;                              // 1/(N_btp*kstages): the averages' normalisation
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -223,6 +224,10 @@ struct StageCfg {
   static constexpr bool FPRE = !SF && !LATE && 4 * NQ * 8 <= QN_END_W;
   // LATE chunk phase KP+1: face fluxes from OFD, LDG fluxes from OLD, past the term tasks
   static constexpr int WTMAX = QC * NGL, OFD = ((WTMAX + RU - 1) / RU) * RU, OLD = OFD + 4 * NQ;
+  // REGACC (persistent sub-cycle): every accumulating task (quad point, face quad point, node,
+  // LDG face node) has its own thread, the same in every stage, so the time averages can live in
+  // that thread's registers for the whole launch and be written once, scaled, at the end
+  static constexpr bool REGACC = WIDE && !LATE && !FD0 && OL + 4 * NGL <= BS;
 };
 
 // Nodal derivatives at node (i,j) keep the reference's 2*NGL-1 nonzero terms (mm==j or
@@ -323,8 +328,11 @@ __device__ __forceinline__ void for_tasks(int tid, int o, int n, F &&f) {
 // register loads and stores (MI355X_MICROARCH.md, inter-workgroup visibility).
 template <int NGL, int NQ, bool SF, bool PERSIST, class ARGS, int NB = 0>
 __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsigned long long *s_prof,
-                                           bool first, const int e, const int tid, unsigned long long ep = 0) {
+                                           bool first, const int e, const int tid, unsigned long long ep = 0,
+                                           double *pacc = nullptr) {
   using C = StageCfg<NGL, NQ, SF, NB>;
+  // persistent: the time averages accumulate in pacc (this thread's registers, see REGACC)
+  constexpr bool REGACC = PERSIST && C::REGACC;
   constexpr int P = C::P, Q = C::Q, BS = C::BS, NCH = C::NCH, QC = C::QC, QCP = C::QCP;
   const auto &m = a.m;
   const int npoin = m.npoin;
@@ -773,8 +781,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       add[FA_QVU] = qvu; add[FA_QVV] = qvv; add[FA_OPEL] = opl; add[FA_OPER] = opr;
       add[FA_OPE2L] = opl * opl; add[FA_OPE2R] = opr * opr; add[FA_OPEE2] = ope_e * ope_e;
       add[FA_UL] = ul; add[FA_UR] = ur; add[FA_VL] = vl; add[FA_VR] = vr;
+      if constexpr (REGACC) {
 #pragma unroll
-      for (int k = 0; k < FA_N; k++) atomicAdd(&a.facc[FACC_I(k, e * 4 + lf, iq)], add[k]);
+        for (int k = 0; k < FA_N; k++) pacc[k] = pacc[k] + add[k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < FA_N; k++) atomicAdd(&a.facc[FACC_I(k, e * 4 + lf, iq)], add[k]);
+      }
     }
     const double H_kx = nxl * Hf, H_ky = nyl * Hf;
     const double lamb = cmlr;
@@ -869,8 +882,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         add[QA_H] = Hq; add[QA_QU] = qu; add[QA_QV] = qv; add[QA_QUV] = quv;
         add[QA_TBU] = tb_u; add[QA_TBV] = tb_v; add[QA_OPE] = ope; add[QA_OPE2] = ope * ope;
         add[QA_MFX] = udp; add[QA_MFY] = vdp; add[QA_UB] = ub; add[QA_VB] = vb;
+        if constexpr (REGACC) {
 #pragma unroll
-        for (int k = 0; k < QA_N; k++) atomicAdd(&a.qacc[QACC_I(k, e, q)], add[k]);
+          for (int k = 0; k < QA_N; k++) pacc[k] = pacc[k] + add[k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < QA_N; k++) atomicAdd(&a.qacc[QACC_I(k, e, q)], add[k]);
+        }
       }
       if constexpr (SF) {
         // weighted integrands of T(v) = wq*(hi*S_v + dhdx*X_v + dhdy*Y_v) split by basis
@@ -911,13 +929,21 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         for (int c = 0; c < 4; c++) s_grad[c * P + p] = g[c];
       }
       if (a.accumulate) {
-        if (!a.lapq)
-#pragma unroll
-          for (int c = 0; c < 4; c++) atomicAdd(&a.nacc[NACC_I(NA_G1 + c, e, p)], g[c]);
         const double t1 = 1.0 + s_qb[p * 4 + 1] * s_ns[NE_OOP * P + p];
-        atomicAdd(&a.nacc[NACC_I(NA_OPE2, e, p)], t1 * t1);
-        atomicAdd(&a.nacc[NACC_I(NA_UB, e, p)], s_u[p]);
-        atomicAdd(&a.nacc[NACC_I(NA_VB, e, p)], s_v[p]);
+        if constexpr (REGACC) {  // (persistent: never the method_visc == 1 branch)
+#pragma unroll
+          for (int c = 0; c < 4; c++) pacc[NA_G1 + c] = pacc[NA_G1 + c] + g[c];
+          pacc[NA_OPE2] = pacc[NA_OPE2] + t1 * t1;
+          pacc[NA_UB] = pacc[NA_UB] + s_u[p];
+          pacc[NA_VB] = pacc[NA_VB] + s_v[p];
+        } else {
+          if (!a.lapq)
+#pragma unroll
+            for (int c = 0; c < 4; c++) atomicAdd(&a.nacc[NACC_I(NA_G1 + c, e, p)], g[c]);
+          atomicAdd(&a.nacc[NACC_I(NA_OPE2, e, p)], t1 * t1);
+          atomicAdd(&a.nacc[NACC_I(NA_UB, e, p)], s_u[p]);
+          atomicAdd(&a.nacc[NACC_I(NA_VB, e, p)], s_v[p]);
+        }
       }
     }
   }
@@ -977,8 +1003,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     if (keep) {
 #pragma unroll
       for (int c = 0; c < 4; c++) {
-        atomicAdd(&a.gfacc[GFACC_I(c, e * 4 + lf, n)], gl[c]);
-        atomicAdd(&a.gfacc[GFACC_I(4 + c, e * 4 + lf, n)], gr[c]);
+        if constexpr (REGACC) {
+          pacc[c] = pacc[c] + gl[c];
+          pacc[4 + c] = pacc[4 + c] + gr[c];
+        } else {
+          atomicAdd(&a.gfacc[GFACC_I(c, e * 4 + lf, n)], gl[c]);
+          atomicAdd(&a.gfacc[GFACC_I(4 + c, e * 4 + lf, n)], gr[c]);
+        }
       }
     }
     double fl[4], fr[4];
@@ -1419,6 +1450,30 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         a.trace_out[slot] = val;
     }
   }
+  if constexpr (REGACC) {
+    // the sub-cycle's last stage: each accumulating thread writes its time averages once, scaled
+    // as btp_finalize_kernel scales the atomically summed ones (mod_rk_mlswe.F90:124-149); the
+    // face slots of faces another element keeps get zeros, as the zeroed atomic buffers did
+    if (!a.write_trace && a.accumulate) {
+      const double ni = a.n_inv;
+      if (tid < Q) {
+#pragma unroll
+        for (int k = 0; k < QA_N; k++) a.qacc[QACC_I(k, e, tid)] = ni * pacc[k];
+      } else if (tid >= C::OF && tid < C::OF + 4 * NQ) {
+        const int t = tid - C::OF, lf = t / NQ, iq = t % NQ;
+#pragma unroll
+        for (int k = 0; k < FA_N; k++) a.facc[FACC_I(k, e * 4 + lf, iq)] = ni * pacc[k];
+      } else if (tid >= C::OG && tid < C::OL) {
+        const int p = tid - C::OG;
+#pragma unroll
+        for (int k = 0; k < NA_N; k++) a.nacc[NACC_I(k, e, p)] = ni * pacc[k];
+      } else if (tid >= C::OL && tid < C::OL + 4 * NGL) {
+        const int t = tid - C::OL, lf = t / NGL, n = t % NGL;
+#pragma unroll
+        for (int c = 0; c < 8; c++) a.gfacc[GFACC_I(c, e * 4 + lf, n)] = ni * pacc[c];
+      }
+    }
+  }
   if (a.prof) {
     LDS_BARRIER();
     STAGE_MARK(5);
@@ -1471,6 +1526,9 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
   const unsigned long long ep = *sa.epoch;
   typedef const __attribute__((address_space(4))) StageArgs CStageArgs;
   CStageArgs *tab = (CStageArgs *)sa.stages;
+  double pacc[16];  // this thread's time averages (StageCfg::REGACC)
+#pragma unroll
+  for (int k = 0; k < 16; k++) pacc[k] = 0.0;
 #pragma unroll 1
   for (int stage = 0; stage < sa.NS; stage++) {
     if (stage > 0) __syncthreads();
@@ -1479,7 +1537,7 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
     int tid_s = tid, e_s = e;
     asm volatile("" : "+v"(tid_s), "+s"(e_s));
     tid_s &= C::BS - 1;  // restore the known range of the thread index
-    stage_body<NGL, NQ, SF, true>(tab[stage], s_arena, s_prof, stage == 0, e_s, tid_s, ep);
+    stage_body<NGL, NQ, SF, true>(tab[stage], s_arena, s_prof, stage == 0, e_s, tid_s, ep, pacc);
   }
 }
 
@@ -1529,15 +1587,17 @@ __global__ void __launch_bounds__(64) grad_trace_kernel(DevMesh m, const double 
 // It also copies the sub-cycle's result state into qb_state (one launch instead of two).
 __global__ void btp_finalize_kernel(double *qacc, double *facc, double *nacc, double *gfacc, double *tau_wind_ave,
                                     const double *tau_wind, int npq, int nfq, int npoin, int nfn, int N_btp,
-                                    double N_inv, double *qb_state, const double *qb_result) {
+                                    double N_inv, double *qb_state, const double *qb_result, int scale_acc) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   if (qb_state != qb_result)
     for (size_t i = tid; i < (size_t)4 * npoin; i += stride) qb_state[i] = qb_result[i];
-  for (size_t i = tid; i < (size_t)QA_N * npq; i += stride) qacc[i] = N_inv * qacc[i];
-  for (size_t i = tid; i < (size_t)FA_N * nfq; i += stride) facc[i] = N_inv * facc[i];
-  for (size_t i = tid; i < (size_t)NA_N * npoin; i += stride) nacc[i] = N_inv * nacc[i];
-  for (size_t i = tid; i < (size_t)8 * nfn; i += stride) gfacc[i] = N_inv * gfacc[i];
+  if (scale_acc) {  // (0: the persistent kernel wrote them scaled, StageCfg::REGACC)
+    for (size_t i = tid; i < (size_t)QA_N * npq; i += stride) qacc[i] = N_inv * qacc[i];
+    for (size_t i = tid; i < (size_t)FA_N * nfq; i += stride) facc[i] = N_inv * facc[i];
+    for (size_t i = tid; i < (size_t)NA_N * npoin; i += stride) nacc[i] = N_inv * nacc[i];
+    for (size_t i = tid; i < (size_t)8 * nfn; i += stride) gfacc[i] = N_inv * gfacc[i];
+  }
   for (size_t i = tid; i < (size_t)2 * npq; i += stride) {
     double s = 0.0, t = tau_wind[i];
     for (int k = 0; k < N_btp; k++) s = s + t;
