@@ -648,30 +648,64 @@ __global__ void __launch_bounds__(64)
     mom_flux_face_kernel(DevMesh m, const double *qf, const double *facc, const double *gdpp_face,
                          const double *gfacc, double *momL, double *momR, double *lap) {
   const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L;
+  const size_t FQ = (size_t)F * NQ, FN = (size_t)F * NGL;
+  const int slot = m.fslotA[f];
+  // every input of the face in one round of independent loads (the face's qf block per layer,
+  // its 16 averages, the LDG face averages and coefficients, the face statics), then the
+  // arithmetic from LDS: one memory round trip instead of one per dependent step
   __shared__ double s_psiq[NGL * NQ], s_psi[NGL * NGL];
+  __shared__ double s_qf[MAXL][NGL * 6];          // qf(v, side, n) of each layer
+  __shared__ double s_fa[FA_N * NQ];              // face averages (FACC_I order)
+  __shared__ double s_gf[8 * NGL];                // graduvb face averages, left | right
+  __shared__ double s_gd[MAXL][10][NGL];          // graduv_dpp_face per layer
+  __shared__ double s_fs[4][NQ];                  // nx, ny, zbot left, zbot right at the quad points
+  __shared__ double s_fn[3][NGL];                 // nx, ny, w at the face nodes
   for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
   for (int t = tid; t < NGL * NGL; t += 64) s_psi[t] = m.basis[2 * NGL * NQ + NGL * NGL + t];
+  for (int t = tid; t < L * 6 * NGL; t += 64) {
+    const int k = t / (6 * NGL), r = t % (6 * NGL);
+    s_qf[k][r] = qf[((size_t)k * F + f) * NGL * 6 + r];
+  }
+  for (int t = tid; t < FA_N * NQ; t += 64) s_fa[t] = facc[FACC_I(0, slot, 0) + t];
+  for (int t = tid; t < 8 * NGL; t += 64) s_gf[t] = gfacc[GFACC_I(0, slot, 0) + t];
+  for (int t = tid; t < L * 10 * NGL; t += 64) {
+    const int k = t / (10 * NGL), c = (t / NGL) % 10, n = t % NGL;
+    s_gd[k][c][n] = gdpp_face[((size_t)k * 10 + c) * FN + (size_t)f * NGL + n];
+  }
+  if (tid < 4 * NQ) {
+    const int c = tid / NQ, iq = tid % NQ;
+    const int fld[4] = {FS_NX, FS_NY, FS_ZBL, FS_ZBR};
+    s_fs[c][iq] = m.fstat[fld[c] * FQ + (size_t)f * NQ + iq];
+  }
+  if (tid < 3 * NGL) {
+    const int c = tid / NGL, n = tid % NGL;
+    const int fld[3] = {FN_NX, FN_NY, FN_W};
+    s_fn[c][n] = m.fnstat[fld[c] * FN + (size_t)f * NGL + n];
+  }
   __syncthreads();
-  const size_t FQ = (size_t)F * NQ, FN = (size_t)F * NGL;
   const int er = m.fer[f];
   const double g = m.gravity, eps1 = 1.0e-20;
+#define FA(k) s_fa[(k) * NQ + iq]
   if (tid < NQ) {
     const int iq = tid;
     const size_t fq = (size_t)f * NQ + iq;
     const double *alpha = m.alpha;
-    double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
-    double qbl0 = facc[FACC_I(FA_OPEL, m.fslotA[f], iq)], qbr0 = facc[FACC_I(FA_OPER, m.fslotA[f], iq)];
-    double qbl1 = facc[FACC_I(FA_UL, m.fslotA[f], iq)], qbr1 = facc[FACC_I(FA_UR, m.fslotA[f], iq)];
-    double qbl2 = facc[FACC_I(FA_VL, m.fslotA[f], iq)], qbr2 = facc[FACC_I(FA_VR, m.fslotA[f], iq)];
+    double nxl = s_fs[0][iq], nyl = s_fs[1][iq];
+    double qbl0 = FA(FA_OPEL), qbr0 = FA(FA_OPER);
+    double qbl1 = FA(FA_UL), qbr1 = FA(FA_UR);
+    double qbl2 = FA(FA_VL), qbr2 = FA(FA_VR);
     double ql[MAXL][3], qr[MAXL][3], udpl[MAXL], udpr[MAXL], vdpl[MAXL], vdpr[MAXL];
     double udpf[2][MAXL], vdpf[2][MAXL], Hf[2][MAXL];
-    for (int k = 0; k < L; k++) {
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
       for (int v = 0; v < 3; v++) ql[k][v] = qr[k][v] = 0.0;
+#pragma unroll
       for (int n = 0; n < NGL; n++) {
         double hi = s_psiq[n * NQ + iq];
         for (int v = 0; v < 3; v++) {
-          ql[k][v] = ql[k][v] + hi * QF(v, 0, n, f, k);
-          qr[k][v] = qr[k][v] + hi * QF(v, 1, n, f, k);
+          ql[k][v] = ql[k][v] + hi * s_qf[k][(n * 2 + 0) * 3 + v];
+          qr[k][v] = qr[k][v] + hi * s_qf[k][(n * 2 + 1) * 3 + v];
         }
       }
       double dpl = qbl0 * ql[k][0], dpr = qbr0 * qr[k][0];
@@ -697,45 +731,74 @@ __global__ void __launch_bounds__(64)
       }
     }
     double s1 = 0, s2 = 0, s3 = 0, s4 = 0;
-    for (int k = 0; k < L; k++) s1 = s1 + udpf[0][k];
-    for (int k = 0; k < L; k++) s2 = s2 + udpf[1][k];
-    for (int k = 0; k < L; k++) s3 = s3 + vdpf[0][k];
-    for (int k = 0; k < L; k++) s4 = s4 + vdpf[1][k];
-    double uu_def = facc[FACC_I(FA_QUU, m.fslotA[f], iq)] - s1, uv_def = facc[FACC_I(FA_QUV, m.fslotA[f], iq)] - s2;
-    double vu_def = facc[FACC_I(FA_QVU, m.fslotA[f], iq)] - s3, vv_def = facc[FACC_I(FA_QVV, m.fslotA[f], iq)] - s4;
+#pragma unroll
+    for (int k = 0; k < MAXL; k++)
+      if (k < L) s1 = s1 + udpf[0][k];
+#pragma unroll
+    for (int k = 0; k < MAXL; k++)
+      if (k < L) s2 = s2 + udpf[1][k];
+#pragma unroll
+    for (int k = 0; k < MAXL; k++)
+      if (k < L) s3 = s3 + vdpf[0][k];
+#pragma unroll
+    for (int k = 0; k < MAXL; k++)
+      if (k < L) s4 = s4 + vdpf[1][k];
+    double uu_def = FA(FA_QUU) - s1, uv_def = FA(FA_QUV) - s2;
+    double vu_def = FA(FA_QVU) - s3, vv_def = FA(FA_QVV) - s4;
     double sl = 0, sr = 0;
-    for (int k = 0; k < L; k++) sl = sl + (fabs(udpl[k]) + eps1);
-    for (int k = 0; k < L; k++) sr = sr + (fabs(udpr[k]) + eps1);
+#pragma unroll
+    for (int k = 0; k < MAXL; k++)
+      if (k < L) sl = sl + (fabs(udpl[k]) + eps1);
+#pragma unroll
+    for (int k = 0; k < MAXL; k++)
+      if (k < L) sr = sr + (fabs(udpr[k]) + eps1);
     double oosl = 1.0 / sl, oosr = 1.0 / sr;
-    for (int k = 0; k < L; k++) {
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
       udpf[0][k] = udpf[0][k] + ((uu_def * nxl > 0.0) ? fabs(udpl[k]) * oosl : fabs(udpr[k]) * oosr) * uu_def;
       udpf[1][k] = udpf[1][k] + ((uv_def * nyl > 0.0) ? fabs(udpl[k]) * oosl : fabs(udpr[k]) * oosr) * uv_def;
     }
     sl = 0;
     sr = 0;
-    for (int k = 0; k < L; k++) sl = sl + (fabs(vdpl[k]) + eps1);
-    for (int k = 0; k < L; k++) sr = sr + (fabs(vdpr[k]) + eps1);
+#pragma unroll
+    for (int k = 0; k < MAXL; k++)
+      if (k < L) sl = sl + (fabs(vdpl[k]) + eps1);
+#pragma unroll
+    for (int k = 0; k < MAXL; k++)
+      if (k < L) sr = sr + (fabs(vdpr[k]) + eps1);
     oosl = 1.0 / sl;
     oosr = 1.0 / sr;
-    for (int k = 0; k < L; k++) {
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
       vdpf[0][k] = vdpf[0][k] + ((vu_def * nxl > 0.0) ? fabs(vdpl[k]) * oosl : fabs(vdpr[k]) * oosr) * vu_def;
       vdpf[1][k] = vdpf[1][k] + ((vv_def * nyl > 0.0) ? fabs(vdpl[k]) * oosl : fabs(vdpr[k]) * oosr) * vv_def;
     }
     // H_r at the face (layer-overlap pressure, :627-707)
     double pf[2][MAXL + 1], zf[2][MAXL + 1], pep[MAXL + 1], pem[MAXL + 1], zep[MAXL + 1], zem[MAXL + 1];
-    for (int k = 0; k <= L; k++) zf[0][k] = zf[1][k] = pf[0][k] = pf[1][k] = zep[k] = zem[k] = pep[k] = pem[k] = 0.0;
-    double ope_l = sqrt(facc[FACC_I(FA_OPE2L, m.fslotA[f], iq)]), ope_r = sqrt(facc[FACC_I(FA_OPE2R, m.fslotA[f], iq)]);
-    for (int k = 1; k <= L; k++) {
+#pragma unroll
+    for (int k = 0; k <= MAXL; k++) zf[0][k] = zf[1][k] = pf[0][k] = pf[1][k] = zep[k] = zem[k] = pep[k] = pem[k] = 0.0;
+    double ope_l = sqrt(FA(FA_OPE2L)), ope_r = sqrt(FA(FA_OPE2R));
+#pragma unroll
+    for (int k = 1; k <= MAXL; k++) {
+      if (k > L) break;
       pf[0][k] = pf[0][k - 1] + ope_l * ql[k - 1][0];
       pf[1][k] = pf[1][k - 1] + ope_r * qr[k - 1][0];
     }
-    double ope_e = sqrt(facc[FACC_I(FA_OPEE2, m.fslotA[f], iq)]);
-    double zbl = m.fstat[FS_ZBL * FQ + fq], zbr = m.fstat[FS_ZBR * FQ + fq];
-    zf[0][L] = zbl;
-    zf[1][L] = zbr;
-    zep[L] = zbl;
-    zem[L] = zbr;
-    for (int k = L; k >= 1; k--) {
+    double ope_e = sqrt(FA(FA_OPEE2));
+    double zbl = s_fs[2][iq], zbr = s_fs[3][iq];
+#pragma unroll
+    for (int k = 1; k <= MAXL; k++)
+      if (k == L) {
+        zf[0][k] = zbl;
+        zf[1][k] = zbr;
+        zep[k] = zbl;
+        zem[k] = zbr;
+      }
+#pragma unroll
+    for (int k = MAXL; k >= 1; k--) {
+      if (k > L) continue;
       double aog = alpha[k - 1] / g;
       zf[0][k - 1] = zf[0][k] + aog * (ope_l * ql[k - 1][0]);
       zf[1][k - 1] = zf[1][k] + aog * (ope_r * qr[k - 1][0]);
@@ -744,14 +807,20 @@ __global__ void __launch_bounds__(64)
     }
     pep[1] = ope_e * ql[0][0];
     pem[1] = ope_e * qr[0][0];
-    for (int k = 2; k <= L; k++) {
+#pragma unroll
+    for (int k = 2; k <= MAXL; k++) {
+      if (k > L) break;
       pep[k] = pep[k - 1] + ope_e * ql[k - 1][0];
       pem[k] = pem[k - 1] + ope_e * qr[k - 1][0];
     }
-    for (int k = 1; k <= L; k++) {
+#pragma unroll
+    for (int k = 1; k <= MAXL; k++) {
+      if (k > L) break;
       double Hrp = 0.5 * alpha[k - 1] * (pep[k] * pep[k] - pep[k - 1] * pep[k - 1]);
       double Hrm = 0.0;
-      for (int kt = 1; kt <= L; kt++) {
+#pragma unroll
+      for (int kt = 1; kt <= MAXL; kt++) {
+        if (kt > L) break;
         double goa = g / alpha[kt - 1];
         double zt = dmin(zem[kt - 1], zep[k - 1]), zb = dmax(zem[kt], zep[k]);
         if (zt - zb > 0.0) {
@@ -763,7 +832,9 @@ __global__ void __launch_bounds__(64)
       Hf[0][k - 1] = 0.5 * (Hrp + Hrm);
       Hrm = 0.5 * alpha[k - 1] * (pem[k] * pem[k] - pem[k - 1] * pem[k - 1]);
       Hrp = 0.0;
-      for (int kt = 1; kt <= L; kt++) {
+#pragma unroll
+      for (int kt = 1; kt <= MAXL; kt++) {
+        if (kt > L) break;
         double goa = g / alpha[kt - 1];
         double zt = dmin(zep[kt - 1], zem[k - 1]), zb = dmax(zep[kt], zem[k]);
         if (zt - zb > 0.0) {
@@ -775,12 +846,16 @@ __global__ void __launch_bounds__(64)
       Hf[1][k - 1] = 0.5 * (Hrp + Hrm);
     }
     if (er == -4) {
-      for (int k = 1; k <= L; k++) {
+#pragma unroll
+      for (int k = 1; k <= MAXL; k++) {
+        if (k > L) break;
         Hf[0][k - 1] = 0.5 * alpha[k - 1] * (pf[0][k] * pf[0][k] - pf[0][k - 1] * pf[0][k - 1]);
         Hf[1][k - 1] = 0.5 * alpha[k - 1] * (pf[1][k] * pf[1][k] - pf[1][k - 1] * pf[1][k - 1]);
       }
     } else {
-      for (int k = 1; k <= L - 1; k++) {
+#pragma unroll
+      for (int k = 1; k <= MAXL - 1; k++) {
+        if (k > L - 1) break;
         double goa = g / alpha[k - 1];
         double pinc1 = goa * (zf[0][k] - zep[k]);
         double Hc1 = 0.5 * alpha[k - 1] * ((pf[0][k] + pinc1) * (pf[0][k] + pinc1) - pf[0][k] * pf[0][k]);
@@ -792,14 +867,21 @@ __global__ void __launch_bounds__(64)
         Hf[1][k] = Hf[1][k] + Hc2;
       }
     }
-    double hfa = facc[FACC_I(FA_H, m.fslotA[f], iq)];
+    double hfa = FA(FA_H);
+#pragma unroll
     for (int sd = 0; sd < 2; sd++) {
       double weight = 1.0, acc = 0.0;
-      for (int k = 0; k < L; k++) acc = acc + Hf[sd][k];
+#pragma unroll
+      for (int k = 0; k < MAXL; k++)
+        if (k < L) acc = acc + Hf[sd][k];
       if (acc > 0.0) weight = hfa / acc;
-      for (int k = 0; k < L; k++) Hf[sd][k] = Hf[sd][k] * weight;
+#pragma unroll
+      for (int k = 0; k < MAXL; k++)
+        if (k < L) Hf[sd][k] = Hf[sd][k] * weight;
     }
-    for (int k = 0; k < L; k++) {
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
       double hlx = nxl * Hf[0][k], hrx = nxl * Hf[1][k], hly = nyl * Hf[0][k], hry = nyl * Hf[1][k];
       double flux_x = nxl * udpf[0][k] + nyl * udpf[1][k];
       double flux_y = nxl * vdpf[0][k] + nyl * vdpf[1][k];
@@ -812,15 +894,15 @@ __global__ void __launch_bounds__(64)
     // layer LDG flux at face node n for every layer
     const int n = tid - 32;
     const size_t fn = (size_t)f * NGL + n;
-    double nx = m.fnstat[FN_NX * FN + fn], ny = m.fnstat[FN_NY * FN + fn], wq = m.fnstat[FN_W * FN + fn];
+    double nx = s_fn[0][n], ny = s_fn[1][n], wq = s_fn[2][n];
     const double beta = 0.5, alpha = 1.0 - beta;
-    for (int k = 0; k < L; k++) {
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
       double fl[4], fr[4];
       for (int iv = 0; iv < 4; iv++) {
-        fl[iv] = gdpp_face[((size_t)k * 10 + 4) * FN + fn] * gfacc[GFACC_I(iv, m.fslotA[f], n)] +
-                 gdpp_face[((size_t)k * 10 + iv) * FN + fn];
-        fr[iv] = gdpp_face[((size_t)k * 10 + 9) * FN + fn] * gfacc[GFACC_I(4 + iv, m.fslotA[f], n)] +
-                 gdpp_face[((size_t)k * 10 + 5 + iv) * FN + fn];
+        fl[iv] = s_gd[k][4][n] * s_gf[iv * NGL + n] + s_gd[k][iv][n];
+        fr[iv] = s_gd[k][9][n] * s_gf[(4 + iv) * NGL + n] + s_gd[k][5 + iv][n];
       }
       double qum0 = alpha * fl[0] + beta * fr[0], qum1 = alpha * fl[1] + beta * fr[1];
       double qvm0 = alpha * fl[2] + beta * fr[2], qvm1 = alpha * fl[3] + beta * fr[3];
@@ -831,6 +913,7 @@ __global__ void __launch_bounds__(64)
       lap[((size_t)k * 2 + 1) * FN + fn] = wq * h1 * flux_qv;
     }
   }
+#undef FA
 }
 
 // ===================================== layer momentum: element volume + update
@@ -847,7 +930,7 @@ struct MomCfg {
 };
 
 template <int NGL, int NQ>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, 3)
     mom_elem_kernel(DevMesh m, const double *qp_in, const double *qacc, const double *nacc, const double *dpp_graduv,
                     const double *dpprime_visc, const double *momL, const double *momR, const double *lapf,
                     const double *qb, double *q, double *qp_out, int mode, const double *lapx) {
