@@ -54,18 +54,49 @@ __device__ __forceinline__ void load_basis(const DevMesh &m, double *s_psiq, dou
 
 // sum_q w(q)*(dpsidx(p,q)*fx(q) + dpsidy(p,q)*fy(q)) accumulated onto acc in quad order
 // (the weak-form divergence of mod_create_rhs_mlswe.F90:866-868 / :911-913)
+// (the thread's basis row psiq(i,:), dpsiq(i,:) in registers; a quad row per iteration, its
+// loads independent of the chain, so only the adds are serial)
 template <int NGL, int NQ>
 __device__ __forceinline__ double weak_div(const double *s_psiq, const double *s_dpsiq, const double *qm0,
                                            const double *qm1, const double *qm2, const double *qm3, const double *w,
                                            const double *fx, const double *fy, int i, int j, double acc) {
-  for (int q = 0; q < NQ * NQ; q++) {
-    const int iq = q % NQ, jq = q / NQ;
-    const double h_e = HE(i, j, iq, jq), h_n = HN(i, j, iq, jq);
-    const double dhdx = h_e * qm0[q] + h_n * qm2[q];
-    const double dhdy = h_e * qm1[q] + h_n * qm3[q];
-    acc = acc + w[q] * (dhdx * fx[q] + dhdy * fy[q]);
+  double pi[NQ], dpi[NQ];
+#pragma unroll
+  for (int iq = 0; iq < NQ; iq++) {
+    pi[iq] = s_psiq[i * NQ + iq];
+    dpi[iq] = s_dpsiq[i * NQ + iq];
+  }
+#pragma unroll 1
+  for (int jq = 0; jq < NQ; jq++) {
+    const double pj = s_psiq[j * NQ + jq], dpj = s_dpsiq[j * NQ + jq];
+#pragma unroll
+    for (int iq = 0; iq < NQ; iq++) {
+      const int q = jq * NQ + iq;
+      const double h_e = dpi[iq] * pj, h_n = pi[iq] * dpj;  // HE(i,j,iq,jq), HN(i,j,iq,jq)
+      const double dhdx = h_e * qm0[q] + h_n * qm2[q];
+      const double dhdy = h_e * qm1[q] + h_n * qm3[q];
+      acc = acc + w[q] * (dhdx * fx[q] + dhdy * fy[q]);
+    }
   }
   return acc;
+}
+
+// sum over the element's nodes of PSIH(n,mm,iq,jq)*x(v, mm*NGL+n), mm outer, n inner (the
+// reference's interpolation order), for NV components x[v*stride + node]; pa/pb = the thread's
+// psiq(:,iq), psiq(:,jq)
+template <int NGL, int NV>
+__device__ __forceinline__ void interp_q(const double *pa, const double *pb, const double *x, int stride,
+                                         double out[NV]) {
+#pragma unroll
+  for (int v = 0; v < NV; v++) out[v] = 0.0;
+#pragma unroll 1
+  for (int mm = 0; mm < NGL; mm++)
+#pragma unroll
+    for (int n = 0; n < NGL; n++) {
+      const double hi = pa[n] * pb[mm];
+#pragma unroll
+      for (int v = 0; v < NV; v++) out[v] = out[v] + hi * x[v * stride + mm * NGL + n];
+    }
 }
 
 // Face terms of one face onto node p: acc -/+ (wq*hi)*flux(iq), quad order (left: -, right: +),
@@ -103,6 +134,17 @@ __device__ __forceinline__ void stage_face_quads(double *dst, const double *src,
     dst[t] = src[c * cstride + (size_t)efaces_e[lf] * NQ + iq];
   }
 }
+
+// A face's qf block (v, side, n) of every layer into s_qf[k][6*NGL] (contiguous per layer)
+template <int NGL>
+__device__ __forceinline__ void stage_qf(double (*s_qf)[6 * NGL], const double *qf, int f, int F, int L, int tid,
+                                         int bs) {
+  for (int t = tid; t < L * 6 * NGL; t += bs) {
+    const int k = t / (6 * NGL), r = t % (6 * NGL);
+    s_qf[k][r] = qf[((size_t)k * F + f) * NGL * 6 + r];
+  }
+}
+#define SQF(v, s, n, k) s_qf[k][((n)*2 + (s)) * 3 + (v)]
 
 // ===================================================================== face traces
 // extract_qprime_df_face: qf(3,2,ngl,nface,L) from nodal qprime(3,npoin,L), with wall ghosts.
@@ -182,13 +224,17 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
   for (int q = tid; q < Q; q += BS) {
     const int iq = q % NQ, jq = q / NQ;
     double quu = 0.0, quv = 0.0, qvv = 0.0, hb = 0.0, pk = 0.0;
-    for (int k = 0; k < L; k++) {
-      double qq[3] = {0.0, 0.0, 0.0};
-      for (int mm = 0; mm < NGL; mm++)
-        for (int n = 0; n < NGL; n++) {
-          const double hi = PSIH(n, mm, iq, jq);
-          for (int v = 0; v < 3; v++) qq[v] = qq[v] + hi * s_q[k][v][mm * NGL + n];
-        }
+    double pa[NGL], pb[NGL];
+#pragma unroll
+    for (int n = 0; n < NGL; n++) {
+      pa[n] = s_psiq[n * NQ + iq];
+      pb[n] = s_psiq[n * NQ + jq];
+    }
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
+      double qq[3];
+      interp_q<NGL, 3>(pa, pb, &s_q[k][0][0], P, qq);
       quu = quu + qq[1] * (qq[1] * qq[0]);
       quv = quv + qq[2] * (qq[1] * qq[0]);
       qvv = qvv + qq[2] * (qq[2] * qq[0]);
@@ -212,9 +258,23 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     const int k = t / (4 * P), c = (t / P) % 4, p = t % P, i = p % NGL, j = p / NGL;
     const double *u = s_q[k][1 + (c >> 1)];
     const double ex = s_nm[(c & 1) ? 1 : 0][p], nx = s_nm[(c & 1) ? 3 : 2][p];
+    // the 2*NGL-1 nonzero terms (row mm == j, column n == i) of the reference's 25-term sum, in
+    // its order: with psi the identity at the LGL nodes (checked at engine creation) HE_DF =
+    // dpsi(n,i) on the row and HN_DF = dpsi(mm,j) on the column, zero elsewhere, and a dropped
+    // zero term leaves the sum unchanged (as in the stage kernel's nodal_grad)
+    double cA[2 * NGL - 1], cB[2 * NGL - 1], cU[2 * NGL - 1];
+#pragma unroll
+    for (int r = 0; r < 2 * NGL - 1; r++) {
+      const int d = r - j;
+      const bool row = (unsigned)d < (unsigned)NGL;
+      const int mm = min(r, j) + max(d - NGL + 1, 0), n = row ? d : i;
+      cA[r] = row ? s_dpsi[n * NGL + i] : 0.0;
+      cB[r] = (row & (d != i)) ? 0.0 : s_dpsi[mm * NGL + j];
+      cU[r] = u[mm * NGL + n];
+    }
     double gsum = 0.0;
-    for (int mm = 0; mm < NGL; mm++)
-      for (int n = 0; n < NGL; n++) gsum = gsum + (HE_DF(n, mm, i, j) * ex + HN_DF(n, mm, i, j) * nx) * u[mm * NGL + n];
+#pragma unroll
+    for (int r = 0; r < 2 * NGL - 1; r++) gsum = gsum + (cA[r] * ex + cB[r] * nx) * cU[r];
     s_g[k][c][p] = gsum;
   }
   __syncthreads();
@@ -248,19 +308,32 @@ __global__ void __launch_bounds__(64)
                            double *fcoef, double *fncoef, double *gdpp_face, double *efcoef) {
   const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L, npoin = m.npoin;
   __shared__ double s_psiq[NGL * NQ];
-  for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
-  __syncthreads();
+  __shared__ double s_qf[MAXL][6 * NGL];
+  __shared__ double s_lr[MAXL][2][5][NGL];  // dpp_graduv(4), dpprime_visc at the left | right face nodes
   const size_t FQ = (size_t)F * NQ, FN = (size_t)F * NGL;
+  const int erf = m.fer[f];
+  for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
+  stage_qf<NGL>(s_qf, qf, f, F, L, tid, 64);
+  for (int t = tid; t < L * 2 * 5 * NGL; t += 64) {
+    const int k = t / (10 * NGL), sd = (t / (5 * NGL)) % 2, c = (t / NGL) % 5, n = t % NGL;
+    if (sd == 1 && erf <= 0) continue;
+    const int I = (sd ? m.fnodeR : m.fnodeL)[(size_t)f * NGL + n];
+    s_lr[k][sd][c][n] = c < 4 ? dpp_graduv[((size_t)k * 4 + c) * npoin + I] : dpprime_visc[(size_t)k * npoin + I];
+  }
+  __syncthreads();
   if (tid < NQ) {
     const int iq = tid;
     double quu = 0, quv = 0, qvv = 0, hb = 0, pl = 0, pr = 0;
-    for (int k = 0; k < L; k++) {
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
       double ql[3] = {0, 0, 0}, qr[3] = {0, 0, 0};
+#pragma unroll
       for (int n = 0; n < NGL; n++) {
         double hi = s_psiq[n * NQ + iq];
         for (int v = 0; v < 3; v++) {
-          ql[v] = ql[v] + hi * QF(v, 0, n, f, k);
-          qr[v] = qr[v] + hi * QF(v, 1, n, f, k);
+          ql[v] = ql[v] + hi * SQF(v, 0, n, k);
+          qr[v] = qr[v] + hi * SQF(v, 1, n, k);
         }
       }
       quu = quu + 0.5 * ((ql[1] * ql[1] * ql[0]) + (qr[1] * qr[1] * qr[0]));
@@ -288,18 +361,17 @@ __global__ void __launch_bounds__(64)
       if (sr >= 0) efcoef[(size_t)sr * EFC + c * NQ + iq] = vals[c];
     }
   } else if (tid >= 32 && tid < 32 + NGL) {
-    const int n = tid - 32, er = m.fer[f];
+    const int n = tid - 32, er = erf;
     const size_t fn = (size_t)f * NGL + n;
-    const int IL = m.fnodeL[fn], IR = m.fnodeR[fn];
     double nx = m.fnstat[FN_NX * FN + fn], ny = m.fnstat[FN_NY * FN + fn];
     double bsum[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    for (int k = 0; k < L; k++) {
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
       double l[5], r[5];
-      for (int c = 0; c < 4; c++) l[c] = dpp_graduv[((size_t)k * 4 + c) * npoin + IL];
-      l[4] = dpprime_visc[(size_t)k * npoin + IL];
+      for (int c = 0; c < 5; c++) l[c] = s_lr[k][0][c][n];
       if (er > 0) {
-        for (int c = 0; c < 4; c++) r[c] = dpp_graduv[((size_t)k * 4 + c) * npoin + IR];
-        r[4] = dpprime_visc[(size_t)k * npoin + IR];
+        for (int c = 0; c < 5; c++) r[c] = s_lr[k][1][c][n];
       } else {
         for (int c = 0; c < 5; c++) r[c] = l[c];
         if (er == -4) {
@@ -339,7 +411,9 @@ __global__ void __launch_bounds__(64)
     mass_flux_face_kernel(DevMesh m, const double *qf, const double *facc, double *fmass, double *slmf_face) {
   const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L;
   __shared__ double s_psiq[NGL * NQ];
+  __shared__ double s_qf[MAXL][6 * NGL];
   for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
+  stage_qf<NGL>(s_qf, qf, f, F, L, tid, 64);
   __syncthreads();
   const size_t FQ = (size_t)F * NQ;
   if (tid < NQ) {
@@ -350,13 +424,16 @@ __global__ void __launch_bounds__(64)
     double qbl1 = facc[FACC_I(FA_UL, m.fslotA[f], iq)], qbr1 = facc[FACC_I(FA_UR, m.fslotA[f], iq)];
     double qbl2 = facc[FACC_I(FA_VL, m.fslotA[f], iq)], qbr2 = facc[FACC_I(FA_VR, m.fslotA[f], iq)];
     double su = 0.0, sv = 0.0;
-    for (int k = 0; k < L; k++) {
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
       double ql[3] = {0, 0, 0}, qr[3] = {0, 0, 0};
+#pragma unroll
       for (int n = 0; n < NGL; n++) {
         double hi = s_psiq[n * NQ + iq];
         for (int v = 0; v < 3; v++) {
-          ql[v] = ql[v] + hi * QF(v, 0, n, f, k);
-          qr[v] = qr[v] + hi * QF(v, 1, n, f, k);
+          ql[v] = ql[v] + hi * SQF(v, 0, n, k);
+          qr[v] = qr[v] + hi * SQF(v, 1, n, k);
         }
       }
       double uu = 0.5 * ((ql[1] + qbl1) + (qr[1] + qbr1));
@@ -385,24 +462,33 @@ __global__ void __launch_bounds__(64)
     cons_flux_face_kernel(DevMesh m, const double *dpp, const double *facc, const double *slmf_face, double *fcons,
                           double *cdef) {
   const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L, npoin = m.npoin;
+  const int erf = m.fer[f];
   __shared__ double s_psiq[NGL * NQ];
+  __shared__ double s_dn[MAXL][2][NGL];  // dp' at the left | right face nodes
   for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
+  for (int t = tid; t < L * 2 * NGL; t += 64) {
+    const int k = t / (2 * NGL), sd = (t / NGL) % 2, n = t % NGL;
+    if (sd == 1 && erf <= 0) continue;
+    s_dn[k][sd][n] = dpp[(size_t)k * npoin + (sd ? m.fnodeR : m.fnodeL)[(size_t)f * NGL + n]];
+  }
   __syncthreads();
   const size_t FQ = (size_t)F * NQ;
   if (tid < NQ) {
-    const int iq = tid, er = m.fer[f];
+    const int iq = tid, er = erf;
     const size_t fq = (size_t)f * NQ + iq;
     double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
     double d1 = facc[FACC_I(FA_MFX, m.fslotA[f], iq)] - slmf_face[0 * FQ + fq];
     double d2 = facc[FACC_I(FA_MFY, m.fslotA[f], iq)] - slmf_face[1 * FQ + fq];
     double pbl = m.fstat[FS_PBL * FQ + fq], pbr = m.fstat[FS_PBR * FQ + fq];
-    for (int k = 0; k < L; k++) {
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
       double ql = 0.0, qr = 0.0;
-      for (int n = 0; n < NGL; n++)
-        ql = ql + s_psiq[n * NQ + iq] * dpp[(size_t)k * npoin + m.fnodeL[(size_t)f * NGL + n]];
+#pragma unroll
+      for (int n = 0; n < NGL; n++) ql = ql + s_psiq[n * NQ + iq] * s_dn[k][0][n];
       if (er > 0) {
-        for (int n = 0; n < NGL; n++)
-          qr = qr + s_psiq[n * NQ + iq] * dpp[(size_t)k * npoin + m.fnodeR[(size_t)f * NGL + n]];
+#pragma unroll
+        for (int n = 0; n < NGL; n++) qr = qr + s_psiq[n * NQ + iq] * s_dn[k][1][n];
       } else {
         qr = ql;
       }
@@ -527,14 +613,18 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     const size_t Iq = (size_t)e * Q + q;
     double qb0 = qacc[QACC_I(QA_OPE, e, q)], qb1 = qacc[QACC_I(QA_UB, e, q)],
            qb2 = qacc[QACC_I(QA_VB, e, q)];
+    double pa[NGL], pb[NGL];
+#pragma unroll
+    for (int n = 0; n < NGL; n++) {
+      pa[n] = s_psiq[n * NQ + iq];
+      pb[n] = s_psiq[n * NQ + jq];
+    }
     double su = 0.0, sv = 0.0;
-    for (int k = 0; k < L; k++) {
-      double qq[3] = {0.0, 0.0, 0.0};
-      for (int mm = 0; mm < NGL; mm++)
-        for (int n = 0; n < NGL; n++) {
-          const double hi = PSIH(n, mm, iq, jq);
-          for (int v = 0; v < 3; v++) qq[v] = qq[v] + hi * s_q[k][v][mm * NGL + n];
-        }
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
+      double qq[3];
+      interp_q<NGL, 3>(pa, pb, &s_q[k][0][0], P, qq);
       double dp_temp = qq[0] * qb0;
       double udp = (qq[1] + qb1) * dp_temp;
       double vdp = (qq[2] + qb2) * dp_temp;
@@ -606,10 +696,18 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     double pb = m.qstat[QS_PB * (size_t)npq + Iq];
     double dx = qacc[QACC_I(QA_MFX, e, q)] - slmf[0 * (size_t)npq + Iq];
     double dy = qacc[QACC_I(QA_MFY, e, q)] - slmf[1 * (size_t)npq + Iq];
-    for (int k = 0; k < L; k++) {
-      double dp = 0.0;
-      for (int mm = 0; mm < NGL; mm++)
-        for (int n = 0; n < NGL; n++) dp = dp + PSIH(n, mm, iq, jq) * s_d[k][mm * NGL + n];
+    double pa[NGL], pbq[NGL];
+#pragma unroll
+    for (int n = 0; n < NGL; n++) {
+      pa[n] = s_psiq[n * NQ + iq];
+      pbq[n] = s_psiq[n * NQ + jq];
+    }
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
+      double dpv[1];
+      interp_q<NGL, 1>(pa, pbq, &s_d[k][0], P, dpv);
+      const double dp = dpv[0];
       double weight = dp / pb;
       s_f[k][0][q] = weight * dx;
       s_f[k][1][q] = weight * dy;

@@ -1,0 +1,27 @@
+#!/bin/bash
+# SQ counters of the baroclinic / glue kernels over a short dg25L3 bench (kernel-trace only, one
+# --pmc set per run).  Usage (via gpurun): bash tools/pmc_glue.sh [outdir]
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=${1:-gpurun_out/pmc_glue}
+mkdir -p $OUT
+i=0
+for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU" \
+           "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_ANY"; do
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $set -d $OUT/p$i -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-c4 --steps 2 --warmup 1 > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
+  i=$((i+1))
+done
+python3 - "$OUT" <<'PY'
+import csv, glob, collections, sys
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in glob.glob(sys.argv[1] + "/p*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        agg[r["Kernel_Name"][:40]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+with open(sys.argv[1] + "/summary.txt", "w") as fh:
+    for kn, d in sorted(agg.items()):
+        w = sum(d["SQ_WAVES"]) / max(len(d["SQ_WAVES"]), 1) if d["SQ_WAVES"] else 0
+        line = kn + " " + " ".join(f"{k}={sum(v)/len(v):.0f}" for k, v in sorted(d.items()))
+        print(line)
+        fh.write(line + "\n")
+PY
