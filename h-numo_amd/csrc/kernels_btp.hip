@@ -277,26 +277,29 @@ __device__ __forceinline__ double nodal_grad(const double *s_dpsi, int i, int j,
 template <int NGL>
 __device__ __forceinline__ void nodal_grad4(const double *s_dpsi, int i, int j, double ex, double ey, double nx,
                                             double ny, const double *s_u, const double *s_v, double g[4]) {
-  constexpr int NT = 2 * NGL - 1;
-  double A[NT], B[NT], U[NT], V[NT];
-#pragma unroll
-  for (int r = 0; r < NT; r++) {
-    int mm, n, ia, ib;
-    nz_coef<NGL>(r, i, j, mm, n, ia, ib);
-    A[r] = s_dpsi[ia];
-    B[r] = s_dpsi[ib];
-    U[r] = s_u[mm * NGL + n];
-    V[r] = s_v[mm * NGL + n];
-  }
-  asm volatile("" ::: "memory");
+  constexpr int NT = 2 * NGL - 1, GB = NT <= 9 ? NT : 5;  // terms per load batch (VGPRs at NGL = 8)
   g[0] = g[1] = g[2] = g[3] = 0.0;
 #pragma unroll
-  for (int r = 0; r < NT; r++) {
-    const double d0 = A[r] * ex + B[r] * nx, d1 = A[r] * ey + B[r] * ny;
-    g[0] = g[0] + d0 * U[r];
-    g[1] = g[1] + d1 * U[r];
-    g[2] = g[2] + d0 * V[r];
-    g[3] = g[3] + d1 * V[r];
+  for (int r0 = 0; r0 < NT; r0 += GB) {
+    double A[GB], B[GB], U[GB], V[GB];
+#pragma unroll
+    for (int r = r0; r < r0 + GB && r < NT; r++) {
+      int mm, n, ia, ib;
+      nz_coef<NGL>(r, i, j, mm, n, ia, ib);
+      A[r - r0] = s_dpsi[ia];
+      B[r - r0] = s_dpsi[ib];
+      U[r - r0] = s_u[mm * NGL + n];
+      V[r - r0] = s_v[mm * NGL + n];
+    }
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int r = r0; r < r0 + GB && r < NT; r++) {
+      const double d0 = A[r - r0] * ex + B[r - r0] * nx, d1 = A[r - r0] * ey + B[r - r0] * ny;
+      g[0] = g[0] + d0 * U[r - r0];
+      g[1] = g[1] + d1 * U[r - r0];
+      g[2] = g[2] + d0 * V[r - r0];
+      g[3] = g[3] + d1 * V[r - r0];
+    }
   }
 }
 
