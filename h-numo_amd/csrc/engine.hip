@@ -94,9 +94,9 @@ struct hnumo_engine {
   bool persistent_ok[2] = {false, false};
   bool regacc[2] = {false, false};           // persistent kernel keeps the averages in registers
   TraceGranule *gtr[2] = {nullptr, nullptr};  // tagged face traces of the persistent sub-cycle
-  unsigned long long *epoch = nullptr;        // tag epoch, bumped before every persistent sub-cycle
+  unsigned long long *epoch = nullptr;        // tag epoch, bumped by every persistent sub-cycle launch
+  unsigned *sub_done = nullptr;               // its finished-workgroup counter
   StageArgs *d_stages[2] = {nullptr, nullptr};  // per-stage arguments: predictor (qp), corrector (qp2)
-  int sub_final = 0;                          // qbuf index holding the sub-cycle result
   // processor-face halo: the reference's own partition contract (face(8) = 0 faces listed per
   // neighbour rank in nbh_send_recv; p4est.c:1686-1712, mod_parallel).  NS shared-face slots in
   // list order; neighbour j owns slots [off, off+n).  Stage traces move between the trace
@@ -172,7 +172,7 @@ struct Launch {
       hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, true>), dim3(n), dim3(StageCfg<NGL, NQ, true>::BS), 0, st, a);
   }
   static void subcycle(hnumo_engine *e, const StageArgs *stages, int ns) {
-    SubArgs sa{stages, ns, e->epoch};
+    SubArgs sa{stages, ns, e->epoch, e->sub_done};
     if (e->summation == HNUMO_SUM_REFERENCE)
       hipLaunchKernelGGL((btp_subcycle_kernel<NGL, NQ, false>), dim3(e->nelem_owned),
                          dim3(StageCfg<NGL, NQ, false>::BS), 0, e->stream, sa);
@@ -634,20 +634,26 @@ static bool use_persistent(const hnumo_engine *e) {
 }
 
 // ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:19-151) on device state qb_state
-static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp, bool timed = false) {
-  const bool pers = use_persistent(e);
+// ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:19-151) from the step-start state e->qb (both
+// sub-cycles of a step start from it, ti_rk_bcl.F90:50,71) into dst: e->qbp (predictor, qp =
+// e->qp) or e->qb (corrector, qp = e->qp2).  The persistent kernel's stage tables read e->qb
+// and write dst themselves; with the averages in registers (REGACC) nothing else runs around it.
+static void launch_subcycle(hnumo_engine *e, double *dst, const double *qp, bool timed = false) {
+  const int tab = (dst == e->qbp && qp == e->qp) ? 0 : ((dst == e->qb && qp == e->qp2) ? 1 : -1);
+  const bool pers = use_persistent(e) && tab >= 0;
   // persistent with register averages: the kernel writes them, zeroed and scaled as below
   const bool racc = pers && e->regacc[e->summation] && !(e->stage_dbg & 32);
-  subcycle_prologue(e, qb_state, pers ? e->epoch : nullptr, !racc);
-  exchange_qb(e, e->qbuf[0]);
-  DISPATCH(e, grad_trace(e, e->qbuf[0], e->gtrace[0], 0, e->nelem, pers ? e->gtr[0] : nullptr));
+  if (!racc) subcycle_prologue(e, e->qb, nullptr, true);
+  if (!pers) exchange_qb(e, e->qbuf[0]);
+  DISPATCH(e, grad_trace(e, pers ? e->qb : e->qbuf[0], e->gtrace[0], 0, e->nelem, pers ? e->gtr[0] : nullptr));
   const int K = e->K, NB = e->p.N_btp;
   int cur;
   if (pers) {
     if (timed && e->kernel_events) (void)hipEventRecord(e->evk0, e->stream);
-    DISPATCH(e, subcycle(e, e->d_stages[qp == e->qp ? 0 : 1], K * NB));
+    DISPATCH(e, subcycle(e, e->d_stages[tab], K * NB));
     if (timed && e->kernel_events) (void)hipEventRecord(e->evk1, e->stream);
-    cur = e->sub_final;
+    if (racc) return;
+    cur = -1;  // (the last stage wrote dst)
   } else if (e->face_halo) {
     // Processor-face halo, two streams (the overlap of mod_rhs_btp.F90:40-46): elements with a
     // processor face ("boundary", B) run on stream2, which then ships their new face traces to
@@ -695,7 +701,7 @@ static void launch_subcycle(hnumo_engine *e, double *qb_state, const double *qp,
   int nblk = 1024;
   hipLaunchKernelGGL(btp_finalize_kernel, dim3(nblk), dim3(256), 0, e->stream, e->qacc, e->facc, e->nacc, e->gfacc,
                      e->tau_wind_ave, e->tau_wind, e->npq, 4 * e->nelem * e->nq, e->npoin, 4 * e->nelem * e->ngl, NB,
-                     1.0 / (double)(K * NB), qb_state, e->qbuf[cur], racc ? 0 : 1);
+                     1.0 / (double)(K * NB), dst, cur >= 0 ? e->qbuf[cur] : dst, 1);
 }
 
 // the full ti_rk_bcl on device state (e->q, e->qb, e->qp)
@@ -703,7 +709,6 @@ static void launch_step(hnumo_engine *e) {
   const size_t n3 = 3 * (size_t)e->npoin * e->L, nf = 6 * e->FN * e->L, nl = (size_t)e->npoin * e->L;
   int blocks = (int)std::min<size_t>((nl + 255) / 256, 4096);
   // prediction (ti_rk_bcl.F90:43-57)
-  launch_copy(e, e->qbp, e->qb, 4 * (size_t)e->npoin);
   launch_bcl_coeffs(e, e->qp, e->qf);
   launch_subcycle(e, e->qbp, e->qp);
   hipLaunchKernelGGL(copy3_kernel, dim3((int)std::min<size_t>((nf + 255) / 256, 2048)), dim3(256), 0, e->stream, e->q2,
@@ -1259,11 +1264,14 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   // persistent sub-cycle: stage tables for the two sub-cycles of a step and the residency check
   if (supported_ngl(ngl) && eng->K <= 8) {
     eng->epoch = dalloc<unsigned long long>(eng, 1);
+    eng->sub_done = dalloc<unsigned>(eng, 1);
     for (int b = 0; b < 2; b++) eng->gtr[b] = dalloc<TraceGranule>(eng, (size_t)E * 32 * ngl);
     const double *qps[2] = {eng->qp, eng->qp2};
     for (int v = 0; v < 2; v++) {
       std::vector<StageArgs> st;
-      eng->sub_final = stage_table(eng, qps[v], st);
+      (void)stage_table(eng, qps[v], st);
+      st.front().qb_in = eng->qb;                        // the step-start state (launch_subcycle)
+      st.back().qb_out = v == 0 ? eng->qbp : eng->qb;    // predictor / corrector result
       eng->d_stages[v] = dalloc<StageArgs>(eng, st.size());
       if (eng->alloc_failed) return fail(eng, HNUMO_ERR_DEVICE, "hipMalloc failed (stage tables)");
       HIPCHK(hipMemcpy(eng->d_stages[v], st.data(), st.size() * sizeof(StageArgs), hipMemcpyHostToDevice));
@@ -1275,6 +1283,11 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
       DISPATCH(eng, occupancy(eng, ncu));
     }
   }
+  // tau_wind_ave = (N_btp times tau_wind summed) / N_btp (mod_rk_mlswe.F90:148) is constant: formed
+  // once here (btp_finalize_kernel also re-forms it after every per-stage sub-cycle)
+  hipLaunchKernelGGL(btp_finalize_kernel, dim3(256), dim3(256), 0, eng->stream, eng->qacc, eng->facc, eng->nacc,
+                     eng->gfacc, eng->tau_wind_ave, eng->tau_wind, (int)npq, 0, 0, 0, par->N_btp, 1.0, nullptr,
+                     nullptr, 0);
   HIPCHK(hipDeviceSynchronize());
   return HNUMO_OK;
 }
@@ -1440,7 +1453,8 @@ int hnumo_ti_barotropic_ssprk(hnumo_engine *eng, double *qb_df, const double *qp
   HIPCHK(hipSetDevice(eng->device));
   int rc = upload_state(eng, nullptr, qb_df, qprime_df);
   if (rc) return rc;
-  launch_subcycle(eng, eng->qb, eng->qp);
+  launch_subcycle(eng, eng->qbp, eng->qp);
+  launch_copy(eng, eng->qb, eng->qbp, 4 * (size_t)eng->npoin);
   HIPCHK(hipGetLastError());
   return download_state(eng, nullptr, qb_df, nullptr);
 }
@@ -1650,7 +1664,6 @@ int hnumo_time_stage_kernel(hnumo_engine *eng, int nsubcycles, double *ms_kernel
   eng->kernel_events = true;
   double total = 0.0;
   for (int s = 0; s < nsubcycles; s++) {
-    launch_copy(eng, eng->qbp, eng->qb, 4 * (size_t)eng->npoin);
     launch_subcycle(eng, eng->qbp, eng->qp, true);
     HIPCHK(hipEventSynchronize(eng->evk1));
     float mk = 0.f;

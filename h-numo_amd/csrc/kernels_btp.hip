@@ -1516,7 +1516,8 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF, NB>::BS), (StageCfg<NGL
 struct SubArgs {
   const StageArgs *stages;         // [NS]
   int NS;
-  const unsigned long long *epoch; // tag base of this launch (bumped before it)
+  unsigned long long *epoch;       // tag base of this launch; the last workgroup to finish bumps it
+  unsigned *done;                  // finished-workgroup counter (back to 0 after every launch)
 };
 
 template <int NGL, int NQ, bool SF>
@@ -1541,6 +1542,15 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
     asm volatile("" : "+v"(tid_s), "+s"(e_s));
     tid_s &= C::BS - 1;  // restore the known range of the thread index
     stage_body<NGL, NQ, SF, true>(tab[stage], s_arena, s_prof, stage == 0, e_s, tid_s, ep, pacc);
+  }
+  // the next launch's tags: every workgroup read the epoch at its start, so the last one to
+  // finish (agent-scope counter) moves it on and resets the counter
+  if (tid == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(sa.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      __hip_atomic_store(sa.epoch, ep + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sa.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
