@@ -57,7 +57,7 @@ FIELDS = [
     ("sum_layer_mass_flux_face", "2,nq,nface"),
 ]
 
-MODES = {"rhs": 1, "btp": 2, "step": 3, "predict": 4, "diag": 5, "setup": 6}
+MODES = {"rhs": 1, "btp": 2, "step": 3, "predict": 4, "diag": 5, "setup": 6, "geom": 7}
 TEST_CASE_ID = {"bump": 1, "lakeAtrest": 2, "double-gyre": 3}
 
 # outputs of mode "setup" (oracle/ref_driver.F90 mode 6: the reference's own start-up routines)
@@ -100,7 +100,7 @@ def write_bundle(path: str, case, mode: str, nsteps: int = 1, metrics: bool = Fa
     with open(path, "wb") as fh:
         fh.write(hi.tobytes())
         fh.write(hd.tobytes())
-        trailer = (METRIC_ARRAYS if metrics else []) + ([("coord", "f8", "3,npoin")] if mode == "diag" else [])
+        trailer = (METRIC_ARRAYS if metrics else []) + ([("coord", "f8", "3,npoin")] if mode in ("diag", "geom") else [])
         if mode == "setup":
             trailer = METRIC_ARRAYS[:5] + [("coord", "f8", "3,npoin")]
         for name, dt, shp in BUNDLE_ARRAYS + trailer:
@@ -149,6 +149,30 @@ def read_outputs(path: str, case, mode: str) -> dict:
     take("ref_dpsiq", (ngl, nq))
     take("ref_psi", (ngl, ngl))
     take("ref_dpsi", (ngl, ngl))
+    assert off == raw.size, (off, raw.size)
+    return out
+
+
+# outputs of mode "geom" (oracle/ref_driver.F90 mode 7: the reference's metrics, metrics_quad,
+# create_normals and create_normals_quad on the bundle's node coordinates and faces)
+GEOM_OUT = [
+    ("ksi_x", "ngl,ngl,nelem"), ("ksi_y", "ngl,ngl,nelem"), ("eta_x", "ngl,ngl,nelem"), ("eta_y", "ngl,ngl,nelem"),
+    ("jac", "ngl,ngl,nelem"), ("ksiq_x", "nq,nq,nelem"), ("ksiq_y", "nq,nq,nelem"), ("etaq_x", "nq,nq,nelem"),
+    ("etaq_y", "nq,nq,nelem"), ("jacq", "nq,nq,nelem"), ("normal_vector", "3,ngl,nface"), ("jac_face", "ngl,nface"),
+    ("normal_vector_q", "3,nq,nface"), ("jac_faceq", "nq,nface"),
+]
+
+
+def read_geom_outputs(path: str, case) -> dict:
+    """Outputs of the reference harness in mode "geom" (GEOM_OUT order)."""
+    d = dims(case)
+    raw = np.fromfile(path, dtype="<f8")
+    off, out = 0, {}
+    for name, shp in GEOM_OUT:
+        s = shape_of(shp, d)
+        n = int(np.prod(s))
+        out[name] = raw[off:off + n].reshape(s, order="F").copy()
+        off += n
     assert off == raw.size, (off, raw.size)
     return out
 

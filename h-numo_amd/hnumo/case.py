@@ -28,6 +28,7 @@ import numpy as np
 
 from .basis import Basis
 from .mesh import BrickMesh
+from .quadmesh import QuadMesh, read_inp, warped_brick
 
 GRAVITY = 9.806                    # set by every IC and by wind_stress_coriolis (mod_initial_mlswe.F90:306)
 PI = math.pi                       # mod_constants pi = pi_trig
@@ -75,6 +76,15 @@ CONFIGS = {
                    xdims=(0.0, 2.0e6), ydims=(0.0, 2.0e6), dt=500.0, dt_btp=25.0,
                    method_visc=3, visc=50.0, botfr=1, cd=1.0e-7, f0=0.93e-4, beta=2.0e-11,
                    ad_mlswe=1.0e-2, max_shear_dz=50.0),
+    # f3 (meshes beyond the brick): general bilinear quadrilaterals with mixed edge orientations
+    # (hnumo/quadmesh.py; "mesh": ("warp", amplitude, rotate corners) or ("inp", path))
+    "qmbump8": dict(test_case="bump", nelx=8, nely=8, nop=4, nlayers=2,
+                    xdims=(0.0, 2000.0), ydims=(0.0, 2000.0), dt=100.0, dt_btp=1.8,
+                    method_visc=0, visc=0.0, botfr=0, cd=0.0, f0=0.0, beta=0.0, mesh=("warp", 0.15, True)),
+    "qmdg8L3": dict(test_case="double-gyre-3", nelx=8, nely=8, nop=4, nlayers=3,
+                    xdims=(0.0, 2.0e6), ydims=(0.0, 2.0e6), dt=500.0, dt_btp=25.0,
+                    method_visc=3, visc=50.0, botfr=1, cd=1.0e-7, f0=0.93e-4, beta=2.0e-11,
+                    mesh=("warp", 0.15, True)),
     # C4: ~1e5 elements, dt scaled for CFL
     "dg316L3": dict(test_case="double-gyre-3", nelx=316, nely=316, nop=4, nlayers=3,
                     xdims=(0.0, 2.0e6), ydims=(0.0, 2.0e6), dt=40.0, dt_btp=2.0,
@@ -152,19 +162,9 @@ def _interp_nodes_to_quad(basis: Basis, nodal_e):
     return out
 
 
-def build_case(cfg: dict, dense: bool = True) -> Case:
-    """Build mesh, tables and ICs.  ``dense`` adds the reference's dense tables (oracle only)."""
-    nop, L = cfg["nop"], cfg["nlayers"]
-    basis = Basis(nop)
-    ngl, nq = basis.ngl, basis.nq
-    mesh = BrickMesh(cfg["nelx"], cfg["nely"], tuple(cfg["xdims"]), tuple(cfg["ydims"]),
-                     ngl, nq, tuple(cfg["x_boundary"]), tuple(cfg["y_boundary"]))
-    mesh.finalize_face_jacobians(basis.wgl, basis.wnq)
-    nelem, npoin, npoin_q, nface = mesh.nelem, mesh.npoin, mesh.npoin_q, mesh.nface
-    P, Q = ngl * ngl, nq * nq
-    A = {}
-
-    # ---------------- metrics (affine brick; metrics_quad.F90:60-126, metrics.F90:113)
+def _brick_metrics(A, basis: Basis, mesh: BrickMesh):
+    """Metrics of the affine brick (metrics_quad.F90:60-126, metrics.F90:113)."""
+    ngl, nq, nelem = basis.ngl, basis.nq, mesh.nelem
     x_ksi, y_eta = 0.5 * mesh.dx, 0.5 * mesh.dy
     xj = x_ksi * y_eta * 1.0 - x_ksi * 0.0 * 0.0 - (0.0 * 0.0 * 1.0 - 0.0 * 0.0 * 0.0) \
         + (0.0 * 0.0 * 0.0 - 0.0 * 0.0 * y_eta)
@@ -189,6 +189,42 @@ def build_case(cfg: dict, dense: bool = True) -> Case:
     A["jac"] = np.asfortranarray(np.broadcast_to(jac_e.T[:, :, None], (ngl, ngl, nelem)))
     # lumped mass: mass(ip) = jac(i,j,e) (one element per DG node), massinv = 1/mass
     A["massinv"] = 1.0 / A["jac"].reshape(-1, order="F")
+
+
+
+def build_case(cfg: dict, dense: bool = True) -> Case:
+    """Build mesh, tables and ICs.  ``dense`` adds the reference's dense tables (oracle only)."""
+    nop, L = cfg["nop"], cfg["nlayers"]
+    basis = Basis(nop)
+    ngl, nq = basis.ngl, basis.nq
+    mspec = cfg.get("mesh")
+    if mspec is None:
+        mesh = BrickMesh(cfg["nelx"], cfg["nely"], tuple(cfg["xdims"]), tuple(cfg["ydims"]),
+                         ngl, nq, tuple(cfg["x_boundary"]), tuple(cfg["y_boundary"]))
+        mesh.finalize_face_jacobians(basis.wgl, basis.wnq)
+    else:
+        # f3: a general conforming quadrilateral grid (hnumo/quadmesh.py)
+        if mspec[0] == "warp":
+            V, Qd, bc = warped_brick(cfg["nelx"], cfg["nely"], cfg["xdims"], cfg["ydims"], mspec[1], mspec[2],
+                                     cfg["x_boundary"][0])
+        elif mspec[0] == "inp":
+            V, Qd, bc = read_inp(mspec[1])
+        else:
+            raise ValueError(mspec)
+        mesh = QuadMesh(V, Qd, bc, ngl, nq)
+    nelem, npoin, npoin_q, nface = mesh.nelem, mesh.npoin, mesh.npoin_q, mesh.nface
+    P, Q = ngl * ngl, nq * nq
+    A = {}
+
+    if isinstance(mesh, QuadMesh):
+        # ---------------- metrics, normals, face Jacobians of a general grid (quadmesh.py)
+        G = mesh.geometry(basis)
+        for k in ("normal_vector", "normal_vector_q", "jac_face", "jac_faceq"):
+            setattr(mesh, k, G.pop(k))
+        A.update(G)
+        A["massinv"] = 1.0 / A["jac"].reshape(-1, order="F")
+    else:
+        _brick_metrics(A, basis, mesh)
 
     # ---------------- mesh arrays
     for k in ("face", "imapl", "imapr", "imapl_q", "imapr_q", "normal_vector", "normal_vector_q", "jac_face",

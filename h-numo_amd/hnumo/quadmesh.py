@@ -1,0 +1,345 @@
+"""General conforming quadrilateral meshes: external grids.
+
+Host-side setup.  h-NUMO reads an external 2-D grid through p4est (``lread_external_grid`` ->
+``p4est_connectivity_read_inp("EXTERNAL_MESH.inp")`` and the reference's own boundary reader
+``p4est_bc_read_inp``, p4est.c:538-900, 1121-1133): Abaqus ``*NODE`` records, quadrilateral
+``*ELEMENT, TYPE=CPS4|C2D4|S4`` records, boundary line elements ``TYPE=T3D2`` grouped into
+``*ELSET`` sets whose name carries ``:BC_<code>``.  Each quadrilateral becomes one element
+whose geometry is the bilinear map of its four corners (p4est's tree geometry with no
+refinement).  p4est itself is not available here, so this module builds the mesh arrays the
+hot path reads directly from such a grid:
+
+* the DG node coordinates (bilinear map of the corners at the LGL points);
+* the metric terms at the nodes and at the quadrature points, restating metrics.F90:53-126 and
+  metrics_quad.F90:47-125 operation for operation (mxm's ordered sums for the nodal
+  derivatives, compute_local_gradient_quad_v3's for the quadrature points, the 3x3 inverse
+  with the 2-D defaults z_zeta = 1);
+* the faces: ``face(5:8)`` (NUMA local face ids 5/6 = xi -/+ 1, 3/4 = eta -/+ 1, left element,
+  right element or ``-bc``), ``imapl/imapr`` (+ ``_q``) with the right side's face points listed
+  in the LEFT side's physical order -- neighbouring quadrilaterals of an unstructured grid
+  may run along a shared edge in opposite directions, the map reverses them so face point n is
+  one physical point for both sides;
+* normals and face Jacobians at the face nodes and face quadrature points from the left
+  element's metric derivatives (create_normals.F90:47-214, create_normals_quad.F90:42-214).
+
+Pinning: ``oracle/_ref/ref_driver`` mode 7 runs the reference's own ``metrics``,
+``metrics_quad``, ``create_normals`` and ``create_normals_quad`` on these node coordinates
+and face lists (tests/test_quadmesh.py, fixture tests/golden/geom_*.npz).  The corner ->
+node map itself (p4est's) is not pinned: p4est is absent.
+"""
+from __future__ import annotations
+
+import re
+
+import numpy as np
+
+# local faces: NUMA id, the two corners it runs between (start, end) in the element's
+# counter-clockwise corner order c0=(-1,-1) c1=(+1,-1) c2=(+1,+1) c3=(-1,+1), and the local
+# (i, j) of its point n of m (create_imaplr / create_normals point order: along eta on xi faces,
+# along xi on eta faces)
+_LFACES = (
+    (5, 0, 3, lambda n, m: (0, n)),
+    (6, 1, 2, lambda n, m: (m - 1, n)),
+    (3, 0, 1, lambda n, m: (n, 0)),
+    (4, 3, 2, lambda n, m: (n, m - 1)),
+)
+
+
+def read_inp(path: str):
+    """Vertices (nv, 2), quadrilaterals (ne, 4; 0-based vertex ids in file order) and the
+    boundary code of every boundary edge {frozenset(v0, v1): code} of an Abaqus .inp grid, as
+    p4est_connectivity_read_inp / p4est_bc_read_inp take it (2-D: CPS4/C2D4/S4 quadrilaterals,
+    T3D2 boundary edges, *ELSET names ``...:BC_<code>``)."""
+    verts, vid, quads, lines, sets = [], {}, [], {}, []
+    mode, cur = None, None
+    with open(path) as fh:
+        for raw in fh:
+            s = raw.strip()
+            if not s or s.startswith("**"):
+                continue
+            if s.startswith("*"):
+                u = s.upper().replace(" ", "")
+                mode = None
+                if u.startswith("*NODE"):
+                    mode = "node"
+                elif u.startswith("*ELEMENT"):
+                    if any(t in u for t in ("TYPE=CPS4", "TYPE=C2D4", "TYPE=S4")) and "TYPE=S4R" not in u:
+                        mode = "quad"
+                    elif "TYPE=T3D2" in u:
+                        mode = "line"
+                elif u.startswith("*ELSET") and ":BC_" in u:
+                    m = re.search(r":BC_(\d+)", u)
+                    cur = (int(m.group(1)), [])
+                    sets.append(cur)
+                    mode = "elset"
+                continue
+            f = [t for t in s.replace(",", " ").split()]
+            if mode == "node":
+                vid[int(f[0])] = len(verts)
+                verts.append((float(f[1]), float(f[2])))
+            elif mode == "quad":
+                quads.append([int(t) for t in f[1:5]])
+            elif mode == "line":
+                lines[int(f[0])] = (int(f[1]), int(f[2]))
+            elif mode == "elset":
+                cur[1].extend(int(t) for t in f)
+    V = np.array(verts, dtype=np.float64)
+    Qd = np.array([[vid[v] for v in q] for q in quads], dtype=np.int64)
+    bc = {}
+    for code, els in sets:
+        for el in els:
+            a, b = lines[el]
+            bc[frozenset((vid[a], vid[b]))] = code
+    return V, Qd, bc
+
+
+def write_inp(path: str, verts, quads, bc):
+    """The inverse of read_inp (used to write test grids)."""
+    with open(path, "w") as fh:
+        fh.write("*HEADING\nh-numo_amd test grid\n*NODE\n")
+        for i, (x, y) in enumerate(verts):
+            fh.write(f"{i + 1}, {x:.17g}, {y:.17g}, 0\n")
+        ne = len(quads)
+        fh.write("*ELEMENT, TYPE=T3D2, ELSET=LINES\n")
+        edges = sorted(bc.items(), key=lambda kv: sorted(kv[0]))
+        for k, (e, _) in enumerate(edges):
+            a, b = sorted(e)
+            fh.write(f"{ne + k + 1}, {a + 1}, {b + 1}\n")
+        fh.write("*ELEMENT, TYPE=CPS4, ELSET=SURFACE\n")
+        for k, q in enumerate(quads):
+            fh.write(f"{k + 1}, " + ", ".join(str(int(v) + 1) for v in q) + "\n")
+        for code in sorted(set(bc.values())):
+            fh.write(f"*ELSET,ELSET=WALL:BC_{code}\n")
+            ids = [str(ne + k + 1) for k, (e, c) in enumerate(edges) if c == code]
+            for i in range(0, len(ids), 8):
+                fh.write(", ".join(ids[i:i + 8]) + "\n")
+
+
+def warped_brick(nelx: int, nely: int, xdims, ydims, amp: float = 0.15, rotate: bool = True, bc: int = 4):
+    """A test grid: the nelx x nely brick with its interior vertices displaced smoothly (every
+    element a general bilinear quadrilateral) and, with ``rotate``, the corner lists of some
+    elements started at another corner, so that neighbours run along shared edges in both the
+    same and opposite directions (as in an unstructured grid)."""
+    xs = np.linspace(xdims[0], xdims[1], nelx + 1)
+    ys = np.linspace(ydims[0], ydims[1], nely + 1)
+    X, Y = np.meshgrid(xs, ys)                       # [iy, ix]
+    dx, dy = (xdims[1] - xdims[0]) / nelx, (ydims[1] - ydims[0]) / nely
+    sx = np.sin(np.pi * (X - xdims[0]) / (xdims[1] - xdims[0])) * np.sin(2 * np.pi * (Y - ydims[0]) / (ydims[1] - ydims[0]))
+    sy = np.sin(2 * np.pi * (X - xdims[0]) / (xdims[1] - xdims[0])) * np.sin(np.pi * (Y - ydims[0]) / (ydims[1] - ydims[0]))
+    X = X + amp * dx * sx
+    Y = Y + amp * dy * sy
+    verts = np.stack([X.ravel(), Y.ravel()], axis=1)
+    vid = lambda ix, iy: iy * (nelx + 1) + ix  # noqa: E731
+    quads = []
+    for iy in range(nely):
+        for ix in range(nelx):
+            q = [vid(ix, iy), vid(ix + 1, iy), vid(ix + 1, iy + 1), vid(ix, iy + 1)]
+            r = ((3 * ix + 5 * iy) % 4) if rotate else 0
+            quads.append(q[r:] + q[:r])
+    bce = {}
+    for ix in range(nelx):
+        bce[frozenset((vid(ix, 0), vid(ix + 1, 0)))] = bc
+        bce[frozenset((vid(ix, nely), vid(ix + 1, nely)))] = bc
+    for iy in range(nely):
+        bce[frozenset((vid(0, iy), vid(0, iy + 1)))] = bc
+        bce[frozenset((vid(nelx, iy), vid(nelx, iy + 1)))] = bc
+    return verts, np.array(quads, dtype=np.int64), bce
+
+
+class QuadMesh:
+    """The hot path's mesh arrays for a conforming quadrilateral grid (attributes as BrickMesh:
+    face, imapl, imapr, imapl_q, imapr_q, normal_vector(_q), jac_face(q), node_coords)."""
+    nelx = nely = None   # (no brick block structure: the brick partitioners do not apply)
+
+    def __init__(self, verts, quads, bc, ngl: int, nq: int, default_bc: int = 4):
+        self.verts = np.asarray(verts, dtype=np.float64)
+        self.quads = np.asarray(quads, dtype=np.int64)
+        self.ngl, self.nq = ngl, nq
+        self.nelem = len(self.quads)
+        self.npts, self.nqq = ngl * ngl, nq * nq
+        self.npoin, self.npoin_q = self.nelem * self.npts, self.nelem * self.nqq
+        self._build_faces(bc, default_bc)
+
+    # ------------------------------------------------------------------ faces
+    def _build_faces(self, bc, default_bc):
+        seen = {}      # edge -> face index
+        rec = []       # [lid_l, lid_r, el, er(+1 or -bc), start vertex, reversed]
+        side = []      # per face: (left lf slot, right lf slot)
+        Q = self.quads
+        for e in range(self.nelem):
+            # (local faces in the order xi-, xi+, eta-, eta+; a face's left element is the
+            # first element that lists it)
+            if not self._ccw(e):
+                raise ValueError(f"element {e + 1}: corners are not counter-clockwise")
+            for k, (lid, a, b, _) in enumerate(_LFACES):
+                va, vb = int(Q[e, a]), int(Q[e, b])
+                key = frozenset((va, vb))
+                if key not in seen:
+                    seen[key] = len(rec)
+                    rec.append([lid, 0, e + 1, -int(bc.get(key, default_bc)), va, False])
+                    side.append([k, -1])
+                else:
+                    f = seen[key]
+                    if rec[f][3] > 0 or side[f][1] >= 0:
+                        raise ValueError("an edge is shared by more than two elements")
+                    rec[f][1] = lid
+                    rec[f][3] = e + 1
+                    rec[f][5] = va != rec[f][4]       # runs the other way along the edge
+                    side[f][1] = k
+        nface = len(rec)
+        self.nface = nface
+        face = np.zeros((8, nface), dtype=np.int32, order="F")
+        for f, (ll, lr, el, er, _, _) in enumerate(rec):
+            face[4, f], face[5, f], face[6, f], face[7, f] = ll, lr, el, er
+        self.face = face
+        self._rev = np.array([r[5] for r in rec], dtype=bool)
+        self._side = np.array(side, dtype=np.int64)
+
+        def imap(m, right):
+            out = np.zeros((3, m, nface), dtype=np.int32, order="F")
+            for f in range(nface):
+                k = self._side[f, 1 if right else 0]
+                if k < 0:
+                    continue
+                for n in range(m):
+                    nn = (m - 1 - n) if (right and self._rev[f]) else n
+                    i, j = _LFACES[k][3](nn, m)
+                    out[:, n, f] = (i + 1, j + 1, 1)
+            return out
+
+        self.imapl, self.imapr = imap(self.ngl, False), imap(self.ngl, True)
+        self.imapl_q, self.imapr_q = imap(self.nq, False), imap(self.nq, True)
+
+    def _ccw(self, e):
+        p = self.verts[self.quads[e]]
+        a = 0.0
+        for k in range(4):
+            x0, y0 = p[k]
+            x1, y1 = p[(k + 1) % 4]
+            a += x0 * y1 - x1 * y0
+        return a > 0.0
+
+    # ------------------------------------------------------------ coordinates
+    def node_coords(self, xgl):
+        """coord(1:3, npoin) of the DG nodes: the bilinear map of the corners at (xgl(i), xgl(j))."""
+        ngl = self.ngl
+        p = self.verts[self.quads]                   # (ne, 4, 2)
+        xi = np.asarray(xgl)[None, :]                # i
+        et = np.asarray(xgl)[:, None]                # j
+        w = [0.25 * (1 - xi) * (1 - et), 0.25 * (1 + xi) * (1 - et), 0.25 * (1 + xi) * (1 + et),
+             0.25 * (1 - xi) * (1 + et)]
+        coord = np.zeros((3, self.npoin), order="F")
+        for d in range(2):
+            v = sum(w[c][None, :, :] * p[:, c, d][:, None, None] for c in range(4))   # (ne, j, i)
+            coord[d] = v.reshape(-1)
+        return coord
+
+    # ---------------------------------------------------------------- metrics
+    def geometry(self, basis):
+        """Metric terms at the nodes and the quadrature points, normals and face Jacobians
+        (metrics.F90, metrics_quad.F90, create_normals.F90, create_normals_quad.F90)."""
+        ngl, nq, ne = self.ngl, self.nq, self.nelem
+        coord = self.node_coords(basis.xgl)
+        Xn = coord[0].reshape(ne, ngl, ngl)          # [e, j, i]
+        Yn = coord[1].reshape(ne, ngl, ngl)
+        dpsi, psiq, dpsiq = basis.dpsi, basis.psiq, basis.dpsiq
+
+        def nodal_d(X):
+            # compute_local_gradient_v3 via mxm (mxm.F90: c(i,j) = a(i,1)*b(1,j) + a(i,2)*b(2,j) + ...):
+            # x_ksi(i,j) = sum_k dpsix(k,i)*x(k,j);  x_eta(i,j) = sum_k x(i,k)*dpsiy(k,j)
+            xk = np.zeros_like(X)
+            xe = np.zeros_like(X)
+            for i in range(ngl):
+                acc = dpsi[0, i] * X[:, :, 0]
+                for k in range(1, ngl):
+                    acc = acc + dpsi[k, i] * X[:, :, k]
+                xk[:, :, i] = acc
+            for j in range(ngl):
+                acc = X[:, 0, :] * dpsi[0, j]
+                for k in range(1, ngl):
+                    acc = acc + X[:, k, :] * dpsi[k, j]
+                xe[:, j, :] = acc
+            return xk, xe
+
+        def quad_d(X):
+            # compute_local_gradient_quad_v3 (mod_gradient.F90:175-228): m outer, n inner, from 0
+            xk = np.zeros((ne, nq, nq))
+            xe = np.zeros((ne, nq, nq))
+            for jq in range(nq):
+                for iq in range(nq):
+                    a = np.zeros(ne)
+                    b = np.zeros(ne)
+                    for m in range(ngl):
+                        for n in range(ngl):
+                            a = a + dpsiq[n, iq] * psiq[m, jq] * X[:, m, n]
+                            b = b + psiq[n, iq] * dpsiq[m, jq] * X[:, m, n]
+                    xk[:, jq, iq] = a
+                    xe[:, jq, iq] = b
+            return xk, xe
+
+        def inverse(xk, xe, yk, ye, w):
+            # metrics.F90:96-114 with the 2-D defaults (z_zeta = 1; x_zeta, y_zeta, z_ksi, z_eta = 0)
+            z1, z0 = 1.0, 0.0
+            xj = (xk * ye * z1 - xk * z0 * z0) - (yk * xe * z1 - yk * z0 * z0) + (z0 * xe * z0 - z0 * z0 * ye)
+            kx = (ye * z1 - z0 * z0) / xj
+            ky = -(xe * z1 - z0 * z0) / xj
+            ex = -(yk * z1 - z0 * z0) / xj
+            ey = (xk * z1 - z0 * z0) / xj
+            jac = w * np.abs(xj)
+            return kx, ky, ex, ey, jac, xj
+
+        xk, xe = nodal_d(Xn)
+        yk, ye = nodal_d(Yn)
+        wn = (basis.wgl[None, :] * basis.wgl[:, None]) * 1.0        # [j, i]: wglx(i)*wgly(j)*wglz
+        kx, ky, ex, ey, jac, _ = inverse(xk, xe, yk, ye, wn[None])
+        xkq, xeq = quad_d(Xn)
+        ykq, yeq = quad_d(Yn)
+        wq = (basis.wnq[None, :] * basis.wnq[:, None]) * 1.0
+        kxq, kyq, exq, eyq, jacq, _ = inverse(xkq, xeq, ykq, yeq, wq[None])
+
+        def fo(a):  # [e, j, i] -> (i, j, e) Fortran order
+            return np.asfortranarray(np.transpose(a, (2, 1, 0)))
+
+        G = dict(ksi_x=fo(kx), ksi_y=fo(ky), eta_x=fo(ex), eta_y=fo(ey), jac=fo(jac),
+                 ksiq_x=fo(kxq), ksiq_y=fo(kyq), etaq_x=fo(exq), etaq_y=fo(eyq), jacq=fo(jacq))
+        nv, jf = self._normals(xk, xe, yk, ye, basis.wgl, ngl)
+        nvq, jfq = self._normals(xkq, xeq, ykq, yeq, basis.wnq, nq)
+        G.update(normal_vector=nv, normal_vector_q=nvq, jac_face=jf, jac_faceq=jfq)
+        return G
+
+    def _normals(self, xk, xe, yk, ye, w, m):
+        """create_normals(_quad): the left element's metric derivatives at its face points."""
+        nface = self.nface
+        nv = np.zeros((3, m, nface), order="F")
+        jf = np.zeros((m, nface), order="F")
+        z1, z0 = 1.0, 0.0
+        for f in range(nface):
+            e = self.face[6, f] - 1
+            k = self._side[f, 0]
+            lid = _LFACES[k][0]
+            for n in range(m):
+                i, j = _LFACES[k][3](n, m)
+                a_k, a_e, b_k, b_e = xk[e, j, i], xe[e, j, i], yk[e, j, i], ye[e, j, i]
+                ww = w[n] * 1.0
+                if lid == 5:
+                    nx = -(b_e * z1) + z0 * z0
+                    ny = a_e * z1 - z0 * z0
+                    nz = -(a_e * z0) + b_e * z0
+                elif lid == 6:
+                    nx = b_e * z1 - z0 * z0
+                    ny = -(a_e * z1) + z0 * z0
+                    nz = a_e * z0 - b_e * z0
+                elif lid == 3:
+                    nx = b_k * z1 - z0 * z0
+                    ny = -(a_k * z1) + z0 * z0
+                    nz = a_k * z0 - b_k * z0
+                else:
+                    nx = -(b_k * z1) + z0 * z0
+                    ny = a_k * z1 - z0 * z0
+                    nz = -(a_k * z0) + b_k * z0
+                nlen = np.sqrt(nx * nx + ny * ny + nz * nz)
+                jf[n, f] = ww * nlen
+                nv[0, n, f] = nx / nlen
+                nv[1, n, f] = ny / nlen
+                nv[2, n, f] = nz / nlen
+        return nv, jf

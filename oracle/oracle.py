@@ -133,7 +133,12 @@ def run_reference(case, mode: str, nsteps: int = 1, workdir: str | None = None, 
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"{os.path.basename(driver)} failed ({r.returncode}): {r.stdout[-2000:]} {r.stderr[-2000:]}")
-    out = _bundle.read_setup_outputs(fout, case) if mode == "setup" else _bundle.read_outputs(fout, case, mode)
+    if mode == "setup":
+        out = _bundle.read_setup_outputs(fout, case)
+    elif mode == "geom":
+        out = _bundle.read_geom_outputs(fout, case)
+    else:
+        out = _bundle.read_outputs(fout, case, mode)
     out["stdout"] = r.stdout
     if workdir is None:
         for f in (fin, fout):

@@ -70,6 +70,7 @@ program ref_driver
     use mod_initial_mlswe, only: compute_reference_edge_variables, bot_topo_derivatives, &
         wind_stress_coriolis, ssprk_coefficients
     use mod_Tensorproduct, only: compute_gradient_quad
+    use mod_basis, only: FACE_LEN
 
     implicit none
 
@@ -91,6 +92,9 @@ program ref_driver
     ! mode 6 (the reference's own set-up routines)
     real(8) :: sp(6)
     real(8), allocatable :: oop_face(:,:,:), pb_edge(:,:), oop_df_face(:,:,:), tw_df(:,:), z_if(:,:), zbot_q(:)
+    ! mode 7 (the reference's own metric terms and normals)
+    real(8), allocatable :: g_n(:,:,:,:,:), g_q(:,:,:,:,:), g_nv(:,:,:,:), g_jf(:,:,:), g_nvq(:,:,:,:), g_jfq(:,:,:)
+    integer, allocatable :: faceL(:,:)
 
     call mpi_init(ierr)
     call mod_constants_create()                 ! pi, earth_radius (amain.F90:171)
@@ -220,6 +224,7 @@ program ref_driver
         end select
     end if
 #endif
+    if (mode == 7) read(u) coord          ! mode 7 trailer: the DG node coordinates
     if (mode == 5) then
         ! mode 5 trailer: the node coordinates (mod_grid coord, read by courant_mlswe), and the
         ! single-rank gather plumbing of diagnostics / print_diagnostics_mlswe
@@ -354,6 +359,29 @@ program ref_driver
         write(u) coeff_pbpert_L, coeff_pbpert_R, coeff_pbub_LR, coeff_mass_pbub_L, coeff_mass_pbub_R
         write(u) coeff_mass_pbpert_LR, alpha_mlswe, zbot_df, zbot_face, grad_zbot_quad, tau_wind
         write(u) coriolis_quad, fdt2_bcl, a_bcl, b_bcl, ssprk_a, ssprk_beta, real(N_btp, 8), dt_btp, gravity
+        close(u)
+        call mpi_finalize(ierr)
+        stop
+    case (7)
+        ! The reference's geometry of the harness mesh (what mod_metrics_create / mod_face_create
+        ! compute at start-up from p4est's node coordinates): metrics (metrics.F90), metrics_quad
+        ! (metrics_quad.F90), create_normals (create_normals.F90), create_normals_quad
+        ! (create_normals_quad.F90), on the bundle's coordinates (intma = intma_dg) and faces.
+        ! Pins hnumo/quadmesh.py (row f3, general quadrilateral grids).
+        allocate(g_n(ngl, ngl, 1, nelem, 11), g_q(nq, nq, 1, nelem, 11))
+        allocate(g_nv(3, ngl, ngl, nface), g_jf(ngl, ngl, nface), g_nvq(3, nq, nq, nface), g_jfq(nq, nq, nface))
+        allocate(faceL(FACE_LEN, nface)); faceL = 0; faceL(1:8, :) = face(1:8, 1:nface)
+        call metrics(g_n(:,:,:,:,1), g_n(:,:,:,:,2), g_n(:,:,:,:,3), g_n(:,:,:,:,4), g_n(:,:,:,:,5), &
+            g_n(:,:,:,:,6), g_n(:,:,:,:,7), g_n(:,:,:,:,8), g_n(:,:,:,:,9), g_n(:,:,:,:,10), g_n(:,:,:,:,11))
+        call metrics_quad(g_q(:,:,:,:,1), g_q(:,:,:,:,2), g_q(:,:,:,:,3), g_q(:,:,:,:,4), g_q(:,:,:,:,5), &
+            g_q(:,:,:,:,6), g_q(:,:,:,:,7), g_q(:,:,:,:,8), g_q(:,:,:,:,9), g_q(:,:,:,:,10), g_q(:,:,:,:,11))
+        call create_normals(g_nv, g_jf, faceL, nface)
+        call create_normals_quad(g_nvq, g_jfq, faceL, nface)
+        open(newunit=u, file=trim(fout), access='stream', form='unformatted', status='replace')
+        ! ksi_x, ksi_y, eta_x, eta_y, jac at the nodes and at the quadrature points
+        write(u) g_n(:,:,1,:,1), g_n(:,:,1,:,2), g_n(:,:,1,:,4), g_n(:,:,1,:,5), g_n(:,:,1,:,10)
+        write(u) g_q(:,:,1,:,1), g_q(:,:,1,:,2), g_q(:,:,1,:,4), g_q(:,:,1,:,5), g_q(:,:,1,:,10)
+        write(u) g_nv(:,:,1,:), g_jf(:,1,:), g_nvq(:,:,1,:), g_jfq(:,1,:)
         close(u)
         call mpi_finalize(ierr)
         stop

@@ -44,6 +44,9 @@ GOLDEN = [
     ("lake10L3_step1", "lake10", "step", 1, 1, dict(nlayers=3)),
     ("bump10q_ns_step1", "bump10q", "step", 1, 1, dict(y_boundary=(2, 2), botfr=2, cd=1e-3)),
     ("dg8L3q_mixed_step1", "dg8L3q", "step", 1, 1, dict(x_boundary=(2, 4))),
+    # f3: general bilinear quadrilaterals, neighbours along shared edges in both directions
+    ("qmbump8_step2", "qmbump8", "step", 2, 1),
+    ("qmdg8L3_step1", "qmdg8L3", "step", 1, 1),
 ]
 FIELDS_KEPT = ["ope_ave", "H_ave", "Qu_ave", "btp_mass_flux_ave", "uvb_face_ave", "H_face_ave",
                "graduvb_ave", "Q_uu_dp", "H_bcl_edge", "btp_graduv_dpp_face"]
@@ -94,6 +97,7 @@ GOLDEN_SETUP = [
     ("setup_lake10L3", "lake10", dict(nlayers=3), 1),
     ("setup_dg25", "dg25", {}, 5),
     ("setup_dg8N7", "dg25", dict(nelx=8, nely=8, nop=7, dt=180.0, dt_btp=9.0), 2),
+    ("setup_qmbump8", "qmbump8", {}, 1),
 ]
 
 
@@ -107,6 +111,28 @@ def make_setup(only=None):
                 "bundle_sha256": np.array(bundle_hash(case, "setup", 1))}
         for k, _ in B.SETUP_OUT:
             keep["ref_" + k] = np.asarray(out[k]).reshape(-1, order="F")[::stride]
+        path = os.path.join(HERE, name + ".npz")
+        np.savez_compressed(path, **keep)
+        print(name, os.path.getsize(path))
+
+
+# f3: the reference's own geometry routines (ref_driver mode 7: metrics, metrics_quad,
+# create_normals, create_normals_quad) on the node coordinates and faces hnumo/quadmesh.py builds
+GOLDEN_GEOM = [
+    ("geom_qmbump8", "qmbump8", {}),
+]
+
+
+def make_geom(only=None):
+    for name, cfg, ov in GOLDEN_GEOM:
+        if only and name not in only:
+            continue
+        case = build_case(make_config(cfg, **ov))
+        out = O.run_reference(case, "geom", 1)
+        keep = {"config": np.array(cfg), "overrides": np.array(json.dumps(ov)),
+                "bundle_sha256": np.array(bundle_hash(case, "geom", 1))}
+        for k, _ in B.GEOM_OUT:
+            keep["ref_" + k] = np.asarray(out[k])
         path = os.path.join(HERE, name + ".npz")
         np.savez_compressed(path, **keep)
         print(name, os.path.getsize(path))
@@ -152,5 +178,7 @@ if __name__ == "__main__":
         make_mpi(args[1:] or None)
     elif args and args[0] == "setup":
         make_setup(args[1:] or None)
+    elif args and args[0] == "geom":
+        make_geom(args[1:] or None)
     else:
         main(args or None)

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = os.path.join(HERE, "golden")
 GOLDEN = ["bump10_rhs", "bump10_btp", "bump10_step2", "lake10_step1", "dg25_step1", "dg25L3_step1",
           "bump10q_step1", "dg8L3q_step1", "dg8N7L3_step1", "bump10_b2ns_step1", "bump10_mixed_step1",
-          "lake10L3_step1", "bump10q_ns_step1", "dg8L3q_mixed_step1"]
+          "lake10L3_step1", "bump10q_ns_step1", "dg8L3q_mixed_step1", "qmbump8_step2", "qmdg8L3_step1"]
 
 
 def load(name):

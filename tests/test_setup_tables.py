@@ -23,7 +23,7 @@ import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = os.path.join(HERE, "golden")
-SETUP = ["setup_bump10", "setup_lake10L3", "setup_dg25", "setup_dg8N7"]
+SETUP = ["setup_bump10", "setup_lake10L3", "setup_dg25", "setup_dg8N7", "setup_qmbump8"]
 
 
 def _mine(case, k, shape):
