@@ -127,6 +127,7 @@ struct hnumo_engine {
   // bottom-layer qprime at the quad points, interpolated once per sub-cycle (StageArgs::qpq;
   // botfr != 0; HNUMO_QPQ=0: every stage interpolates, for A/B timing)
   double *qpq = nullptr;      // [E][3][Q]
+  double *qsv = nullptr;      // [E][2][P][4] Shu-Osher states of the slim persistent sub-cycle (StageArgs::qsv)
 };
 
 template <typename T>
@@ -189,6 +190,9 @@ struct Launch {
                                                        StageCfg<NGL, NQ, true>::BS, 0);
     (void)hipGetLastError();
     e->persistent_ok[0] = (long)nb0 * ncu >= e->nelem_owned;
+    // the slim arena keeps the bottom-layer qprime only for the first stage: the later ones need
+    // the per-sub-cycle quad-point scratch
+    if (StageCfg<NGL, NQ, false>::SLIM && e->m.botfr && !e->qpq) e->persistent_ok[0] = false;
     e->persistent_ok[1] = (long)nb1 * ncu >= e->nelem_owned;
     e->regacc[0] = StageCfg<NGL, NQ, false>::REGACC;
     e->regacc[1] = StageCfg<NGL, NQ, true>::REGACC;
@@ -618,6 +622,7 @@ static int stage_table(hnumo_engine *e, const double *qp, std::vector<StageArgs>
       a.lapq = e->lapq_on ? e->lapq : nullptr;
       a.qpq = e->qpq;
       a.qpq_mode = stage == 0 ? 1 : 2;
+      a.qsv = e->qsv;
       a.n_inv = 1.0 / (double)(K * NB);
       out_args.push_back(a);
       gt = 1 - gt;
@@ -1050,7 +1055,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   std::vector<double> qsE((size_t)E * QE_N * Qe), nsE((size_t)E * NE_N * P), efs((size_t)E * 4 * FBLK);
   {
     const int qmap[QE_N] = {QS_W, QS_EX, QS_EY, QS_NX, QS_NY, QS_COR, QS_TW1, QS_TW2, QS_GZ1, QS_GZ2, QS_OOP};
-    const int nmap[NE_N] = {NS_EX, NS_EY, NS_NX, NS_NY, NS_W, NS_MINV, NS_PB, NS_OOP};
+    const int nmap[NE_N] = {NS_EX, NS_EY, NS_NX, NS_NY, NS_W, NS_OOP, NS_MINV, NS_PB};
     const int fmap_[EF_PBLQ] = {FS_NX, FS_NY, FS_W, FS_CL, FS_CR, FS_CLR, FS_CML, FS_CMR, FS_CMLR, FS_OOPE};
     const int fnmap[EFN_N] = {FN_NX, FN_NY, FN_W, FN_PBL, FN_PBR};
     for (int e = 0; e < E; e++) {
@@ -1264,6 +1269,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   // persistent sub-cycle: stage tables for the two sub-cycles of a step and the residency check
   if (supported_ngl(ngl) && eng->K <= 8) {
     eng->epoch = dalloc<unsigned long long>(eng, 1);
+    eng->qsv = dalloc<double>(eng, (size_t)E * 8 * ngl * ngl);
     eng->sub_done = dalloc<unsigned>(eng, 1);
     for (int b = 0; b < 2; b++) eng->gtr[b] = dalloc<TraceGranule>(eng, (size_t)E * 32 * ngl);
     const double *qps[2] = {eng->qp, eng->qp2};

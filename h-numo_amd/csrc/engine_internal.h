@@ -20,7 +20,7 @@
 //   erec   int  [E][ERS]              faces, side, bc, nbr elem, nbr local face, keeps-averages flag, face->node map,
 //                                     node->(lf*NGL+n) of the <=2 faces through each node
 //   qstatE      [E][QE_N][Q]          W, e_x, e_y, n_x, n_y, coriolis, tau_wind(2), grad_zbot(2), 1/pb
-//   nstatE      [E][NE_N][P]          e_x, e_y, n_x, n_y, w, massinv, pbprime, 1/pbprime
+//   nstatE      [E][NE_N][P]          e_x, e_y, n_x, n_y, w, 1/pbprime, massinv, pbprime
 //   efstat      [E][4][FBLK]          face statics at face quad points (EF_*) and face nodes (EFN_*)
 //   ecoef       [E][4Q + 5P]          per-sub-cycle Q_uu/uv/vv_dp, H_bcl | pbprime_visc, btp_dpp_graduv
 //   efcoef      [E][4][4NQ + 10NGL]   per-sub-cycle face Q_*_edge, H_bcl_edge | btp_graduv_dpp_face
@@ -67,8 +67,11 @@ enum FNStat { FN_NX = 0, FN_NY, FN_W, FN_PBL, FN_PBR, FN_N };
 // element-major quad statics order (qstatE): the first QE_KEEP rows live for the whole stage
 enum QStatE { QE_W = 0, QE_EX, QE_EY, QE_NX, QE_NY, QE_COR, QE_TW1, QE_TW2, QE_GZ1, QE_GZ2, QE_OOP, QE_N };
 constexpr int QE_KEEP = 5;
-// element-major nodal statics order (nstatE)
-enum NStatE { NE_EX = 0, NE_EY, NE_NX, NE_NY, NE_W, NE_MINV, NE_PB, NE_OOP, NE_N };
+// element-major nodal statics order (nstatE); the first NE_LDS rows are the ones the stage
+// kernel's slim LDS arena (StageCfg::SLIM) stages -- its E1 reads massinv and pbprime into
+// registers from global memory
+enum NStatE { NE_EX = 0, NE_EY, NE_NX, NE_NY, NE_W, NE_OOP, NE_MINV, NE_PB, NE_N };
+constexpr int NE_LDS = 6;
 // element-side face statics block: FS fields at NQ face quad points, then FN fields at NGL nodes
 // (EF_PBLQ/EF_PBRQ: pbprime_df_face interpolated to the face quad points, sum_n psiq(n,iq) *
 //  pbprime_df_face(s,n,f) in the reference's order -- static, so computed once on the host)

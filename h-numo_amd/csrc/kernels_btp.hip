@@ -49,6 +49,10 @@
 #ifndef HNUMO_OTF_MIN_NGL
 #define HNUMO_OTF_MIN_NGL 8
 #endif
+// The slim OTF arena (StageCfg::SLIM); 0 keeps the round-1 layout for A/B measurement.
+#ifndef HNUMO_SLIM
+#define HNUMO_SLIM 1
+#endif
 #ifndef HNUMO_OTF_UNROLL
 #define HNUMO_OTF_UNROLL 5
 #endif
@@ -118,6 +122,9 @@ struct StageArgs {
   // interpolates and stores them (a sub-cycle's first stage), 2: loads them (the later stages)
   double *qpq;
   int qpq_mode;
+  // persistent sub-cycle, slim arena (StageCfg::SLIM): the element's Shu-Osher states qb0, qb2
+  // ([E][2][P][4], components 1..3) -- kept by the E1 lane of each node
+  double *qsv;
   double n_inv;                              // 1/(N_btp*kstages): the averages' normalisation
 };
 
@@ -159,25 +166,41 @@ struct StageCfg {
   static constexpr int ECO = 4 * Q + 5 * P;                 // ecoef record per element
   static constexpr int NB = 2 * NGL * NQ + NGL * NGL;       // psiq, dpsiq, dpsi (+ a zero slot)
   static_assert(Q <= BS, "one quad-point task per thread");
+  static constexpr bool OTF = !SF && NGL >= HNUMO_OTF_MIN_NGL;
+  // SLIM (OTF): an arena small enough for 3 workgroups per CU, so the persistent sub-cycle holds
+  // all 625 elements of dg25 at N=7 at once.  The last wave (EW), idle beside the on-the-fly
+  // volume sums of waves 0..2, runs the LDG volume fluxes, LDG face fluxes and the Laplacian
+  // there and then E1; what only E1 and qq read -- the Shu-Osher states qb0/qb2, massinv,
+  // pbprime, the nodal coefficients, the Laplacian -- lives in that wave's registers (loaded
+  // from global memory while waves 0..2 sum) instead of LDS; the new state overwrites the
+  // stage input in place; the bottom-layer qprime (A2 only) overlays the nodal gradients.
+  static constexpr bool SLIM = OTF && HNUMO_SLIM;
+  static constexpr int EW = BS / 64 - 1;
+  static_assert(!SLIM || (P <= 64 && 3 * P <= EW * 64), "SLIM: one node per lane of the last wave");
   // LDS arena (doubles).  Persistent (A..E); the wall normals of the face nodes are copied
   // out of the face statics (which live in the B region) for E1:
   static constexpr int O_BASIS = 0, O_EREC = O_BASIS + NB + 1, O_QB = O_EREC + ERSD, O_Q0 = O_QB + 4 * P,
-                       O_Q2 = O_Q0 + 4 * P, O_QK = O_Q2 + 4 * P, O_NS = O_QK + QE_KEEP * Q, O_NC = O_NS + NE_N * P,
-                       O_UV = O_NC + 5 * P, O_WN = O_UV + 2 * P;
+                       O_Q2 = O_Q0 + (SLIM ? 0 : 4 * P), O_QK = O_Q2 + (SLIM ? 0 : 4 * P), O_NS = O_QK + QE_KEEP * Q,
+                       O_NC = O_NS + (SLIM ? NE_LDS : NE_N) * P, O_UV = O_NC + (SLIM ? 0 : 5 * P), O_WN = O_UV + 2 * P;
   // working arrays: quad-point values (exact: the 7 integrand factors; SF: the 8 weighted
   // integrands F1,F2,G0..G2,H0..H2), B outputs, then a region written only after B that the
   // SF variant also uses for the interpolation partials Y [NYV][NGL][NQ] (A2 -> B)
   static constexpr int NQV = SF ? 8 : 7, NYV = 7;
+  // (SLIM: no Laplacian / new-state buffers; the face-quad traces of FPRE, A2 -> B, share the W
+  // region with qq and rhs, D -> E)
   static constexpr int O_QV = O_WN + 8 * NGL, O_GR = O_QV + NQV * Q, O_FQ = O_GR + 4 * P, O_FL = O_FQ + 16 * NQ,
                        O_W = O_FL + 8 * NGL, O_QQ = O_W, O_RHS = O_QQ + 4 * P, O_LAP = O_RHS + 3 * P,
-                       O_QN = O_LAP + 2 * P, O_Y = O_W, W_END = O_QN + 4 * P, QN_END_W = W_END - O_W,
+                       O_QN = O_LAP + (SLIM ? 0 : 2 * P), O_Y = O_W, W_END0 = O_QN + (SLIM ? 0 : 4 * P),
+                       QN_END_W = W_END0 - O_W,
+                       W_END = (SLIM && O_W + 32 * NQ > W_END0) ? O_W + 32 * NQ : W_END0,
                        O_BIN = (SF && O_Y + NYV * NGL * NQ > W_END) ? O_Y + NYV * NGL * NQ : W_END;
   // B inputs: the bottom-layer qprime, face statics, neighbour traces, face coefficients.
   // RES: resident for the whole launch (the persistent sub-cycle loads them once), the work
   // region (term buffers / contraction partials) follows; otherwise reloaded every stage and
-  // overlaid by term buffer 1 once B and the LDG fluxes (D0) are done
+  // overlaid by term buffer 1 once B and the LDG fluxes (D0) are done.  (SLIM: the qprime of
+  // A2 in the nodal-gradient slot, written only from B on)
   static constexpr bool RES = HNUMO_RES;
-  static constexpr int B_QP = 0, B_EF = B_QP + 3 * P, B_TR = B_EF + 4 * FBLK, B_EC = B_TR + 32 * NGL,
+  static constexpr int B_QP = 0, B_EF = B_QP + (SLIM ? 0 : 3 * P), B_TR = B_EF + 4 * FBLK, B_EC = B_TR + 32 * NGL,
                        B_SIZE = B_EC + 4 * EFC, O_B = RES ? O_BIN + B_SIZE : O_BIN;
   // exact: term chunks of RC quad rows, two buffers of [3P][QCP] (odd pitch against bank
   // conflicts), as many rows as the LDS budget allows
@@ -190,7 +213,6 @@ struct StageCfg {
   static constexpr int RC0 = rc_fit(TAV);
   static constexpr int RCM = RC0 < 1 ? 1 : (RC0 > NQ ? NQ : RC0);
   static constexpr int NCH = (NQ + RCM - 1) / RCM, RC = (NQ + NCH - 1) / NCH, QC = RC * NQ;
-  static constexpr bool OTF = !SF && NGL >= HNUMO_OTF_MIN_NGL;
   static constexpr int QCP = QC | 1, TSZ = OTF ? 0 : 3 * P * QCP;
   static constexpr int TB0 = RES ? 0 : (TSZ > B_SIZE ? TSZ : B_SIZE), TB1 = RES ? TSZ : 0;
   // SF: first-pass contraction partials U, W [3][2][NGL][NQ] (C1 runs the LDG face fluxes)
@@ -221,7 +243,7 @@ struct StageCfg {
   // FPRE (exact, not LATE): A2 also interpolates each face's own-side traces and, on physical
   // boundaries, the ghost-side traces to the face quad points, into s_fi [4][NQ][8] (in the
   // W region, dead from A to D0), so B's face fluxes interpolate only the neighbour traces
-  static constexpr bool FPRE = !SF && !LATE && 4 * NQ * 8 <= QN_END_W;
+  static constexpr bool FPRE = !SF && !LATE && (SLIM || 4 * NQ * 8 <= QN_END_W);
   // LATE chunk phase KP+1: face fluxes from OFD, LDG fluxes from OLD, past the term tasks
   static constexpr int WTMAX = QC * NGL, OFD = ((WTMAX + RU - 1) / RU) * RU, OLD = OFD + 4 * NQ;
   // REGACC (persistent sub-cycle): every accumulating task (quad point, face quad point, node,
@@ -358,11 +380,11 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   double *s_fq = S + C::O_FQ;      // [4][NQ][4]: wq, flux, H_kx+flux_x, H_ky+flux_y
   double *s_fl = S + C::O_FL;      // [4][NGL][2]
   double *s_rhs = S + C::O_RHS, *s_lap = S + C::O_LAP;  // [3][P], [2][P]
-  double *s_qn = S + C::O_QN;      // [P][4]
+  double *s_qn = C::SLIM ? s_qb : S + C::O_QN;  // [P][4] (SLIM: in place of the input, E1)
   double *s_fi = S + C::O_W;       // FPRE: [4][NQ][8] face-quad traces, own side | ghost side (A2 -> B)
   double *SI = S + C::O_BIN;       // B inputs
   double *SB = S + C::O_B;         // term buffers / partials
-  double *s_qp = SI + C::B_QP;     // [P][3] qprime of the bottom layer
+  double *s_qp = C::SLIM ? S + C::O_GR : SI + C::B_QP;  // [P][3] qprime of the bottom layer (A2)
   double *s_ef = SI + C::B_EF;     // [4][FBLK]
   double *s_tr = SI + C::B_TR;     // [4][8][NGL]
   double *s_ec = SI + C::B_EC;     // [4][EFC]
@@ -384,13 +406,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       glds_copy<BS>(m.basis, S + C::O_BASIS, 2 * C::NB, tid, rot);
       glds_copy<BS>(m.erec + (size_t)e * C::ERS, S + C::O_EREC, C::ERS, tid, rot);
       glds_copy<BS>(m.qstatE + (size_t)e * QE_N * Q, s_qk, 2 * QE_KEEP * Q, tid, rot);
-      glds_copy<BS>(a.ecoef + (size_t)e * C::ECO + 4 * Q, s_nc, 2 * 5 * P, tid, rot);
-      glds_copy<BS>(m.nstatE + (size_t)e * NE_N * P, s_ns, 2 * NE_N * P, tid, rot);
+      if constexpr (!C::SLIM) glds_copy<BS>(a.ecoef + (size_t)e * C::ECO + 4 * Q, s_nc, 2 * 5 * P, tid, rot);
+      glds_copy<BS>(m.nstatE + (size_t)e * NE_N * P, s_ns, 2 * (C::SLIM ? NE_LDS : NE_N) * P, tid, rot);
     }
     if (!PERSIST) {
       glds_copy<BS>(a.qb_in + (size_t)e * 4 * P, s_qb, 8 * P, tid, rot);
-      if (use_q0) glds_copy<BS>(a.qb0 + (size_t)e * 4 * P, s_q0, 8 * P, tid, rot);
-      if (use_q2) glds_copy<BS>(a.qb2 + (size_t)e * 4 * P, s_q2, 8 * P, tid, rot);
+      if (!C::SLIM && use_q0) glds_copy<BS>(a.qb0 + (size_t)e * 4 * P, s_q0, 8 * P, tid, rot);
+      if (!C::SLIM && use_q2) glds_copy<BS>(a.qb2 + (size_t)e * 4 * P, s_q2, 8 * P, tid, rot);
       if (m.etsrc) {
         // processor-face halo: each face's neighbour trace from its own slot (the receive
         // slot of a processor face); the slot ids are uniform, scalar loads
@@ -414,11 +436,16 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     // the element's state stays in LDS from stage to stage: the previous stage's result
     // (s_qn) becomes the input, and the Shu-Osher states qb0 / qb2 are kept copies of it.
     // Stage 0 reads the sub-cycle input written by the previous launch.
-    for (int t = tid; t < 4 * P; t += BS) {
-      const double x = first ? a.qb_in[(size_t)e * 4 * P + t] : s_qn[t];
-      s_qb[t] = x;
-      if (a.first_of_step) s_q0[t] = x;
-      if (a.save_q2) s_q2[t] = x;
+    if constexpr (C::SLIM) {  // (s_qn is s_qb; qb0 / qb2 are saved below)
+      if (first)
+        for (int t = tid; t < 4 * P; t += BS) s_qb[t] = a.qb_in[(size_t)e * 4 * P + t];
+    } else {
+      for (int t = tid; t < 4 * P; t += BS) {
+        const double x = first ? a.qb_in[(size_t)e * 4 * P + t] : s_qn[t];
+        s_qb[t] = x;
+        if (a.first_of_step) s_q0[t] = x;
+        if (a.save_q2) s_q2[t] = x;
+      }
     }
   }
   // Register loads for this thread's quad-point task in B (quad point tid), issued before
@@ -456,6 +483,19 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     load_pre();
   }
   STAGE_MARK(21);
+  if constexpr (C::SLIM && PERSIST) {
+    // the Shu-Osher states, saved by the E1 lane of each node (which reads them back in D)
+    if ((a.first_of_step || a.save_q2) && tid >= C::EW * 64 && tid - C::EW * 64 < P) {
+      const int p = tid - C::EW * 64;
+      double *d = a.qsv + (size_t)e * 8 * P + p * 4;
+#pragma unroll
+      for (int v = 1; v < 4; v++) {
+        const double x = s_qb[p * 4 + v];
+        if (a.first_of_step) d[v] = x;
+        if (a.save_q2) d[4 * P + v] = x;
+      }
+    }
+  }
 
   if (tid == 0) S[C::O_BASIS + C::NB] = 0.0;  // zero slot of the dpsi table (nz_coef)
 
@@ -1039,7 +1079,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   };
   // lap(c,p): volume over source nodes s=(ii,jj) (mod_laplacian_quad.F90:382-386), nonzero
   // terms only (jj==j or ii==i), then faces (:489-513)
-  auto lap_task = [&](int c, int p) {
+  auto lap_val = [&](int c, int p) {
     const int i = p % NGL, j = p / NGL;
     double acc = 0.0;
     const int qa = (2 * c) * P, qb_ = (2 * c + 1) * P;
@@ -1081,8 +1121,11 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     const int r0 = s_pf[2 * p], r1 = s_pf[2 * p + 1];
     if (r0 >= 0) acc = acc + s_fl[r0 * 2 + c];
     if (r1 >= 0) acc = acc + s_fl[r1 * 2 + c];
-    s_lap[c * P + p] = acc;
+    return acc;
   };
+  auto lap_task = [&](int c, int p) { s_lap[c * P + p] = lap_val(c, p); };
+  // SLIM: values the last wave loads for its qq and E1 lanes (see StageCfg::SLIM)
+  double r_q0[3] = {0.0, 0.0, 0.0}, r_q2[3] = {0.0, 0.0, 0.0}, r_mi = 0.0, r_pb = 0.0, r_lap[2] = {0.0, 0.0};
 
   if constexpr (SF) {
     // C1: first contraction pass over iq, per (v, i, jq):
@@ -1167,14 +1210,51 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       }
       s_rhs[v * P + p] = face_proj(v, p, acc);
     };
-    for_tasks<BS>(tid, 0, 3 * P, otf_task);
-    for_tasks<BS>(tid, 3 * P, P, [&](int t, bool) { qq_task(t); });
-    for_tasks<BS>(tid, 4 * P, 4 * NGL, ldg_task);
-    LDS_BARRIER();
-    STAGE_MARK(6);
-    for_tasks<BS>(tid, 0, 2 * P, [&](int t, bool) { lap_task(t / P, t % P); });
-    LDS_BARRIER();
-    STAGE_MARK(7);
+    if constexpr (C::SLIM) {
+      // waves 0..EW-1: the volume sums; the last wave: its register loads, qq, the LDG face
+      // fluxes and the Laplacian (it alone writes and reads qq and the face fluxes: a wave-local
+      // LDS wait, no barrier)
+      if (tid < C::EW * 64) {
+        for (int t = tid; t < 3 * P; t += C::EW * 64) otf_task(t, true);
+      } else {
+        const int p = tid - C::EW * 64;
+        if (p < P) {
+          const double *nco = a.ecoef + (size_t)e * C::ECO + 4 * Q + p;
+          double nc[5];
+#pragma unroll
+          for (int k = 0; k < 5; k++) nc[k] = nco[k * P];
+          const double *q0s = PERSIST ? a.qsv + (size_t)e * 8 * P : a.qb0 + (size_t)e * 4 * P;
+          const double *q2s = PERSIST ? a.qsv + (size_t)e * 8 * P + 4 * P : a.qb2 + (size_t)e * 4 * P;
+#pragma unroll
+          for (int v = 0; v < 3; v++) {
+            if (use_q0) r_q0[v] = q0s[p * 4 + 1 + v];
+            if (use_q2) r_q2[v] = q2s[p * 4 + 1 + v];
+          }
+          r_mi = m.nstatE[((size_t)e * NE_N + NE_MINV) * P + p];
+          r_pb = m.nstatE[((size_t)e * NE_N + NE_PB) * P + p];
+          // qq_task with its coefficients from registers
+#pragma unroll
+          for (int c = 0; c < 4; c++) s_qq[c * P + p] = nc[NC_PV] * s_grad[c * P + p] + nc[NC_D1 + c];
+        }
+        if (p < 4 * NGL) ldg_task(p, false);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (p < P && !(a.dbg & 2)) {
+          r_lap[0] = lap_val(0, p);
+          r_lap[1] = lap_val(1, p);
+        }
+      }
+      LDS_BARRIER();
+      STAGE_MARK(6);
+    } else {
+      for_tasks<BS>(tid, 0, 3 * P, otf_task);
+      for_tasks<BS>(tid, 3 * P, P, [&](int t, bool) { qq_task(t); });
+      for_tasks<BS>(tid, 4 * P, 4 * NGL, ldg_task);
+      LDS_BARRIER();
+      STAGE_MARK(6);
+      for_tasks<BS>(tid, 0, 2 * P, [&](int t, bool) { lap_task(t / P, t % P); });
+      LDS_BARRIER();
+      STAGE_MARK(7);
+    }
   } else {
     // D0 .. D_NCH: weak-form terms T(v,p,q) of quad-row chunk k computed in parallel into
     // term buffer k&1 (create_rhs_btp_volume_qdf, mod_rhs_btp.F90:194-206: rhs(v,I) +=
@@ -1360,19 +1440,22 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   if constexpr (PERSIST && !C::RES) {
     if (a.write_trace) {  // a next stage follows
       int rot = 0;
-      if (m.botfr && qpm == 0) glds_copy<BS>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
+      if (!C::SLIM && m.botfr && qpm == 0) glds_copy<BS>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
       glds_copy<BS>(m.efstat + (size_t)e * 4 * C::FBLK, s_ef, 2 * 4 * C::FBLK, tid, rot);
       glds_copy<BS>(a.efcoef + (size_t)e * 4 * C::EFC, s_ec, 2 * 4 * C::EFC, tid, rot);
     }
   }
 
   // ------------------------------------------------------------- E1: update + wall fix
-  for (int p = tid; p < P; p += BS) {
+  // (SLIM: on the last wave, with its registers; otherwise wave 0)
+  constexpr int EW0 = C::SLIM ? C::EW * 64 : 0;
+  static_assert(P <= 64, "E1 and the nodal gradients run on one wave");
+  for (int p = tid - EW0; p >= 0 && p < P; p += BS) {
     const size_t I = (size_t)e * P + p;
-    const double mi = s_ns[NE_MINV * P + p];
+    const double mi = C::SLIM ? r_mi : s_ns[NE_MINV * P + p];
     double rh0 = mi * s_rhs[0 * P + p], rh1 = mi * s_rhs[1 * P + p], rh2 = mi * s_rhs[2 * P + p];
-    const double l0 = a.lapq ? a.lapq[I] : s_lap[0 * P + p];
-    const double l1 = a.lapq ? a.lapq[(size_t)npoin + I] : s_lap[1 * P + p];
+    const double l0 = a.lapq ? a.lapq[I] : (C::SLIM ? r_lap[0] : s_lap[0 * P + p]);
+    const double l1 = a.lapq ? a.lapq[(size_t)npoin + I] : (C::SLIM ? r_lap[1] : s_lap[1 * P + p]);
     rh1 = rh1 + m.visc * mi * l0;
     rh2 = rh2 + m.visc * mi * l1;
     if (a.rhs_only) {
@@ -1387,12 +1470,12 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
 #pragma unroll
     for (int v = 1; v < 4; v++) {
       double x = 0.0;
-      if (a.a1 != 0.0) x = a.a1 * s_q0[p * 4 + v];
+      if (a.a1 != 0.0) x = a.a1 * (C::SLIM ? r_q0[v - 1] : s_q0[p * 4 + v]);
       x = x + a.a2 * s_qb[p * 4 + v];
-      if (a.a3 != 0.0) x = x + a.a3 * s_q2[p * 4 + v];
+      if (a.a3 != 0.0) x = x + a.a3 * (C::SLIM ? r_q2[v - 1] : s_q2[p * 4 + v]);
       qn[v] = x + a.dtt * rh[v - 1];
     }
-    qn[0] = qn[1] + s_ns[NE_PB * P + p];
+    qn[0] = qn[1] + (C::SLIM ? r_pb : s_ns[NE_PB * P + p]);
     // btp_mom_boundary_df (mod_barotropic_terms.F90:180-215), faces in face-id order
 #pragma unroll
     for (int kf = 0; kf < 2; kf++) {
@@ -1419,10 +1502,9 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     // grad(u_bar) of the new state at every node, once (the sums B's nodal task forms): the
     // traces below read it, and the persistent kernel's next stage takes it as its own.  The
     // nodes' u_bar, v_bar were written by this same wave (P <= 64).
-    static_assert(P <= 64, "E1 and the nodal gradients run on wave 0");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (tid < P) {
-      const int p = tid, i = p % NGL, j = p / NGL;
+    if (tid >= EW0 && tid - EW0 < P) {
+      const int p = tid - EW0, i = p % NGL, j = p / NGL;
       double g[4];
       nodal_grad4<NGL>(s_dpsi, i, j, s_ns[NE_EX * P + p], s_ns[NE_EY * P + p], s_ns[NE_NX * P + p],
                        s_ns[NE_NY * P + p], s_u, s_v, g);

@@ -300,13 +300,15 @@ def test_factored_summation_parity(cfg, case_factory, engines):
         assert np.abs(qbe[v] - qb[v]).max() / (pb * np.sqrt(g * pb)) < 1e-6, v
 
 
-@pytest.mark.parametrize("cfg", ["bump10", "dg25L3"])
+@pytest.mark.parametrize("cfg", ["bump10", "dg25L3", "dg25N7L3"])
 def test_persistent_subcycle_matches_stage_launches(cfg, case_factory, monkeypatch):
     """The persistent sub-cycle kernel (one launch per sub-cycle, neighbour hand-offs in the
-    launch) gives the same bits as one launch per stage (HNUMO_PERSISTENT=0)."""
+    launch) gives the same bits as one launch per stage (HNUMO_PERSISTENT=0).  dg25N7L3 (C3,
+    625 elements at N=7): the slim LDS arena fits 3 workgroups per CU, so all are resident."""
     from hnumo.engine import Engine
     case = case_factory(cfg)
     e1 = Engine(case)
+    assert e1.stage_path == "persistent", e1.stage_path
     monkeypatch.setenv("HNUMO_PERSISTENT", "0")
     e0 = Engine(case)
     monkeypatch.delenv("HNUMO_PERSISTENT")
