@@ -53,6 +53,12 @@
 #ifndef HNUMO_SLIM
 #define HNUMO_SLIM 1
 #endif
+#ifndef HNUMO_SLIM_LATE
+#define HNUMO_SLIM_LATE 1
+#endif
+#ifndef HNUMO_OTF_PAIR
+#define HNUMO_OTF_PAIR 1
+#endif
 #ifndef HNUMO_OTF_UNROLL
 #define HNUMO_OTF_UNROLL 5
 #endif
@@ -175,6 +181,15 @@ struct StageCfg {
   // from global memory while waves 0..2 sum) instead of LDS; the new state overwrites the
   // stage input in place; the bottom-layer qprime (A2 only) overlays the nodal gradients.
   static constexpr bool SLIM = OTF && HNUMO_SLIM;
+  // SLATE (SLIM): the face fluxes also run on the last wave in D, so the neighbour traces are
+  // needed (persistent: polled) only there, behind the element's own interpolation, quad-point
+  // physics and most of its volume sums -- the neighbours' stage-to-stage skew hides behind them;
+  // the volume sums' face lifts follow a barrier
+  static constexpr bool SLATE = SLIM && HNUMO_SLIM_LATE;
+  // OPAIR (SLATE): a node's component-1 and -2 volume sums on one thread (see otf_sum12).  Used by
+  // the per-stage kernel only (stage_body's PERSIST = false): at dg25N7L3 it took the per-stage
+  // launch from 65.0 to 57.0 us, but the persistent sub-cycle from 56.4 to 63.6 us
+  static constexpr bool OPAIR = SLATE && HNUMO_OTF_PAIR;
   static constexpr int EW = BS / 64 - 1;
   static_assert(!SLIM || (P <= 64 && 3 * P <= EW * 64), "SLIM: one node per lane of the last wave");
   // LDS arena (doubles).  Persistent (A..E); the wall normals of the face nodes are copied
@@ -192,7 +207,7 @@ struct StageCfg {
                        O_W = O_FL + 8 * NGL, O_QQ = O_W, O_RHS = O_QQ + 4 * P, O_LAP = O_RHS + 3 * P,
                        O_QN = O_LAP + (SLIM ? 0 : 2 * P), O_Y = O_W, W_END0 = O_QN + (SLIM ? 0 : 4 * P),
                        QN_END_W = W_END0 - O_W,
-                       W_END = (SLIM && O_W + 32 * NQ > W_END0) ? O_W + 32 * NQ : W_END0,
+                       W_END = (SLIM && !SLATE && O_W + 32 * NQ > W_END0) ? O_W + 32 * NQ : W_END0,
                        O_BIN = (SF && O_Y + NYV * NGL * NQ > W_END) ? O_Y + NYV * NGL * NQ : W_END;
   // B inputs: the bottom-layer qprime, face statics, neighbour traces, face coefficients.
   // RES: resident for the whole launch (the persistent sub-cycle loads them once), the work
@@ -236,14 +251,14 @@ struct StageCfg {
   // [OG,OG+P) | LDG face nodes [OL,OL+4NGL) (SF: C1), on their own
   // waves when they fit
   static constexpr int RU = 64, OFa = ((Q + RU - 1) / RU) * RU,
-                       OGa = LATE ? OFa : ((OFa + 4 * NQ + RU - 1) / RU) * RU;
+                       OGa = (LATE || SLATE) ? OFa : ((OFa + 4 * NQ + RU - 1) / RU) * RU;
   static constexpr bool WIDE = OGa + P + (SF ? 4 * NGL : 0) <= BS;  // (exact: the LDG range runs in D0)
-  static constexpr int OF = WIDE ? OFa : Q, OG = WIDE ? OGa : (LATE ? Q : OF + 4 * NQ), OL = OG + P,
+  static constexpr int OF = WIDE ? OFa : Q, OG = WIDE ? OGa : ((LATE || SLATE) ? Q : OF + 4 * NQ), OL = OG + P,
                        WEND = OL + 4 * NGL, BEND = OL;
   // FPRE (exact, not LATE): A2 also interpolates each face's own-side traces and, on physical
   // boundaries, the ghost-side traces to the face quad points, into s_fi [4][NQ][8] (in the
   // W region, dead from A to D0), so B's face fluxes interpolate only the neighbour traces
-  static constexpr bool FPRE = !SF && !LATE && (SLIM || 4 * NQ * 8 <= QN_END_W);
+  static constexpr bool FPRE = !SF && !LATE && !SLATE && (SLIM || 4 * NQ * 8 <= QN_END_W);
   // LATE chunk phase KP+1: face fluxes from OFD, LDG fluxes from OLD, past the term tasks
   static constexpr int WTMAX = QC * NGL, OFD = ((WTMAX + RU - 1) / RU) * RU, OLD = OFD + 4 * NQ;
   // REGACC (persistent sub-cycle): every accumulating task (quad point, face quad point, node,
@@ -562,7 +577,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   constexpr bool FD0 = C::FD0;
   granule_u4 gxr[C::NGR];
   auto issue_granules_wave = [&]() {
-    if constexpr (PERSIST && FD0) {
+    if constexpr (PERSIST && (FD0 || C::SLATE)) {
       if (tid >= BS - 64) {
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(a.gtr_in + (size_t)e * 32 * NGL), 0, 32 * NGL * (int)sizeof(TraceGranule), 0x00020000);
@@ -573,7 +588,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     }
   };
   auto poll_wave = [&]() {
-    if constexpr (PERSIST && FD0) {
+    if constexpr (PERSIST && (FD0 || C::SLATE)) {
       const unsigned long long want = (ep << 20) | a.tag_in;
       const unsigned long long c0 = a.prof ? clock64() : 0;
 #pragma unroll
@@ -598,7 +613,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   };
   if constexpr (FD0)
     issue_granules_wave();
-  else if constexpr (!LATE)
+  else if constexpr (!LATE && !C::SLATE)
     issue_granule();
   {
     // persistent, after the first stage: the wall normals and u_bar, v_bar of this state are in
@@ -725,7 +740,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       }
     }
   }
-  if constexpr (!LATE && !FD0) poll_traces();  // (the granule was issued before the interpolation)
+  if constexpr (!LATE && !FD0 && !C::SLATE) poll_traces();  // (the granule was issued before the interpolation)
   LDS_BARRIER();
   STAGE_MARK(1);
 
@@ -957,7 +972,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         s_qv[5 * Q + q] = sc_y;
         s_qv[6 * Q + q] = Hq + qv;
       }
-    } else if (!LATE && !FD0 && w >= C::OF && w < C::OF + 4 * NQ) {
+    } else if (!LATE && !FD0 && !C::SLATE && w >= C::OF && w < C::OF + 4 * NQ) {
       face_task(w - C::OF);
     } else if (w >= C::OG && w < C::OL) {
       const int p = w - C::OG, i = p % NGL, j = p / NGL;
@@ -1184,7 +1199,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     // zero term can only differ in the sign of zero -- added to a sum that starts at +0 it
     // changes nothing (round-to-nearest never produces -0 from +0 + x).  Then the face
     // projections; qq and the LDG face fluxes run beside; the Laplacian after the barrier.
-    auto otf_task = [&](int t, bool) {
+    auto otf_sum = [&](int t) {
       const int v = t / P, p = t % P, i = p % NGL, j = p / NGL;
       const int r1 = v == 2 ? 5 : 2, r2 = v == 0 ? 0 : (v == 1 ? 3 : 4), r3 = v == 0 ? 1 : (v == 1 ? 4 : 6);
       const bool z1 = v == 0;
@@ -1208,33 +1223,113 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           acc = acc + Wq[q] * ((hi * s1 + dhdx * Q2[q]) + Q3[q] * dhdy);
         }
       }
-      s_rhs[v * P + p] = face_proj(v, p, acc);
+      return acc;
+    };
+    auto otf_task = [&](int t, bool) { s_rhs[t] = face_proj(t / P, t % P, otf_sum(t)); };
+    // OPAIR: node p's component-0 sum on one thread (without the zero hi*s1 term: the
+    // reference's own wq*(dhdx*udp + dhdy*vdp)), its component-1 and -2 sums together on
+    // another, sharing hi, dhdx, dhdy -- 36 instead of 48 f64 operations per (p, q), the same
+    // terms in the same order
+    auto otf_sum0 = [&](int p) {
+      const int i = p % NGL, j = p / NGL;
+      const double *U = s_qv + 0 * Q, *V = s_qv + 1 * Q;
+      const double *Wq = s_qk + QE_W * Q, *Ex = s_qk + QE_EX * Q, *Ey = s_qk + QE_EY * Q;
+      const double *Nx = s_qk + QE_NX * Q, *Ny = s_qk + QE_NY * Q;
+      const double *Pi = s_psiq + i * NQ, *DPi = s_dpsiq + i * NQ, *Pj = s_psiq + j * NQ, *DPj = s_dpsiq + j * NQ;
+      double acc = 0.0;
+#pragma unroll 1
+      for (int jq = 0; jq < NQ; jq++) {
+        const double pj = Pj[jq], dpj = DPj[jq];
+        const int q0 = jq * NQ;
+#pragma unroll HNUMO_OTF_UNROLL
+        for (int iq = 0; iq < NQ; iq++) {
+          const int q = q0 + iq;
+          const double pi = Pi[iq], dpi = DPi[iq];
+          const double h_e = dpi * pj, h_n = pi * dpj;
+          const double dhdx = h_e * Ex[q] + h_n * Nx[q];
+          const double dhdy = h_e * Ey[q] + h_n * Ny[q];
+          acc = acc + Wq[q] * (dhdx * U[q] + V[q] * dhdy);
+        }
+      }
+      return acc;
+    };
+    auto otf_sum12 = [&](int p, double &acc1, double &acc2) {
+      const int i = p % NGL, j = p / NGL;
+      const double *SX = s_qv + 2 * Q, *A_ = s_qv + 3 * Q, *UV = s_qv + 4 * Q, *SY = s_qv + 5 * Q, *B_ = s_qv + 6 * Q;
+      const double *Wq = s_qk + QE_W * Q, *Ex = s_qk + QE_EX * Q, *Ey = s_qk + QE_EY * Q;
+      const double *Nx = s_qk + QE_NX * Q, *Ny = s_qk + QE_NY * Q;
+      const double *Pi = s_psiq + i * NQ, *DPi = s_dpsiq + i * NQ, *Pj = s_psiq + j * NQ, *DPj = s_dpsiq + j * NQ;
+      double a1 = 0.0, a2 = 0.0;
+#pragma unroll 1
+      for (int jq = 0; jq < NQ; jq++) {
+        const double pj = Pj[jq], dpj = DPj[jq];
+        const int q0 = jq * NQ;
+#pragma unroll HNUMO_OTF_UNROLL
+        for (int iq = 0; iq < NQ; iq++) {
+          const int q = q0 + iq;
+          const double pi = Pi[iq], dpi = DPi[iq];
+          const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
+          const double dhdx = h_e * Ex[q] + h_n * Nx[q];
+          const double dhdy = h_e * Ey[q] + h_n * Ny[q];
+          const double w = Wq[q], uv = UV[q];
+          a1 = a1 + w * ((hi * SX[q] + dhdx * A_[q]) + uv * dhdy);
+          a2 = a2 + w * ((hi * SY[q] + dhdx * uv) + B_[q] * dhdy);
+        }
+      }
+      acc1 = a1;
+      acc2 = a2;
     };
     if constexpr (C::SLIM) {
       // waves 0..EW-1: the volume sums; the last wave: its register loads, qq, the LDG face
       // fluxes and the Laplacian (it alone writes and reads qq and the face fluxes: a wave-local
       // LDS wait, no barrier)
+      double acc_r = 0.0, acc_r2 = 0.0;  // SLATE: this thread's volume sum(s), lifted after the barrier
       if (tid < C::EW * 64) {
-        for (int t = tid; t < 3 * P; t += C::EW * 64) otf_task(t, true);
+        if constexpr (C::OPAIR && !PERSIST) {
+          if (tid < P)
+            acc_r = otf_sum0(tid);
+          else if (tid >= 64 && tid < 64 + P)
+            otf_sum12(tid - 64, acc_r, acc_r2);
+          if (a.prof && tid == 0) s_prof[28] = clock64();
+        } else if constexpr (C::SLATE) {
+          if (tid < 3 * P) acc_r = otf_sum(tid);
+          if (a.prof && tid == 0) s_prof[28] = clock64();
+        } else {
+          for (int t = tid; t < 3 * P; t += C::EW * 64) otf_task(t, true);
+        }
       } else {
         const int p = tid - C::EW * 64;
+        // the E1 lane's values (see StageCfg::SLIM), loaded now or, SLATE, after the Laplacian
+        auto load_e1 = [&]() {
+          if (p < P) {
+            const double *q0s = PERSIST ? a.qsv + (size_t)e * 8 * P : a.qb0 + (size_t)e * 4 * P;
+            const double *q2s = PERSIST ? a.qsv + (size_t)e * 8 * P + 4 * P : a.qb2 + (size_t)e * 4 * P;
+#pragma unroll
+            for (int v = 0; v < 3; v++) {
+              if (use_q0) r_q0[v] = q0s[p * 4 + 1 + v];
+              if (use_q2) r_q2[v] = q2s[p * 4 + 1 + v];
+            }
+            r_mi = m.nstatE[((size_t)e * NE_N + NE_MINV) * P + p];
+            r_pb = m.nstatE[((size_t)e * NE_N + NE_PB) * P + p];
+          }
+        };
+        if constexpr (!C::SLATE) load_e1();
         if (p < P) {
           const double *nco = a.ecoef + (size_t)e * C::ECO + 4 * Q + p;
           double nc[5];
 #pragma unroll
           for (int k = 0; k < 5; k++) nc[k] = nco[k * P];
-          const double *q0s = PERSIST ? a.qsv + (size_t)e * 8 * P : a.qb0 + (size_t)e * 4 * P;
-          const double *q2s = PERSIST ? a.qsv + (size_t)e * 8 * P + 4 * P : a.qb2 + (size_t)e * 4 * P;
-#pragma unroll
-          for (int v = 0; v < 3; v++) {
-            if (use_q0) r_q0[v] = q0s[p * 4 + 1 + v];
-            if (use_q2) r_q2[v] = q2s[p * 4 + 1 + v];
-          }
-          r_mi = m.nstatE[((size_t)e * NE_N + NE_MINV) * P + p];
-          r_pb = m.nstatE[((size_t)e * NE_N + NE_PB) * P + p];
           // qq_task with its coefficients from registers
 #pragma unroll
           for (int c = 0; c < 4; c++) s_qq[c * P + p] = nc[NC_PV] * s_grad[c * P + p] + nc[NC_D1 + c];
+        }
+        if constexpr (C::SLATE) {
+          // the neighbour traces (persistent: checked now), then the face fluxes
+          issue_granules_wave();
+          poll_wave();
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          for (int t = p; t < 4 * NQ; t += 64) face_task(t);
+          asm volatile("" ::: "memory");
         }
         if (p < 4 * NGL) ldg_task(p, false);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1242,9 +1337,24 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           r_lap[0] = lap_val(0, p);
           r_lap[1] = lap_val(1, p);
         }
+        if constexpr (C::SLATE) load_e1();
+      }
+      if constexpr (C::SLATE) {
+        LDS_BARRIER();  // the face fluxes are in
+        STAGE_MARK(6);
+        if constexpr (C::OPAIR && !PERSIST) {
+          if (tid < P) {
+            s_rhs[tid] = face_proj(0, tid, acc_r);
+          } else if (tid >= 64 && tid < 64 + P) {
+            s_rhs[P + tid - 64] = face_proj(1, tid - 64, acc_r);
+            s_rhs[2 * P + tid - 64] = face_proj(2, tid - 64, acc_r2);
+          }
+        } else if (tid < 3 * P) {
+          s_rhs[tid] = face_proj(tid / P, tid % P, acc_r);
+        }
       }
       LDS_BARRIER();
-      STAGE_MARK(6);
+      STAGE_MARK(C::SLATE ? 7 : 6);
     } else {
       for_tasks<BS>(tid, 0, 3 * P, otf_task);
       for_tasks<BS>(tid, 3 * P, P, [&](int t, bool) { qq_task(t); });
@@ -1564,7 +1674,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     STAGE_MARK(5);
     if (tid == 0) {
       if (PERSIST) {  // sums over the stages: A incl. the trace waits | the rest | stages
-        if (first) s_prof[24] = s_prof[25] = s_prof[26] = s_prof[27] = 0;
+        if (first) s_prof[24] = s_prof[25] = s_prof[26] = s_prof[27] = s_prof[8] = s_prof[9] = s_prof[10] = s_prof[11] = s_prof[29] = 0;
+        // per-phase sums over the stages: A2 | B | D | E, and (SLATE) the volume sums of wave 0
+        s_prof[8] += s_prof[1] - s_prof[21];
+        s_prof[9] += s_prof[2] - s_prof[1];
+        s_prof[10] += s_prof[3] - s_prof[2];
+        s_prof[11] += s_prof[5] - s_prof[3];
+        if (C::SLATE) s_prof[29] += s_prof[28] - s_prof[2];
         s_prof[27] += s_prof[22];
         s_prof[24] += s_prof[21] - s_prof[0];
         s_prof[25] += s_prof[5] - s_prof[21];

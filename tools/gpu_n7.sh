@@ -10,5 +10,5 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-me
 tail -1 $O/pytest.log
 timeout -k 10 300 python -u tools/ab_stage.py dg25N7L3:persist dg25N7L3:stage dg25L3:persist > $O/ab_new.log 2>&1 || { echo "ab new failed"; tail -20 $O/ab_new.log; exit 1; }
 cat $O/ab_new.log
-HNUMO_LIB=$2 timeout -k 10 300 python -u tools/ab_stage.py dg25N7L3:stage dg25L3:persist > $O/ab_ref.log 2>&1 || { echo "ab ref failed"; tail -20 $O/ab_ref.log; exit 1; }
+HNUMO_LIB=$2 timeout -k 10 300 python -u tools/ab_stage.py dg25N7L3:persist dg25N7L3:stage > $O/ab_ref.log 2>&1 || { echo "ab ref failed"; tail -20 $O/ab_ref.log; exit 1; }
 cat $O/ab_ref.log

@@ -60,6 +60,9 @@ if pr[:, 26].max() > 0:
         print(f"    xcc {x}: work-wait mean {(wk - wt)[sel].mean():.0f}, wait {wt[sel].mean():.0f}")
     bpc = c[np.searchsorted(u, key)]
     print(f"  persistent: per stage A(+waits) mean {aw.mean():.0f} clk, work mean {wk.mean():.0f} clk")
+    ph = [pr[:, k] / nst for k in (8, 9, 10, 11, 29)]
+    print("  persistent per-stage phase means: A2 %.0f | B %.0f | D %.0f (wave-0 volume sums %.0f) | E %.0f clk"
+          % (ph[0].mean(), ph[1].mean(), ph[2].mean(), ph[4].mean(), ph[3].mean()))
     for k in sorted(set(bpc.tolist())):
         sel = bpc == k
         print(f"    CUs with {k} blocks: {sel.sum()} blocks, A(+waits) {aw[sel].mean():.0f}, work {wk[sel].mean():.0f} "
