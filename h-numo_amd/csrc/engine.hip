@@ -288,16 +288,6 @@ __global__ void copy_kernel(double *dst, const double *src, size_t n) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s) dst[i] = src[i];
 }
 
-// dpp2 = qp2(1); qp2(1) = 0.5*(qp(1) + dpp2)   (ti_rk_bcl.F90:78-79)
-__global__ void dp_average_kernel(double *qp2, const double *qp, double *dpp2, size_t n) {
-  const size_t s = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s) {
-    double d = qp2[i * 3];
-    dpp2[i] = d;
-    qp2[i * 3] = 0.5 * (qp[i * 3] + d);
-  }
-}
-
 // non-finite guard on the barotropic state (ABI return code 2); bit 2 of the flag word
 __global__ void finite_check_kernel(const double *x, size_t n, int *flag) {
   const size_t s = (size_t)gridDim.x * blockDim.x;
@@ -306,14 +296,40 @@ __global__ void finite_check_kernel(const double *x, size_t n, int *flag) {
   if (__any(bad) && (threadIdx.x % 64) == 0) atomicOr(flag, 2);
 }
 
-// qprime(1) = dpp2; qprime(2:3) = qprime2(2:3)   (ti_rk_bcl.F90:84-85)
-__global__ void qprime_final_kernel(double *qp, const double *qp2, const double *dpp2, size_t n) {
+// qprime(1) = dpp2; qprime(2:3) = qprime2(2:3)   (ti_rk_bcl.F90:84-85), and in the same launch
+// the non-finite guard on the barotropic state x[nx] (finite_check_kernel)
+__global__ void qprime_final_kernel(double *qp, const double *qp2, const double *dpp2, size_t n, const double *x,
+                                    size_t nx, int *flag) {
   const size_t s = (size_t)gridDim.x * blockDim.x;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s) {
     qp[i * 3] = dpp2[i];
     qp[i * 3 + 1] = qp2[i * 3 + 1];
     qp[i * 3 + 2] = qp2[i * 3 + 2];
   }
+  bool bad = false;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nx; i += s) bad |= !isfinite(x[i]);
+  if (__any(bad) && (threadIdx.x % 64) == 0) atomicOr(flag, 2);
+}
+
+// The corrector's two averages in one launch (ti_rk_bcl.F90:64-65): a0 = 0.5*(a0 + b0) [n0],
+// a1 = 0.5*(b1 + a1) [n1]
+__global__ void average2_kernel(double *a0, const double *b0, size_t n0, double *a1, const double *b1, size_t n1) {
+  const size_t s = (size_t)gridDim.x * blockDim.x, t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (size_t i = t0; i < n0; i += s) a0[i] = 0.5 * (a0[i] + b0[i]);
+  for (size_t i = t0; i < n1; i += s) a1[i] = 0.5 * (b1[i] + a1[i]);
+}
+
+// dpp2 = qp2(1); qp2(1) = 0.5*(qp(1) + dpp2) (ti_rk_bcl.F90:78-79) with, in the same launch, the
+// face average of component 1: qf2(1) = 0.5*(qf(1) + qf2(1)) at stride 3 (:80)
+__global__ void dp_average_face_kernel(double *qp2, const double *qp, double *dpp2, size_t n, double *qf2,
+                                       const double *qf, size_t nf) {
+  const size_t s = (size_t)gridDim.x * blockDim.x, t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (size_t i = t0; i < n; i += s) {
+    double d = qp2[i * 3];
+    dpp2[i] = d;
+    qp2[i * 3] = 0.5 * (qp[i * 3] + d);
+  }
+  for (size_t i = t0; i < nf; i += s) qf2[i * 3] = 0.5 * (qf[i * 3] + qf2[i * 3]);
 }
 
 // ------------------------------------------------------------------ ghost exchange
@@ -529,11 +545,6 @@ static void launch_copy(hnumo_engine *e, double *dst, const double *src, size_t 
   (void)hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, e->stream);
 }
 
-static void launch_avg(hnumo_engine *e, double *out, const double *a, const double *b, size_t n, int stride) {
-  int blocks = (int)std::min<size_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(average_kernel, dim3(std::max(blocks, 1)), dim3(256), 0, e->stream, out, a, b, n, stride);
-}
-
 // Sub-cycle prologue (mod_rk_mlswe.F90:45-72): zero the time averages, copy the state into
 // stage buffer 0 and bump the persistent kernel's epoch -- one launch instead of four memsets,
 // a copy and a one-thread kernel (each a graph node of ~4 us at this size).
@@ -650,7 +661,7 @@ static void launch_subcycle(hnumo_engine *e, double *dst, const double *qp, bool
   const bool racc = pers && e->regacc[e->summation] && !(e->stage_dbg & 32);
   if (!racc) subcycle_prologue(e, e->qb, nullptr, true);
   if (!pers) exchange_qb(e, e->qbuf[0]);
-  DISPATCH(e, grad_trace(e, pers ? e->qb : e->qbuf[0], e->gtrace[0], 0, e->nelem, pers ? e->gtr[0] : nullptr));
+  if (!pers) DISPATCH(e, grad_trace(e, e->qbuf[0], e->gtrace[0], 0, e->nelem));  // (persistent: its stage 0)
   const int K = e->K, NB = e->p.N_btp;
   int cur;
   if (pers) {
@@ -725,8 +736,8 @@ static void launch_step(hnumo_engine *e) {
   exchange_qp(e, e->qp2);
   DISPATCH(e, extract(e, e->qp2, e->qf2, 0));
   // correction (ti_rk_bcl.F90:62-85)
-  launch_avg(e, e->qp2, e->qp2, e->qp, n3, 1);
-  launch_avg(e, e->qf2, e->qf, e->qf2, nf, 1);
+  hipLaunchKernelGGL(average2_kernel, dim3((int)std::min<size_t>((n3 + 255) / 256, 2048)), dim3(256), 0, e->stream,
+                     e->qp2, e->qp, n3, e->qf2, e->qf, nf);
   DISPATCH(e, bcl_coeffs(e, e->qp2, e->qf2));
   launch_subcycle(e, e->qb, e->qp2, true);
   DISPATCH(e, mass(e, e->qp2, e->qf2, e->q));
@@ -734,12 +745,12 @@ static void launch_step(hnumo_engine *e) {
   DISPATCH(e, cons(e, e->q, e->qp2, 1));
   exchange_qp(e, e->qp2);
   DISPATCH(e, extract(e, e->qp2, e->qf2, 1));
-  hipLaunchKernelGGL(dp_average_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp2, e->qp, e->dpp2, nl);
-  launch_avg(e, e->qf2, e->qf, e->qf2, nf / 3, 3);
+  hipLaunchKernelGGL(dp_average_face_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp2, e->qp, e->dpp2, nl, e->qf2,
+                     e->qf, nf / 3);
   DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qb, e->q, e->qp2, 1));
-  hipLaunchKernelGGL(qprime_final_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp, e->qp2, e->dpp2, nl);
+  hipLaunchKernelGGL(qprime_final_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp, e->qp2, e->dpp2, nl, e->qb,
+                     4 * (size_t)e->npoin, e->neg_flag);
   exchange_qp(e, e->qp);
-  hipLaunchKernelGGL(finite_check_kernel, dim3(256), dim3(256), 0, e->stream, e->qb, 4 * (size_t)e->npoin, e->neg_flag);
   // ad_mlswe > 0 with the reference's corrector input leaves NaN layer momenta (hnumo_params)
   if (e->p.ad_mlswe > 0.0)
     hipLaunchKernelGGL(finite_check_kernel, dim3(256), dim3(256), 0, e->stream, e->q, n3, e->neg_flag);
@@ -1277,6 +1288,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
       std::vector<StageArgs> st;
       (void)stage_table(eng, qps[v], st);
       st.front().qb_in = eng->qb;                        // the step-start state (launch_subcycle)
+      st.front().self_trace = 1;                         // stage 0 publishes its input traces
       st.back().qb_out = v == 0 ? eng->qbp : eng->qb;    // predictor / corrector result
       eng->d_stages[v] = dalloc<StageArgs>(eng, st.size());
       if (eng->alloc_failed) return fail(eng, HNUMO_ERR_DEVICE, "hipMalloc failed (stage tables)");

@@ -190,15 +190,6 @@ __global__ void extract_face_kernel(DevMesh m, const double *qp, double *qf, int
   }
 }
 
-// out = 0.5*(a + b) elementwise (ti_rk_bcl.F90:64-65,79-80); comp1_only: stride-3 component 1
-__global__ void average_kernel(double *out, const double *a, const double *b, size_t n, int stride) {
-  const size_t stride_ = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride_) {
-    size_t j = i * stride;
-    out[j] = 0.5 * (a[j] + b[j]);
-  }
-}
-
 // ======================================================= btp_bcl_coeffs_qdf: element
 // Q_uu_dp, Q_uv_dp, Q_vv_dp, H_bcl at quad points (mod_barotropic_terms.F90:265-283);
 // dpp_graduv, btp_dpp_graduv, pbprime_visc at nodes (:287-304).  dpprime_visc =

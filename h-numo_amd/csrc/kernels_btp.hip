@@ -132,6 +132,9 @@ struct StageArgs {
   // ([E][2][P][4], components 1..3) -- kept by the E1 lane of each node
   double *qsv;
   double n_inv;                              // 1/(N_btp*kstages): the averages' normalisation
+  // persistent sub-cycle, stage 0: publish the input state's face traces (qb and grad(u_bar))
+  // as this stage's granules before polling the neighbours' (no grad_trace launch before it)
+  int self_trace;
 };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -740,6 +743,30 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       }
     }
   }
+  if constexpr (PERSIST) {
+    if (first && a.self_trace) {
+      // the input state's traces for the neighbours' stage 0 (what grad_trace_kernel writes for the
+      // per-stage path): grad(u_bar) at every node (B takes it from s_grad), then the granules
+      LDS_BARRIER();  // u_bar, v_bar (A2)
+      if (tid < P) {
+        const int p = tid, i = p % NGL, j = p / NGL;
+        double g[4];
+        nodal_grad4<NGL>(s_dpsi, i, j, s_ns[NE_EX * P + p], s_ns[NE_EY * P + p], s_ns[NE_NX * P + p],
+                         s_ns[NE_NY * P + p], s_u, s_v, g);
+#pragma unroll
+        for (int c = 0; c < 4; c++) s_grad[c * P + p] = g[c];
+      }
+      LDS_BARRIER();
+      for (int t = tid; t < 4 * 8 * NGL; t += BS) {
+        const int lf = t / (8 * NGL), c = (t / NGL) % 8, n = t % NGL;
+        if (s_bc[lf] < 0) continue;
+        const int p = s_map[lf * NGL + n];
+        const double val = c < 4 ? s_qb[p * 4 + c] : s_grad[(c - 4) * P + p];
+        const size_t slot = (((size_t)s_nbe[lf] * 4 + s_nblf[lf]) * 8 + c) * NGL + n;
+        st_granule(a.gtr_in + slot, val, (ep << 20) | a.tag_in);
+      }
+    }
+  }
   if constexpr (!LATE && !FD0 && !C::SLATE) poll_traces();  // (the granule was issued before the interpolation)
   LDS_BARRIER();
   STAGE_MARK(1);
@@ -977,7 +1004,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     } else if (w >= C::OG && w < C::OL) {
       const int p = w - C::OG, i = p % NGL, j = p / NGL;
       double g[4];
-      if (PERSIST && !first) {  // formed by the previous stage's E2 for this same state
+      if (PERSIST && (!first || a.self_trace)) {  // formed by the previous stage's E2 (or A2) for this state
 #pragma unroll
         for (int c = 0; c < 4; c++) g[c] = s_grad[c * P + p];
       } else {
