@@ -12,7 +12,8 @@ condition (data: synthetic IC, no files).
 Workloads (BASELINE.json configs):
   N=1   dg25L3  -- configs[1], the double gyre at 25x25 elements, N=4, 3 layers (the metric's
                    1-GPU configuration); the line also carries "c4_single_gpu", the C4 mesh
-                   below on this one GPU (the strong-scaling base of the N>1 lines).
+                   below on this one GPU (the strong-scaling base of the N>1 lines), and
+                   "c3_single_gpu", configs[2] (dg25N7L3: N=7, 3 layers, 25x25 elements).
   N>1   dg316L3 -- configs[3] (C4), the double gyre at 316x316 = 99,856 elements, N=4,
                    3 layers, dt=40 s, dt_btp=2 s, split over the N GPUs (strong scaling:
                    rank grid 2x1, 2x2, 4x2 of 158x316 / 158x158 / 79x158 element blocks).
@@ -118,14 +119,15 @@ def cpu_baseline(case, steps: int, cores: int):
             "sample": sample + f", {steps} baroclinic steps of the C restatement (oracle/hnumo_oracle.c, -O2), {t:.2f} s"}
 
 
-def c4_single_gpu(steps: int = 3):
-    """The C4 mesh (dg316L3, 99,856 elements) on this one GPU: the base of the N>1 strong-scaling
-    lines (reported beside the N=1 configs[1] line)."""
+def single_gpu_line(cfg: str, workload: str, steps: int = 3):
+    """Another BASELINE config on this one GPU, reported beside the N=1 configs[1] line: the C4
+    mesh (dg316L3, 99,856 elements; the base of the N>1 strong-scaling lines) and C3 (dg25N7L3,
+    N=7)."""
     import torch
     from hnumo.case import build_case, make_config
     from hnumo.engine import Engine
     from hnumo.roofline import element_updates_per_step
-    case = build_case(make_config("dg316L3"), dense=False)
+    case = build_case(make_config(cfg), dense=False)
     eng = Engine(case)
     eng.set_resident(True)
     q, qb, qp = eng.state()
@@ -136,10 +138,11 @@ def c4_single_gpu(steps: int = 3):
     torch.cuda.synchronize()
     t = time.perf_counter() - t0
     k_ms = eng.time_stage_kernel(1)
+    path = eng.stage_path
     from hnumo.roofline import HBM_PEAK_GBS, stage_bytes
     eng.close()
     ach = stage_bytes(case) / (k_ms * 1e-3) / 1e9
-    return {"workload": "dg316L3 (C4: 316x316 elements, N=4, 3 layers) on 1 GPU, per-stage launches",
+    return {"workload": f"{workload} on 1 GPU, {path} stage path",
             "value": round(element_updates_per_step(case) * steps / t, 1), "unit": "element-updates/s",
             "steps": steps, "ms_per_step": round(1e3 * t / steps, 3),
             "stage_kernel_us": round(k_ms * 1e3, 2), "stage_kernel_frac": round(ach / HBM_PEAK_GBS, 4)}
@@ -158,7 +161,7 @@ def main():
     ap.add_argument("--cpu-cores", type=int, default=16,
                     help="MPI ranks (= host cores) of the reference CPU baseline (the GPU box's share is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-c4", action="store_true", help="N=1: skip the c4_single_gpu figure")
+    ap.add_argument("--no-c4", action="store_true", help="N=1: skip the c4_single_gpu / c3_single_gpu figures")
     ap.add_argument("--summation", default="reference", choices=["reference", "factored"],
                     help="stage summation order (hnumo_set_summation); only 'reference' meets the 1e-10 bar")
     args = ap.parse_args()
@@ -326,10 +329,12 @@ def main():
     }
     eng.close()
     if rank == 0 and world == 1 and not args.no_c4 and args.config is None:
-        try:
-            out["c4_single_gpu"] = c4_single_gpu()
-        except Exception as exc:  # pragma: no cover - diagnostic only
-            out["c4_single_gpu"] = {"error": f"{type(exc).__name__}: {exc}"}
+        for key, cfg, wl, n in [("c4_single_gpu", "dg316L3", "dg316L3 (C4: 316x316 elements, N=4, 3 layers)", 3),
+                                ("c3_single_gpu", "dg25N7L3", "dg25N7L3 (C3: 25x25 elements, N=7, 3 layers)", 5)]:
+            try:
+                out[key] = single_gpu_line(cfg, wl, n)
+            except Exception as exc:  # pragma: no cover - diagnostic only
+                out[key] = {"error": f"{type(exc).__name__}: {exc}"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ncores = max(1, min(args.cpu_cores, len(os.sched_getaffinity(0))))
         out["cpu_baseline"] = cpu_baseline(build_case(make_config(cfg_name)), args.cpu_steps, ncores)

@@ -22,6 +22,23 @@
 
 namespace hnumo {
 
+// Diagnostics (HNUMO_BCL_PROF builds only): per-block phase clocks of the element kernels,
+// [kernel][block][8]: marks 0..5 clock64 at the phase boundaries of thread 0, 6/7 wall clock
+// at its start / end (read by hnumo_bcl_prof; tools/bcl_profile.py)
+#ifndef HNUMO_BCL_PROF
+#define HNUMO_BCL_PROF 0
+#endif
+#if HNUMO_BCL_PROF
+__device__ unsigned long long g_bcl_prof[3][8192][8];
+#define BCL_MARK(kid, k) \
+  if (threadIdx.x == 0 && blockIdx.x < 8192) g_bcl_prof[kid][blockIdx.x][k] = clock64();
+#define BCL_WALL(kid, k) \
+  if (threadIdx.x == 0 && blockIdx.x < 8192) g_bcl_prof[kid][blockIdx.x][k] = wall_clock64();
+#else
+#define BCL_MARK(kid, k)
+#define BCL_WALL(kid, k)
+#endif
+
 #define QF(v, s, n, f, k) qf[((((size_t)(k) * F + (f)) * NGL + (n)) * 2 + (s)) * 3 + (v)]
 
 template <int NGL, int NQ>
@@ -574,6 +591,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     mass_elem_kernel(DevMesh m, const double *qp, const double *qacc, const double *fmass, double *q,
                      double *slmf, double *dpp, int *neg_flag) {
   constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BS;
+  BCL_MARK(0, 0) BCL_WALL(0, 6)
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
   __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
   __shared__ double s_q[MAXL][3][P];
@@ -599,6 +617,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     s_qm[c][t % Q] = m.qstat[(c < 4 ? QS_EX + c : QS_W) * (size_t)npq + (size_t)e * Q + t % Q];
   }
   __syncthreads();
+  BCL_MARK(0, 1)
   for (int q = tid; q < Q; q += BS) {
     const int iq = q % NQ, jq = q / NQ;
     const size_t Iq = (size_t)e * Q + q;
@@ -628,6 +647,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     slmf[1 * (size_t)npq + Iq] = sv;
   }
   __syncthreads();
+  BCL_MARK(0, 2)
   for (int t = tid; t < L * P; t += BS) {
     const int k = t / P, p = t % P, i = p % NGL, j = p / NGL;
     double acc = weak_div<NGL, NQ>(s_psiq, s_dpsiq, s_qm[0], s_qm[1], s_qm[2], s_qm[3], s_qm[4], s_f[k][0], s_f[k][1],
@@ -641,6 +661,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     s_adv[k][p] = v;
   }
   __syncthreads();
+  BCL_MARK(0, 3)
   for (int p = tid; p < P; p += BS) {
     const size_t I = (size_t)e * P + p;
     double sum = 0.0;
@@ -648,6 +669,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     double ope = sum / m.nstat[NS_PB * (size_t)npoin + I];
     for (int k = 0; k < L; k++) dpp[(size_t)k * npoin + I] = s_adv[k][p] / ope;
   }
+  BCL_MARK(0, 5) BCL_WALL(0, 7)
 }
 
 // ============================================== consistency: element update
@@ -659,6 +681,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     cons_elem_kernel(DevMesh m, const double *dpp, const double *qacc, const double *slmf, const double *fcons,
                      double *q, double *qp_out, int finalize_dp) {
   constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BS;
+  BCL_MARK(1, 0) BCL_WALL(1, 6)
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
   __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
   __shared__ double s_d[MAXL][P];
@@ -681,6 +704,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     s_qm[c][t % Q] = m.qstat[(c < 4 ? QS_EX + c : QS_W) * (size_t)npq + (size_t)e * Q + t % Q];
   }
   __syncthreads();
+  BCL_MARK(1, 1)
   for (int q = tid; q < Q; q += BS) {
     const int iq = q % NQ, jq = q / NQ;
     const size_t Iq = (size_t)e * Q + q;
@@ -705,6 +729,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     }
   }
   __syncthreads();
+  BCL_MARK(1, 3)
   for (int t = tid; t < L * P; t += BS) {
     const int k = t / P, p = t % P, i = p % NGL, j = p / NGL;
     double acc = weak_div<NGL, NQ>(s_psiq, s_dpsiq, s_qm[0], s_qm[1], s_qm[2], s_qm[3], s_qm[4], s_f[k][0], s_f[k][1],
@@ -717,6 +742,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
   }
   if (!finalize_dp) return;
   __syncthreads();
+  BCL_MARK(1, 4)
   for (int p = tid; p < P; p += BS) {
     const size_t I = (size_t)e * P + p;
     double sum = 0.0;
@@ -724,6 +750,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     double ope = sum / m.nstat[NS_PB * (size_t)npoin + I];
     for (int k = 0; k < L; k++) qp_out[((size_t)k * npoin + I) * 3] = s_new[k][p] / ope;
   }
+  BCL_MARK(1, 5) BCL_WALL(1, 7)
 }
 
 // ========================================== layer momentum: face kernel
@@ -1026,6 +1053,7 @@ __global__ void __launch_bounds__(256, 3)
   constexpr int P = MomCfg<NGL, NQ>::P, Q = MomCfg<NGL, NQ>::Q, BS = MomCfg<NGL, NQ>::BS;
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
   const double g = m.gravity, eps1 = 1.0e-20;
+  BCL_MARK(2, 0) BCL_WALL(2, 6)
   __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
   __shared__ double s_qp[MAXL][3][P], s_qm2[MAXL][2][P], s_z[MAXL + 1][P];
   __shared__ double s_qm[5][Q];            // e_x, e_y, n_x, n_y, w at quad points
@@ -1085,6 +1113,7 @@ __global__ void __launch_bounds__(256, 3)
     s_nm[c][t % P] = m.nstat[(c < 4 ? NS_EX + c : NS_W) * (size_t)npoin + (size_t)e * P + t % P];
   }
   __syncthreads();
+  BCL_MARK(2, 1)
 
   // ---- 1: per (layer, quad point) interpolations of dp', u', v', u*dp, v*dp (reference
   //      order: PSIH(n,mm,iq,jq) over mm outer, n inner); per node the layer interfaces
@@ -1140,6 +1169,7 @@ __global__ void __launch_bounds__(256, 3)
     }
   }
   __syncthreads();
+  BCL_MARK(2, 2)
 
   // ---- 2: per quad point the layer coupling (mod_create_rhs_mlswe.F90:326-400);
   //      alongside, per (layer, component, node) the LDG Laplacian (mod_laplacian_quad.F90:
@@ -1276,6 +1306,7 @@ __global__ void __launch_bounds__(256, 3)
     }
   }
   __syncthreads();
+  BCL_MARK(2, 3)
 
   // ---- 3: weak forms, one thread per (layer, output, node), reference accumulation order
   //      (create_rhs_dynamics_volume_layers :401-456, then Apply_layers_fluxes :778-817)
@@ -1302,6 +1333,7 @@ __global__ void __launch_bounds__(256, 3)
     s_r[k][o][p] = acc;
   }
   __syncthreads();
+  BCL_MARK(2, 4)
 
   // ---- 4: per node: rhs_mom and q_df_temp = q + dt*rhs_mom (mod_splitting.F90:134-137 /
   //      :242-245), kept in s_r[k][0..1].  With ad_mlswe > 0 also the shear-stress input
@@ -1568,6 +1600,7 @@ __global__ void __launch_bounds__(256, 3)
       o[2] = uv[k][1] - b4 / b1;
     }
   }
+  BCL_MARK(2, 5) BCL_WALL(2, 7)
 }
 
 #define HNUMO_INSTANTIATE_BCL(NGL, NQ)                                                                              \

@@ -1,0 +1,41 @@
+"""Phase clocks of the baroclinic element kernels (mass_elem, cons_elem, mom_elem) from an
+HNUMO_BCL_PROF=1 build (diagnostics).  Usage (GPU): HNUMO_LIB=<prof .so> python tools/bcl_profile.py [cfg]"""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "h-numo_amd"))
+import numpy as np  # noqa: E402
+from hnumo.case import build_case, make_config  # noqa: E402
+from hnumo.engine import Engine, lib  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else "dg25L3"
+case = build_case(make_config(cfg), dense=False)
+eng = Engine(case)
+eng.set_resident(True)
+q, qb, qp = eng.state()
+for _ in range(2):
+    eng.ti_rk_bcl(q, qb, qp)
+buf = np.zeros(3 * 8192 * 8, dtype=np.uint64)
+L = lib()
+L.hnumo_bcl_prof.argtypes = [ctypes.c_void_p, ctypes.c_int]
+assert L.hnumo_bcl_prof(buf.ctypes.data, buf.size) == 0
+E = case.scalars["nelem"]
+pr = buf.reshape(3, 8192, 8)[:, :E].astype(np.int64)
+names = {0: ("mass_elem", ["loads", "quad", "node", "-", "final"]),
+         1: ("cons_elem", ["loads", "-", "quad", "node", "final"]),
+         2: ("mom_elem", ["loads", "ph1 interp", "ph2 couple+lap", "ph3 weak", "ph4 tail"])}
+for k, (nm, ph) in names.items():
+    a = pr[k]
+    tot = a[:, 5] - a[:, 0]
+    w0, w1 = a[:, 6], a[:, 7]
+    print(f"{nm}: block clocks mean {tot.mean():.0f} max {tot.max():.0f}; wall (100 MHz) start spread "
+          f"{(w0.max() - w0.min())}, block span mean {(w1 - w0).mean():.0f}, kernel span {(w1.max() - w0.min())}")
+    prev = a[:, 0]
+    for i, p in enumerate(ph):
+        cur = a[:, i + 1]
+        if p != "-" and (cur > 0).all():
+            d = cur - prev
+            print(f"    {p:16s} mean {d.mean():8.0f}  max {d.max():8.0f}")
+            prev = cur
+eng.close()
