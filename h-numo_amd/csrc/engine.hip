@@ -244,7 +244,7 @@ struct Launch {
   static void mass(hnumo_engine *e, const double *qp, const double *qf, double *q) {
     hipLaunchKernelGGL((mass_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
                        e->fmass, e->slmf_face);
-    hipLaunchKernelGGL((mass_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(BSE), 0, e->stream, e->m, qp,
+    hipLaunchKernelGGL((mass_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(Blk<NGL, NQ>::BSW), 0, e->stream, e->m, qp,
                        e->qacc, e->fmass, q, e->slmf, e->dpp, e->neg_flag);
   }
   static void cons(hnumo_engine *e, double *q, double *qp_out, int finalize_dp) {
@@ -256,7 +256,7 @@ struct Launch {
         hipLaunchKernelGGL((cons_flux_proc_kernel<NQ>), dim3((e->NS * NQ + 63) / 64), dim3(64), 0, e->stream, e->m,
                          e->cdef, e->d_sface, e->NS, e->fcons);
     }
-    hipLaunchKernelGGL((cons_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(BSE), 0, e->stream, e->m, e->dpp,
+    hipLaunchKernelGGL((cons_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(Blk<NGL, NQ>::BSW), 0, e->stream, e->m, e->dpp,
                        e->qacc, e->slmf, e->fcons, q, qp_out, finalize_dp);
   }
   static void momentum(hnumo_engine *e, const double *qf, const double *qp_in, const double *qb, double *q,

@@ -41,10 +41,6 @@ __device__ unsigned long long g_bcl_prof[3][8192][8];
 
 #define QF(v, s, n, f, k) qf[((((size_t)(k) * F + (f)) * NGL + (n)) * 2 + (s)) * 3 + (v)]
 
-template <int NGL, int NQ>
-struct Blk {
-  static constexpr int P = NGL * NGL, Q = NQ * NQ, BS = ((Q + 63) / 64) * 64;
-};
 
 __device__ __forceinline__ double dmin(double a, double b) { return a < b ? a : (b < a ? b : a); }
 __device__ __forceinline__ double dmax(double a, double b) { return a > b ? a : (b > a ? b : a); }
@@ -69,34 +65,105 @@ __device__ __forceinline__ void load_basis(const DevMesh &m, double *s_psiq, dou
 #define HE_DF(n, m, i, j) (s_dpsi[(n)*NGL + (i)] * s_psi[(m)*NGL + (j)])
 #define HN_DF(n, m, i, j) (s_psi[(n)*NGL + (i)] * s_dpsi[(m)*NGL + (j)])
 
-// sum_q w(q)*(dpsidx(p,q)*fx(q) + dpsidy(p,q)*fy(q)) accumulated onto acc in quad order
-// (the weak-form divergence of mod_create_rhs_mlswe.F90:866-868 / :911-913)
-// (the thread's basis row psiq(i,:), dpsiq(i,:) in registers; a quad row per iteration, its
-// loads independent of the chain, so only the adds are serial)
-template <int NGL, int NQ>
-__device__ __forceinline__ double weak_div(const double *s_psiq, const double *s_dpsiq, const double *qm0,
-                                           const double *qm1, const double *qm2, const double *qm3, const double *w,
-                                           const double *fx, const double *fy, int i, int j, double acc) {
-  double pi[NQ], dpi[NQ];
-#pragma unroll
-  for (int iq = 0; iq < NQ; iq++) {
-    pi[iq] = s_psiq[i * NQ + iq];
-    dpi[iq] = s_dpsiq[i * NQ + iq];
+// Workgroup barrier for LDS hand-offs only (no release fence: outstanding global stores of the
+// wave are not drained, unlike __syncthreads())
+#define BCL_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+
+// Term buffers of ordered_quad_sums: chunks of RC quad rows (RC | NQ) for NT chains, two buffers
+// when they fit the budget (doubles), else one
+template <int NQ, int NT, int BUDGET>
+struct QSumCfg {
+  static constexpr int rc_pick(int nbuf) {
+    for (int rc = NQ; rc >= 1; rc--)
+      if (NQ % rc == 0 && nbuf * NT * ((rc * NQ) | 1) <= BUDGET) return rc;
+    return 0;
   }
-#pragma unroll 1
-  for (int jq = 0; jq < NQ; jq++) {
-    const double pj = s_psiq[j * NQ + jq], dpj = s_dpsiq[j * NQ + jq];
+  static constexpr int NBUF = rc_pick(2) ? 2 : 1;
+  static constexpr int RC = rc_pick(NBUF) ? rc_pick(NBUF) : 1;
+  static constexpr int QC = RC * NQ, QCP = QC | 1, NCH = NQ / RC;
+  static constexpr int SIZE = NBUF * NT * QCP;
+};
+
+// Reference-order quad-point sums of nt <= NT chains, chain c summed by thread c:
+//   acc_c = sum over q = 0..Q-1, in order, of T(c, q).
+// The terms of a chunk of RC quad rows are evaluated in parallel into LDS -- thread t evaluates
+// quad row r = t / nt of chain c = t % nt, row(c, jq, dst) writing T(c, jq*NQ + iq) for iq =
+// 0..NQ-1 to dst[iq] (so a thread keeps one chain, and its per-chain values can live in its
+// registers) -- and thread c adds them in quad order (with two buffers, while the next chunk's
+// terms are evaluated): the same terms in the same order as one thread forming and adding each
+// itself, so the same bits, but the dependent chain is one add per quad point instead of the
+// whole term, and the terms of a row are independent.  Every thread must call it.
+template <int NQ, int NT, int BS, class CFG, class RowF>
+__device__ __forceinline__ double ordered_quad_sums(double *tb, int tid, int nt, RowF &&row) {
+  constexpr int QCP = CFG::QCP, NCH = CFG::NCH, NBUF = CFG::NBUF, RC = CFG::RC;
+  double acc = 0.0;
+  auto eval = [&](int k) {
+    double *T = tb + (NBUF == 2 ? (k & 1) * NT * QCP : 0);
+    for (int t = tid; t < nt * RC; t += BS) {
+      const int r = t / nt, c = t - r * nt;
+      row(c, k * RC + r, T + c * QCP + r * NQ);
+    }
+  };
+  auto add = [&](int k) {
+    if (tid < nt) {
+      const double *T = tb + (NBUF == 2 ? (k & 1) * NT * QCP : 0) + tid * QCP;
 #pragma unroll
-    for (int iq = 0; iq < NQ; iq++) {
-      const int q = jq * NQ + iq;
-      const double h_e = dpi[iq] * pj, h_n = pi[iq] * dpj;  // HE(i,j,iq,jq), HN(i,j,iq,jq)
-      const double dhdx = h_e * qm0[q] + h_n * qm2[q];
-      const double dhdy = h_e * qm1[q] + h_n * qm3[q];
-      acc = acc + w[q] * (dhdx * fx[q] + dhdy * fy[q]);
+      for (int r = 0; r < RC; r++) {
+        double tv[NQ];
+#pragma unroll
+        for (int i = 0; i < NQ; i++) tv[i] = T[r * NQ + i];
+        asm volatile("" ::: "memory");  // the row's loads before its adds
+#pragma unroll
+        for (int i = 0; i < NQ; i++) acc = acc + tv[i];
+      }
+    }
+  };
+  if constexpr (NBUF == 2) {
+#pragma unroll 1
+    for (int k = 0; k <= NCH; k++) {
+      if (k < NCH) eval(k);
+      if (k >= 1) add(k - 1);
+      BCL_LDS_BARRIER();
+    }
+  } else {
+#pragma unroll 1
+    for (int k = 0; k < NCH; k++) {
+      eval(k);
+      BCL_LDS_BARRIER();
+      add(k);
+      BCL_LDS_BARRIER();
     }
   }
   return acc;
 }
+
+// One quad row jq of the weak-form divergence terms w(q)*(dpsidx(p,q)*fx(q) + dpsidy(p,q)*fy(q))
+// (mod_create_rhs_mlswe.F90:866-868 / :911-913) for node
+// p = (i, j), with the node's basis row psiq(i,:), dpsiq(i,:) in registers (pi, dpi)
+template <int NGL, int NQ>
+__device__ __forceinline__ void weak_div_row(const double *s_psiq, const double *s_dpsiq, const double *pi,
+                                             const double *dpi, const double *qm0, const double *qm1,
+                                             const double *qm2, const double *qm3, const double *w, const double *fx,
+                                             const double *fy, int j, int jq, double *dst) {
+  const double pj = s_psiq[j * NQ + jq], dpj = s_dpsiq[j * NQ + jq];
+  const int q0 = jq * NQ;
+#pragma unroll
+  for (int iq = 0; iq < NQ; iq++) {
+    const int q = q0 + iq;
+    const double h_e = dpi[iq] * pj, h_n = pi[iq] * dpj;
+    const double dhdx = h_e * qm0[q] + h_n * qm2[q];
+    const double dhdy = h_e * qm1[q] + h_n * qm3[q];
+    dst[iq] = w[q] * (dhdx * fx[q] + dhdy * fy[q]);
+  }
+}
+
+template <int NGL, int NQ>
+struct Blk {
+  static constexpr int P = NGL * NGL, Q = NQ * NQ, BS = ((Q + 63) / 64) * 64;
+  // mass_elem / cons_elem: 256 threads at least (the quad-point sums' row tasks, ordered_quad_sums)
+  static constexpr int BSW = BS < 256 ? 256 : BS;
+  using QS = QSumCfg<NQ, MAXL * P, 34 * 1024 / 8>;
+};
 
 // sum over the element's nodes of PSIH(n,mm,iq,jq)*x(v, mm*NGL+n), mm outer, n inner (the
 // reference's interpolation order), for NV components x[v*stride + node]; pa/pb = the thread's
@@ -116,26 +183,40 @@ __device__ __forceinline__ void interp_q(const double *pa, const double *pb, con
     }
 }
 
-// Face terms of one face onto node p: acc -/+ (wq*hi)*flux(iq), quad order (left: -, right: +),
-// from the element's own face data staged in LDS: s_fw[lf][NQ] (w of the face quad points)
-// and s_fx[lf][NQ] (the flux), lf = the element's local face.
-template <int NGL, int NQ>
-__device__ __forceinline__ double face_terms_lds(const double *s_psiq, const int *s_map, const int *s_side,
-                                                 const double *s_fw, const double *s_fx, int p, double acc) {
-  // (not unrolled: a node lies on at most two faces, and the unrolled search with its loads
-  // hoisted costs hundreds of registers)
-#pragma unroll 1
-  for (int lf = 0; lf < 4; lf++)
-#pragma unroll 1
-    for (int n = 0; n < NGL; n++) {
-      if (s_map[lf * NGL + n] != p) continue;
-      const bool left = s_side[lf] == 0;
+// Face terms onto node p: acc -/+ (wq*hi)*flux(iq) in quad order (left: -, right: +), faces in
+// the order of the element's local faces, from the element's own face data staged in LDS:
+// s_fw[lf][NQ] (w of the face quad points) and s_fx[lf][NQ] (the flux).  node_faces finds the
+// (at most two) face points lf*NGL + n at node p, ascending (-1: none), once per thread (a search
+// loop per sum diverged into one masked pass per face point of the element) ...
+template <int NGL>
+__device__ __forceinline__ void node_faces(const int *s_map, int p, int &r0, int &r1) {
+  int m_[4 * NGL];
 #pragma unroll
-      for (int iq = 0; iq < NQ; iq++) {
-        const double c = s_fw[lf * NQ + iq] * s_psiq[n * NQ + iq] * s_fx[lf * NQ + iq];
-        acc = left ? acc - c : acc + c;
-      }
+  for (int x = 0; x < 4 * NGL; x++) m_[x] = s_map[x];
+  r0 = r1 = -1;
+#pragma unroll
+  for (int x = 4 * NGL - 1; x >= 0; x--)
+    if (m_[x] == p) {
+      r1 = r0;
+      r0 = x;
     }
+}
+// ... and face_terms_at adds their terms, each face's loads before its chain
+template <int NGL, int NQ>
+__device__ __forceinline__ double face_terms_at(const double *s_psiq, const int *s_side, const double *s_fw,
+                                                const double *s_fx, int r0, int r1, double acc) {
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int r = h ? r1 : r0;
+    if (r < 0) continue;
+    const int lf = r / NGL, n = r - lf * NGL;
+    const bool left = s_side[lf] == 0;
+    double c[NQ];
+#pragma unroll
+    for (int iq = 0; iq < NQ; iq++) c[iq] = s_fw[lf * NQ + iq] * s_psiq[n * NQ + iq] * s_fx[lf * NQ + iq];
+#pragma unroll
+    for (int iq = 0; iq < NQ; iq++) acc = left ? acc - c[iq] : acc + c[iq];
+  }
   return acc;
 }
 
@@ -587,10 +668,12 @@ __global__ void face_unpack_kernel(double *base, const double *buf, const int *s
 // (:74-76), q(1) += dt*dp_advec and the negativity check (mod_splitting.F90:69-78 /
 // :224-232), then dp' = q(1)/(sum_k q(1)/pb') for the consistency step (:350-353).
 template <int NGL, int NQ>
-__global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
+__global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     mass_elem_kernel(DevMesh m, const double *qp, const double *qacc, const double *fmass, double *q,
                      double *slmf, double *dpp, int *neg_flag) {
-  constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BS;
+  constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BSW;
+  using QS = typename Blk<NGL, NQ>::QS;
+  static_assert(MAXL * P <= BS, "one quad-point sum per thread");
   BCL_MARK(0, 0) BCL_WALL(0, 6)
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
   __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
@@ -599,6 +682,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
   __shared__ double s_f[MAXL][2][Q];        // udp, vdp per layer
   __shared__ double s_adv[MAXL][P];
   __shared__ double s_fw[4 * NQ], s_fx[MAXL][4 * NQ];  // face weights, layer mass fluxes of the 4 faces
+  __shared__ double s_tb[QS::SIZE];                    // quad-sum term buffers
   __shared__ int s_map[4 * NGL], s_face[4], s_side[4];
   load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
   if (tid < 4) {
@@ -648,20 +732,41 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
   }
   __syncthreads();
   BCL_MARK(0, 2)
-  for (int t = tid; t < L * P; t += BS) {
-    const int k = t / P, p = t % P, i = p % NGL, j = p / NGL;
-    double acc = weak_div<NGL, NQ>(s_psiq, s_dpsiq, s_qm[0], s_qm[1], s_qm[2], s_qm[3], s_qm[4], s_f[k][0], s_f[k][1],
-                                   i, j, 0.0);
-    acc = face_terms_lds<NGL, NQ>(s_psiq, s_map, s_side, s_fw, s_fx[k], p, acc);
+  {
+    // thread t: layer k, node p -- the weak-form divergence (ordered_quad_sums), then the faces
+    const int t = tid, k = t / P, p = t % P;
     const size_t I = (size_t)e * P + p;
-    double adv = m.nstat[NS_MINV * (size_t)npoin + I] * acc;
-    double v = q[((size_t)k * npoin + I) * 3] + m.dt * adv;
-    if (v < 0.0) atomicOr(neg_flag, 1);
-    q[((size_t)k * npoin + I) * 3] = v;
-    s_adv[k][p] = v;
+    double r_mi = 0.0, r_q = 0.0;
+    if (t < L * P) {
+      r_mi = m.nstat[NS_MINV * (size_t)npoin + I];
+      r_q = q[((size_t)k * npoin + I) * 3];
+    }
+    // this thread's chain in ordered_quad_sums' row tasks: tid % (L*P)
+    const int cr = tid % (L * P), kr = cr / P, pr = cr % P, ir = pr % NGL, jr = pr / NGL;
+    double pi[NQ], dpi[NQ];
+#pragma unroll
+    for (int iq = 0; iq < NQ; iq++) {
+      pi[iq] = s_psiq[ir * NQ + iq];
+      dpi[iq] = s_dpsiq[ir * NQ + iq];
+    }
+    double acc = ordered_quad_sums<NQ, MAXL * P, BS, QS>(s_tb, tid, L * P, [&](int, int jq, double *dst) {
+      weak_div_row<NGL, NQ>(s_psiq, s_dpsiq, pi, dpi, s_qm[0], s_qm[1], s_qm[2], s_qm[3], s_qm[4], s_f[kr][0],
+                            s_f[kr][1], jr, jq, dst);
+    });
+    BCL_MARK(0, 3)
+    if (t < L * P) {
+      int r0, r1;
+      node_faces<NGL>(s_map, p, r0, r1);
+      acc = face_terms_at<NGL, NQ>(s_psiq, s_side, s_fw, s_fx[k], r0, r1, acc);
+      double adv = r_mi * acc;
+      double v = r_q + m.dt * adv;
+      if (v < 0.0) atomicOr(neg_flag, 1);
+      q[((size_t)k * npoin + I) * 3] = v;
+      s_adv[k][p] = v;
+    }
   }
   __syncthreads();
-  BCL_MARK(0, 3)
+  BCL_MARK(0, 4)
   for (int p = tid; p < P; p += BS) {
     const size_t I = (size_t)e * P + p;
     double sum = 0.0;
@@ -677,10 +782,12 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
 // q(1) += dt*massinv*dp_advec (mod_splitting.F90:362-364).  finalize_dp (thickness): also
 // qprime(1,:,k) = q(1,:,k)/(sum_k q(1)/pb') (mod_splitting.F90:84-87).
 template <int NGL, int NQ>
-__global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
+__global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     cons_elem_kernel(DevMesh m, const double *dpp, const double *qacc, const double *slmf, const double *fcons,
                      double *q, double *qp_out, int finalize_dp) {
-  constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BS;
+  constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BSW;
+  using QS = typename Blk<NGL, NQ>::QS;
+  static_assert(MAXL * P <= BS, "one quad-point sum per thread");
   BCL_MARK(1, 0) BCL_WALL(1, 6)
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
   __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
@@ -689,6 +796,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
   __shared__ double s_f[MAXL][2][Q];
   __shared__ double s_new[MAXL][P];
   __shared__ double s_fw[4 * NQ], s_fx[MAXL][4 * NQ];  // face weights, consistency fluxes of the 4 faces
+  __shared__ double s_tb[QS::SIZE];                    // quad-sum term buffers
   __shared__ int s_map[4 * NGL], s_face[4], s_side[4];
   load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
   if (tid < 4) {
@@ -730,15 +838,35 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
   }
   __syncthreads();
   BCL_MARK(1, 3)
-  for (int t = tid; t < L * P; t += BS) {
-    const int k = t / P, p = t % P, i = p % NGL, j = p / NGL;
-    double acc = weak_div<NGL, NQ>(s_psiq, s_dpsiq, s_qm[0], s_qm[1], s_qm[2], s_qm[3], s_qm[4], s_f[k][0], s_f[k][1],
-                                   i, j, 0.0);
-    acc = face_terms_lds<NGL, NQ>(s_psiq, s_map, s_side, s_fw, s_fx[k], p, acc);
+  {
+    // thread t: layer k, node p -- the weak-form divergence (ordered_quad_sums), then the faces
+    const int t = tid, k = t / P, p = t % P;
     const size_t I = (size_t)e * P + p;
-    double v = q[((size_t)k * npoin + I) * 3] + m.dt * m.nstat[NS_MINV * (size_t)npoin + I] * acc;
-    q[((size_t)k * npoin + I) * 3] = v;
-    s_new[k][p] = v;
+    double r_mi = 0.0, r_q = 0.0;
+    if (t < L * P) {
+      r_mi = m.nstat[NS_MINV * (size_t)npoin + I];
+      r_q = q[((size_t)k * npoin + I) * 3];
+    }
+    // this thread's chain in ordered_quad_sums' row tasks: tid % (L*P)
+    const int cr = tid % (L * P), kr = cr / P, pr = cr % P, ir = pr % NGL, jr = pr / NGL;
+    double pi[NQ], dpi[NQ];
+#pragma unroll
+    for (int iq = 0; iq < NQ; iq++) {
+      pi[iq] = s_psiq[ir * NQ + iq];
+      dpi[iq] = s_dpsiq[ir * NQ + iq];
+    }
+    double acc = ordered_quad_sums<NQ, MAXL * P, BS, QS>(s_tb, tid, L * P, [&](int, int jq, double *dst) {
+      weak_div_row<NGL, NQ>(s_psiq, s_dpsiq, pi, dpi, s_qm[0], s_qm[1], s_qm[2], s_qm[3], s_qm[4], s_f[kr][0],
+                            s_f[kr][1], jr, jq, dst);
+    });
+    if (t < L * P) {
+      int r0, r1;
+      node_faces<NGL>(s_map, p, r0, r1);
+      acc = face_terms_at<NGL, NQ>(s_psiq, s_side, s_fw, s_fx[k], r0, r1, acc);
+      double v = r_q + m.dt * r_mi * acc;
+      q[((size_t)k * npoin + I) * 3] = v;
+      s_new[k][p] = v;
+    }
   }
   if (!finalize_dp) return;
   __syncthreads();
@@ -1058,7 +1186,12 @@ __global__ void __launch_bounds__(256, 3)
   __shared__ double s_qp[MAXL][3][P], s_qm2[MAXL][2][P], s_z[MAXL + 1][P];
   __shared__ double s_qm[5][Q];            // e_x, e_y, n_x, n_y, w at quad points
   __shared__ double s_nm[5][P];            // e_x, e_y, n_x, n_y, w at nodes
-  __shared__ double s_iv[MAXL][5][Q];      // interpolated dp', u', v', u*dp, v*dp per layer
+  // interpolated dp', u', v', u*dp, v*dp per layer (phases 1-2); then the weak forms' term buffers
+  using QS = QSumCfg<NQ, MAXL * 2 * P, 2700>;
+  constexpr bool QSUM = MAXL * 2 * P <= BS;  // one weak-form sum per thread (ordered_quad_sums)
+  constexpr int IVTB = (QSUM && QS::SIZE > MAXL * 5 * Q) ? QS::SIZE : MAXL * 5 * Q;
+  __shared__ double s_ivtb[IVTB];
+  double(*s_iv)[5][Q] = reinterpret_cast<double(*)[5][Q]>(s_ivtb);
   __shared__ double s_G[MAXL][6][Q];       // source_x, Hq+uu, uv, source_y, vu, Hq+vv
   __shared__ double s_qq[MAXL][4][P];      // LDG volume fluxes per layer
   __shared__ double s_r[MAXL][4][P];       // rhs_mom(2) and lap(2) per layer
@@ -1294,14 +1427,15 @@ __global__ void __launch_bounds__(256, 3)
         const double dy = both ? ey_ + ny_ : (mid ? ey_ : ny_);
         acc = acc - s_nm[4][sn] * (dx * s_qq[k][2 * c][sn] + dy * s_qq[k][2 * c + 1][sn]);
       }
-#pragma unroll 1
-      for (int lf = 0; lf < 4; lf++)
-#pragma unroll 1
-        for (int n = 0; n < NGL; n++)
-          if (s_map[lf * NGL + n] == p) {
-            const double v = s_fl[k][c][lf * NGL + n];
-            acc = s_side[lf] == 0 ? acc + v : acc - v;
-          }
+      int r0, r1;
+      node_faces<NGL>(s_map, p, r0, r1);
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int r = h ? r1 : r0;
+        if (r < 0) continue;
+        const double v = s_fl[k][c][r];
+        acc = s_side[r / NGL] == 0 ? acc + v : acc - v;
+      }
       s_r[k][2 + c][p] = acc;
     }
   }
@@ -1310,6 +1444,37 @@ __global__ void __launch_bounds__(256, 3)
 
   // ---- 3: weak forms, one thread per (layer, output, node), reference accumulation order
   //      (create_rhs_dynamics_volume_layers :401-456, then Apply_layers_fluxes :778-817)
+  if constexpr (QSUM) {
+    // thread t: the chain (k, o, p) below, its terms evaluated in parallel (ordered_quad_sums)
+    const int t = tid, k = t / (2 * P), o = (t / P) % 2, p = t % P;
+    // this thread's chain in ordered_quad_sums' row tasks: tid % (2*L*P)
+    const int cr = tid % (L * 2 * P), kr = cr / (2 * P), orr = (cr / P) % 2, pr = cr % P, ir = pr % NGL,
+              jr = pr / NGL;
+    const double *G0 = s_G[kr][3 * orr], *G1 = s_G[kr][3 * orr + 1], *G2 = s_G[kr][3 * orr + 2];
+    double pi[NQ], dpi[NQ];
+#pragma unroll
+    for (int iq = 0; iq < NQ; iq++) {
+      pi[iq] = s_psiq[ir * NQ + iq];
+      dpi[iq] = s_dpsiq[ir * NQ + iq];
+    }
+    double acc = ordered_quad_sums<NQ, MAXL * 2 * P, BS, QS>(s_ivtb, tid, L * 2 * P, [&](int, int jq, double *dst) {
+      const double pj = s_psiq[jr * NQ + jq], dpj = s_dpsiq[jr * NQ + jq];
+#pragma unroll
+      for (int iq = 0; iq < NQ; iq++) {
+        const int qd = jq * NQ + iq;
+        const double hi = pi[iq] * pj, h_e = dpi[iq] * pj, h_n = pi[iq] * dpj;
+        const double dhdx = h_e * s_qm[0][qd] + h_n * s_qm[2][qd];
+        const double dhdy = h_e * s_qm[1][qd] + h_n * s_qm[3][qd];
+        dst[iq] = s_qm[4][qd] * (hi * G0[qd] + dhdx * G1[qd] + dhdy * G2[qd]);
+      }
+    });
+    if (t < L * 2 * P) {
+      int r0, r1;
+      node_faces<NGL>(s_map, p, r0, r1);
+      acc = face_terms_at<NGL, NQ>(s_psiq, s_side, s_fw, s_fm[k][o], r0, r1, acc);
+      s_r[k][o][p] = acc;
+    }
+  } else
   for (int t = tid; t < L * 2 * P; t += BS) {
     const int k = t / (2 * P), o = (t / P) % 2, p = t % P, i = p % NGL, j = p / NGL;
     const double *G0 = s_G[k][3 * o], *G1 = s_G[k][3 * o + 1], *G2 = s_G[k][3 * o + 2];
@@ -1329,7 +1494,9 @@ __global__ void __launch_bounds__(256, 3)
         acc = acc + term;
       }
     }
-    acc = face_terms_lds<NGL, NQ>(s_psiq, s_map, s_side, s_fw, s_fm[k][o], p, acc);
+    int r0, r1;
+    node_faces<NGL>(s_map, p, r0, r1);
+    acc = face_terms_at<NGL, NQ>(s_psiq, s_side, s_fw, s_fm[k][o], r0, r1, acc);
     s_r[k][o][p] = acc;
   }
   __syncthreads();

@@ -22,7 +22,7 @@ L.hnumo_bcl_prof.argtypes = [ctypes.c_void_p, ctypes.c_int]
 assert L.hnumo_bcl_prof(buf.ctypes.data, buf.size) == 0
 E = case.scalars["nelem"]
 pr = buf.reshape(3, 8192, 8)[:, :E].astype(np.int64)
-names = {0: ("mass_elem", ["loads", "quad", "node", "-", "final"]),
+names = {0: ("mass_elem", ["loads", "quad", "node sums", "faces+store", "final"]),
          1: ("cons_elem", ["loads", "-", "quad", "node", "final"]),
          2: ("mom_elem", ["loads", "ph1 interp", "ph2 couple+lap", "ph3 weak", "ph4 tail"])}
 for k, (nm, ph) in names.items():
