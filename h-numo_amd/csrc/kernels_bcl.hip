@@ -69,7 +69,7 @@ __device__ __forceinline__ void load_basis(const DevMesh &m, double *s_psiq, dou
 // wave are not drained, unlike __syncthreads())
 #define BCL_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
-// Term buffers of ordered_quad_sums: chunks of RC quad rows (RC | NQ) for NT chains, two buffers
+// Term buffers of ordered_node_sums: chunks of RC quad rows (RC | NQ) for NT chains, two buffers
 // when they fit the budget (doubles), else one
 template <int NQ, int NT, int BUDGET>
 struct QSumCfg {
@@ -84,28 +84,31 @@ struct QSumCfg {
   static constexpr int SIZE = NBUF * NT * QCP;
 };
 
-// Reference-order quad-point sums of nt <= NT chains, chain c summed by thread c:
-//   acc_c = sum over q = 0..Q-1, in order, of T(c, q).
-// The terms of a chunk of RC quad rows are evaluated in parallel into LDS -- thread t evaluates
-// quad row r = t / nt of chain c = t % nt, row(c, jq, dst) writing T(c, jq*NQ + iq) for iq =
-// 0..NQ-1 to dst[iq] (so a thread keeps one chain, and its per-chain values can live in its
-// registers) -- and thread c adds them in quad order (with two buffers, while the next chunk's
-// terms are evaluated): the same terms in the same order as one thread forming and adding each
-// itself, so the same bits, but the dependent chain is one add per quad point instead of the
-// whole term, and the terms of a row are independent.  Every thread must call it.
-template <int NQ, int NT, int BS, class CFG, class RowF>
-__device__ __forceinline__ double ordered_quad_sums(double *tb, int tid, int nt, RowF &&row) {
-  constexpr int QCP = CFG::QCP, NCH = CFG::NCH, NBUF = CFG::NBUF, RC = CFG::RC;
+// Reference-order quad-point sums of the chains (p, c) -- p < NP nodes, c < nc <= CPN sums per
+// node -- chain p*CPN + c summed by thread p*CPN + c:
+//   acc = sum over q = 0..Q-1, in order, of T(p, c, q).
+// The terms of a chunk of RC quad rows are evaluated in parallel into LDS: task (p, quad point q of
+// the chunk) writes all nc terms of node p at q, eval(p, q, dst, stride) -> dst[c*stride] = T(p, c, q),
+// so the node's basis products and metric derivatives are formed once for its nc terms; the
+// summing threads add the chunk in quad order (with two buffers, while the next chunk's terms are
+// evaluated).  The same terms in the same order as one thread forming and adding each itself, so
+// the same bits, but the dependent chain is one add per quad point instead of the whole term (the
+// element kernels ran ~40k clocks per such sum with one wave per SIMD).  Every thread must call it.
+template <int NQ, int NP, int CPN, int BS, class CFG, class EvalF>
+__device__ __forceinline__ double ordered_node_sums(double *tb, int tid, int nc, EvalF &&eval) {
+  constexpr int NT = NP * CPN, QC = CFG::QC, QCP = CFG::QCP, NCH = CFG::NCH, NBUF = CFG::NBUF, RC = CFG::RC;
+  static_assert(NT <= BS, "one sum per thread");
   double acc = 0.0;
-  auto eval = [&](int k) {
+  const bool summer = tid < NT && tid % CPN < nc;
+  auto ev = [&](int k) {
     double *T = tb + (NBUF == 2 ? (k & 1) * NT * QCP : 0);
-    for (int t = tid; t < nt * RC; t += BS) {
-      const int r = t / nt, c = t - r * nt;
-      row(c, k * RC + r, T + c * QCP + r * NQ);
+    for (int t = tid; t < NP * QC; t += BS) {
+      const int p = t / QC, qi = t - p * QC;
+      eval(p, k * QC + qi, T + p * CPN * QCP + qi, QCP);
     }
   };
   auto add = [&](int k) {
-    if (tid < nt) {
+    if (summer) {
       const double *T = tb + (NBUF == 2 ? (k & 1) * NT * QCP : 0) + tid * QCP;
 #pragma unroll
       for (int r = 0; r < RC; r++) {
@@ -121,14 +124,14 @@ __device__ __forceinline__ double ordered_quad_sums(double *tb, int tid, int nt,
   if constexpr (NBUF == 2) {
 #pragma unroll 1
     for (int k = 0; k <= NCH; k++) {
-      if (k < NCH) eval(k);
+      if (k < NCH) ev(k);
       if (k >= 1) add(k - 1);
       BCL_LDS_BARRIER();
     }
   } else {
 #pragma unroll 1
     for (int k = 0; k < NCH; k++) {
-      eval(k);
+      ev(k);
       BCL_LDS_BARRIER();
       add(k);
       BCL_LDS_BARRIER();
@@ -137,32 +140,30 @@ __device__ __forceinline__ double ordered_quad_sums(double *tb, int tid, int nt,
   return acc;
 }
 
-// One quad row jq of the weak-form divergence terms w(q)*(dpsidx(p,q)*fx(q) + dpsidy(p,q)*fy(q))
-// (mod_create_rhs_mlswe.F90:866-868 / :911-913) for node
-// p = (i, j), with the node's basis row psiq(i,:), dpsiq(i,:) in registers (pi, dpi)
+// The weak-form divergence terms w(q)*(dpsidx(p,q)*fx_k(q) + dpsidy(p,q)*fy_k(q)) of the layers
+// k < L at node p, quad point q (mod_create_rhs_mlswe.F90:866-868 / :911-913), f[k][0..1][Q]
 template <int NGL, int NQ>
-__device__ __forceinline__ void weak_div_row(const double *s_psiq, const double *s_dpsiq, const double *pi,
-                                             const double *dpi, const double *qm0, const double *qm1,
-                                             const double *qm2, const double *qm3, const double *w, const double *fx,
-                                             const double *fy, int j, int jq, double *dst) {
-  const double pj = s_psiq[j * NQ + jq], dpj = s_dpsiq[j * NQ + jq];
-  const int q0 = jq * NQ;
+__device__ __forceinline__ void weak_div_terms(const double *s_psiq, const double *s_dpsiq, const double (*qm)[NQ * NQ],
+                                               const double (*f)[2][NQ * NQ], int L, int p, int q, double *dst,
+                                               int stride) {
+  const int i = p % NGL, j = p / NGL, iq = q % NQ, jq = q / NQ;
+  const double h_e = s_dpsiq[i * NQ + iq] * s_psiq[j * NQ + jq], h_n = s_psiq[i * NQ + iq] * s_dpsiq[j * NQ + jq];
+  const double dhdx = h_e * qm[0][q] + h_n * qm[2][q];
+  const double dhdy = h_e * qm[1][q] + h_n * qm[3][q];
+  const double w = qm[4][q];
 #pragma unroll
-  for (int iq = 0; iq < NQ; iq++) {
-    const int q = q0 + iq;
-    const double h_e = dpi[iq] * pj, h_n = pi[iq] * dpj;
-    const double dhdx = h_e * qm0[q] + h_n * qm2[q];
-    const double dhdy = h_e * qm1[q] + h_n * qm3[q];
-    dst[iq] = w[q] * (dhdx * fx[q] + dhdy * fy[q]);
+  for (int k = 0; k < MAXL; k++) {
+    if (k >= L) break;
+    dst[k * stride] = w * (dhdx * f[k][0][q] + dhdy * f[k][1][q]);
   }
 }
 
 template <int NGL, int NQ>
 struct Blk {
   static constexpr int P = NGL * NGL, Q = NQ * NQ, BS = ((Q + 63) / 64) * 64;
-  // mass_elem / cons_elem: 256 threads at least (the quad-point sums' row tasks, ordered_quad_sums)
+  // mass_elem / cons_elem: 256 threads at least (the quad-point sums, ordered_node_sums)
   static constexpr int BSW = BS < 256 ? 256 : BS;
-  using QS = QSumCfg<NQ, MAXL * P, 34 * 1024 / 8>;
+  using QS = QSumCfg<NQ, P * MAXL, 34 * 1024 / 8>;
 };
 
 // sum over the element's nodes of PSIH(n,mm,iq,jq)*x(v, mm*NGL+n), mm outer, n inner (the
@@ -733,28 +734,20 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   __syncthreads();
   BCL_MARK(0, 2)
   {
-    // thread t: layer k, node p -- the weak-form divergence (ordered_quad_sums), then the faces
-    const int t = tid, k = t / P, p = t % P;
+    // thread t: node p, layer k -- the weak-form divergence (ordered_node_sums), then the faces
+    const int t = tid, p = t / MAXL, k = t % MAXL;
+    const bool mine = t < P * MAXL && k < L;
     const size_t I = (size_t)e * P + p;
     double r_mi = 0.0, r_q = 0.0;
-    if (t < L * P) {
+    if (mine) {
       r_mi = m.nstat[NS_MINV * (size_t)npoin + I];
       r_q = q[((size_t)k * npoin + I) * 3];
     }
-    // this thread's chain in ordered_quad_sums' row tasks: tid % (L*P)
-    const int cr = tid % (L * P), kr = cr / P, pr = cr % P, ir = pr % NGL, jr = pr / NGL;
-    double pi[NQ], dpi[NQ];
-#pragma unroll
-    for (int iq = 0; iq < NQ; iq++) {
-      pi[iq] = s_psiq[ir * NQ + iq];
-      dpi[iq] = s_dpsiq[ir * NQ + iq];
-    }
-    double acc = ordered_quad_sums<NQ, MAXL * P, BS, QS>(s_tb, tid, L * P, [&](int, int jq, double *dst) {
-      weak_div_row<NGL, NQ>(s_psiq, s_dpsiq, pi, dpi, s_qm[0], s_qm[1], s_qm[2], s_qm[3], s_qm[4], s_f[kr][0],
-                            s_f[kr][1], jr, jq, dst);
+    double acc = ordered_node_sums<NQ, P, MAXL, BS, QS>(s_tb, tid, L, [&](int pp, int qd, double *dst, int st) {
+      weak_div_terms<NGL, NQ>(s_psiq, s_dpsiq, s_qm, s_f, L, pp, qd, dst, st);
     });
     BCL_MARK(0, 3)
-    if (t < L * P) {
+    if (mine) {
       int r0, r1;
       node_faces<NGL>(s_map, p, r0, r1);
       acc = face_terms_at<NGL, NQ>(s_psiq, s_side, s_fw, s_fx[k], r0, r1, acc);
@@ -839,27 +832,19 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   __syncthreads();
   BCL_MARK(1, 3)
   {
-    // thread t: layer k, node p -- the weak-form divergence (ordered_quad_sums), then the faces
-    const int t = tid, k = t / P, p = t % P;
+    // thread t: node p, layer k -- the weak-form divergence (ordered_node_sums), then the faces
+    const int t = tid, p = t / MAXL, k = t % MAXL;
+    const bool mine = t < P * MAXL && k < L;
     const size_t I = (size_t)e * P + p;
     double r_mi = 0.0, r_q = 0.0;
-    if (t < L * P) {
+    if (mine) {
       r_mi = m.nstat[NS_MINV * (size_t)npoin + I];
       r_q = q[((size_t)k * npoin + I) * 3];
     }
-    // this thread's chain in ordered_quad_sums' row tasks: tid % (L*P)
-    const int cr = tid % (L * P), kr = cr / P, pr = cr % P, ir = pr % NGL, jr = pr / NGL;
-    double pi[NQ], dpi[NQ];
-#pragma unroll
-    for (int iq = 0; iq < NQ; iq++) {
-      pi[iq] = s_psiq[ir * NQ + iq];
-      dpi[iq] = s_dpsiq[ir * NQ + iq];
-    }
-    double acc = ordered_quad_sums<NQ, MAXL * P, BS, QS>(s_tb, tid, L * P, [&](int, int jq, double *dst) {
-      weak_div_row<NGL, NQ>(s_psiq, s_dpsiq, pi, dpi, s_qm[0], s_qm[1], s_qm[2], s_qm[3], s_qm[4], s_f[kr][0],
-                            s_f[kr][1], jr, jq, dst);
+    double acc = ordered_node_sums<NQ, P, MAXL, BS, QS>(s_tb, tid, L, [&](int pp, int qd, double *dst, int st) {
+      weak_div_terms<NGL, NQ>(s_psiq, s_dpsiq, s_qm, s_f, L, pp, qd, dst, st);
     });
-    if (t < L * P) {
+    if (mine) {
       int r0, r1;
       node_faces<NGL>(s_map, p, r0, r1);
       acc = face_terms_at<NGL, NQ>(s_psiq, s_side, s_fw, s_fx[k], r0, r1, acc);
@@ -1187,8 +1172,8 @@ __global__ void __launch_bounds__(256, 3)
   __shared__ double s_qm[5][Q];            // e_x, e_y, n_x, n_y, w at quad points
   __shared__ double s_nm[5][P];            // e_x, e_y, n_x, n_y, w at nodes
   // interpolated dp', u', v', u*dp, v*dp per layer (phases 1-2); then the weak forms' term buffers
-  using QS = QSumCfg<NQ, MAXL * 2 * P, 2700>;
-  constexpr bool QSUM = MAXL * 2 * P <= BS;  // one weak-form sum per thread (ordered_quad_sums)
+  using QS = QSumCfg<NQ, P * 2 * MAXL, 2700>;
+  constexpr bool QSUM = P * 2 * MAXL <= BS;  // one weak-form sum per thread (ordered_node_sums)
   constexpr int IVTB = (QSUM && QS::SIZE > MAXL * 5 * Q) ? QS::SIZE : MAXL * 5 * Q;
   __shared__ double s_ivtb[IVTB];
   double(*s_iv)[5][Q] = reinterpret_cast<double(*)[5][Q]>(s_ivtb);
@@ -1445,30 +1430,28 @@ __global__ void __launch_bounds__(256, 3)
   // ---- 3: weak forms, one thread per (layer, output, node), reference accumulation order
   //      (create_rhs_dynamics_volume_layers :401-456, then Apply_layers_fluxes :778-817)
   if constexpr (QSUM) {
-    // thread t: the chain (k, o, p) below, its terms evaluated in parallel (ordered_quad_sums)
-    const int t = tid, k = t / (2 * P), o = (t / P) % 2, p = t % P;
-    // this thread's chain in ordered_quad_sums' row tasks: tid % (2*L*P)
-    const int cr = tid % (L * 2 * P), kr = cr / (2 * P), orr = (cr / P) % 2, pr = cr % P, ir = pr % NGL,
-              jr = pr / NGL;
-    const double *G0 = s_G[kr][3 * orr], *G1 = s_G[kr][3 * orr + 1], *G2 = s_G[kr][3 * orr + 2];
-    double pi[NQ], dpi[NQ];
+    // thread t: node p, chain ko = (k, o) -- its terms evaluated in parallel per node and quad
+    // point (ordered_node_sums), then the face lifts
+    constexpr int CPN = 2 * MAXL;
+    const int t = tid, p = t / CPN, ko = t % CPN, k = ko >> 1, o = ko & 1;
+    double acc = ordered_node_sums<NQ, P, CPN, BS, QS>(s_ivtb, tid, 2 * L, [&](int pp, int qd, double *dst, int st) {
+      const int i = pp % NGL, j = pp / NGL, iq = qd % NQ, jq = qd / NQ;
+      const double pi = s_psiq[i * NQ + iq], dpi = s_dpsiq[i * NQ + iq];
+      const double pj = s_psiq[j * NQ + jq], dpj = s_dpsiq[j * NQ + jq];
+      const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
+      const double dhdx = h_e * s_qm[0][qd] + h_n * s_qm[2][qd];
+      const double dhdy = h_e * s_qm[1][qd] + h_n * s_qm[3][qd];
+      const double w = s_qm[4][qd];
 #pragma unroll
-    for (int iq = 0; iq < NQ; iq++) {
-      pi[iq] = s_psiq[ir * NQ + iq];
-      dpi[iq] = s_dpsiq[ir * NQ + iq];
-    }
-    double acc = ordered_quad_sums<NQ, MAXL * 2 * P, BS, QS>(s_ivtb, tid, L * 2 * P, [&](int, int jq, double *dst) {
-      const double pj = s_psiq[jr * NQ + jq], dpj = s_dpsiq[jr * NQ + jq];
+      for (int kk = 0; kk < MAXL; kk++) {
+        if (kk >= L) break;
 #pragma unroll
-      for (int iq = 0; iq < NQ; iq++) {
-        const int qd = jq * NQ + iq;
-        const double hi = pi[iq] * pj, h_e = dpi[iq] * pj, h_n = pi[iq] * dpj;
-        const double dhdx = h_e * s_qm[0][qd] + h_n * s_qm[2][qd];
-        const double dhdy = h_e * s_qm[1][qd] + h_n * s_qm[3][qd];
-        dst[iq] = s_qm[4][qd] * (hi * G0[qd] + dhdx * G1[qd] + dhdy * G2[qd]);
+        for (int oo = 0; oo < 2; oo++)
+          dst[(2 * kk + oo) * st] =
+              w * (hi * s_G[kk][3 * oo][qd] + dhdx * s_G[kk][3 * oo + 1][qd] + dhdy * s_G[kk][3 * oo + 2][qd]);
       }
     });
-    if (t < L * 2 * P) {
+    if (t < P * CPN && ko < 2 * L) {
       int r0, r1;
       node_faces<NGL>(s_map, p, r0, r1);
       acc = face_terms_at<NGL, NQ>(s_psiq, s_side, s_fw, s_fm[k][o], r0, r1, acc);
