@@ -67,6 +67,10 @@ __device__ __forceinline__ void load_basis(const DevMesh &m, double *s_psiq, dou
 
 // Workgroup barrier for LDS hand-offs only (no release fence: outstanding global stores of the
 // wave are not drained, unlike __syncthreads())
+// mom_elem phase 2: the interface-height gradient sums on their own threads first (see GZS there)
+#ifndef HNUMO_MOM_GZS
+#define HNUMO_MOM_GZS 1
+#endif
 #define BCL_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
 // Term buffers of ordered_node_sums: chunks of RC quad rows (RC | NQ) for NT chains, two buffers
@@ -1294,6 +1298,44 @@ __global__ void __launch_bounds__(256, 3)
   //      392-425, nonzero terms only, then the face terms :521-611)
   const double Pstress = (g / m.alpha[0]) * 50.0;
   const double Pbstress = (g / m.alpha[L - 1]) * 10.0;
+  // GZS: the interface-height gradients gz0[k] (x), gz1[k] (y) at the quad points (the coupling's
+  // 25-term sums, :339-349) first, one thread per (quad point, direction), into s_gz (in the part
+  // of s_ivtb past the interpolations, free until phase 3); the coupling then reads them
+  constexpr bool GZS = HNUMO_MOM_GZS && 2 * Q <= BS && MAXL * 5 * Q + 2 * (MAXL + 1) * Q <= IVTB;
+  double(*s_gz)[MAXL + 1][Q] = reinterpret_cast<double(*)[MAXL + 1][Q]>(s_ivtb + MAXL * 5 * Q);
+  if constexpr (GZS) {
+    if (tid < 2 * Q) {
+      const int d = tid / Q, qd = tid - d * Q, iq = qd % NQ, jq = qd / NQ;
+      double gz[MAXL + 1];
+#pragma unroll
+      for (int k = 0; k <= MAXL; k++) gz[k] = 0.0;
+      double pa[NGL], da[NGL], pb[NGL], db[NGL];
+#pragma unroll
+      for (int n = 0; n < NGL; n++) {
+        pa[n] = s_psiq[n * NQ + iq];
+        da[n] = s_dpsiq[n * NQ + iq];
+        pb[n] = s_psiq[n * NQ + jq];
+        db[n] = s_dpsiq[n * NQ + jq];
+      }
+      const double ea = s_qm[d][qd], eb = s_qm[2 + d][qd];  // (e_x, n_x) | (e_y, n_y)
+#pragma unroll 1
+      for (int mm = 0; mm < NGL; mm++)
+#pragma unroll
+        for (int n = 0; n < NGL; n++) {
+          const int ip = mm * NGL + n;
+          const double h_e = da[n] * pb[mm], h_n = pa[n] * db[mm];
+          const double dd = h_e * ea + h_n * eb;
+#pragma unroll
+          for (int k = 0; k <= MAXL; k++) {
+            if (k > L) break;
+            gz[k] = gz[k] + dd * s_z[k][ip];
+          }
+        }
+#pragma unroll
+      for (int k = 0; k <= MAXL; k++) s_gz[d][k][qd] = gz[k];
+    }
+    BCL_LDS_BARRIER();
+  }
   for (int w = tid; w < Q + L * 2 * P; w += BS) {
     if (w < Q) {
       const int qd = w, iq = qd % NQ, jq = qd / NQ;
@@ -1318,6 +1360,14 @@ __global__ void __launch_bounds__(256, 3)
       }
 #pragma unroll
       for (int k = 0; k <= MAXL; k++) gz0[k] = gz1[k] = 0.0;
+      if constexpr (GZS) {
+#pragma unroll
+        for (int k = 0; k <= MAXL; k++)
+          if (k <= L) {
+            gz0[k] = s_gz[0][k][qd];
+            gz1[k] = s_gz[1][k][qd];
+          }
+      } else {
       double pa[NGL], da[NGL], pb[NGL], db[NGL];
 #pragma unroll
       for (int n = 0; n < NGL; n++) {
@@ -1342,6 +1392,7 @@ __global__ void __launch_bounds__(256, 3)
             gz1[k] = gz1[k] + dy * s_z[k][ip];
           }
         }
+      }
       double su = 0, suv = 0, sv = 0, stu = 0, stv = 0, sH = 0;
 #pragma unroll
       for (int k = 0; k < MAXL; k++)
