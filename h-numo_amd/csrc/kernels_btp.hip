@@ -70,6 +70,11 @@
 #ifndef HNUMO_FD0
 #define HNUMO_FD0 0
 #endif
+// Chunked D phases (StageCfg::VSUM): term tasks split in two node halves, and one summing thread
+// per (component, node) for the whole volume integral (its partial sum in a register)
+#ifndef HNUMO_VSUM
+#define HNUMO_VSUM 1
+#endif
 namespace hnumo {
 
 // A trace value with the tag of the stage it is for: one 16-byte write-through store makes
@@ -264,6 +269,14 @@ struct StageCfg {
   static constexpr bool FPRE = !SF && !LATE && !SLATE && (SLIM || 4 * NQ * 8 <= QN_END_W);
   // LATE chunk phase KP+1: face fluxes from OFD, LDG fluxes from OLD, past the term tasks
   static constexpr int WTMAX = QC * NGL, OFD = ((WTMAX + RU - 1) / RU) * RU, OLD = OFD + 4 * NQ;
+  // VSUM (exact, chunked D): a chunk's term tasks split in two node halves on threads
+  // [0, 2*WTMAX) (the longest lane forms ceil(NGL/2) nodes' terms instead of NGL), and the 3P
+  // ordered chains summed by threads [OVS, BS), one per (component, node) and the same in every
+  // phase, the partial sum in a register (instead of 3 chains per thread through s_rhs); qq and
+  // the LDG face fluxes (D0, no sums yet) after the terms
+  static constexpr int OVS = BS - 3 * P;
+  static constexpr bool VSUM = HNUMO_VSUM && !SF && !OTF && !LATE && !FD0 && 2 * WTMAX <= OVS &&
+                               2 * WTMAX + P <= BS && OL >= 2 * WTMAX + P && OL + 4 * NGL <= BS;
   // REGACC (persistent sub-cycle): every accumulating task (quad point, face quad point, node,
   // LDG face node) has its own thread, the same in every stage, so the time averages can live in
   // that thread's registers for the whole launch and be written once, scaled, at the end
@@ -1399,9 +1412,14 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     // D0, the Laplacian in the last phase.
     // term task (q in chunk k, i): T(v, p=(i,j), q) for j = 0..NGL-1
     auto tbuf = [&](int k) { return SB + ((k & 1) ? C::TB1 : C::TB0); };
+    // (VSUM: task t >= WTMAX is the second node half of pair t - WTMAX: j from JH on; the halves
+    // run the same code, the second's surplus iteration masked)
+    constexpr bool VSUM = C::VSUM;
+    constexpr int JH = VSUM ? (NGL + 1) / 2 : NGL;
     auto term_task = [&](int k, int t) {
       double *T = tbuf(k);
-      const int qi = t / NGL, i = t % NGL;
+      const int h = (VSUM && t >= C::WTMAX) ? 1 : 0, tq = t - h * C::WTMAX;
+      const int qi = tq / NGL, i = tq % NGL;
       const int q = k * QC + qi, iq = q % NQ, jq = q / NQ;
       const double wq = s_qk[QE_W * Q + q], ex = s_qk[QE_EX * Q + q], ey = s_qk[QE_EY * Q + q];
       const double nx = s_qk[QE_NX * Q + q], ny = s_qk[QE_NY * Q + q];
@@ -1409,7 +1427,9 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       const double quv = s_qv[4 * Q + q], scy = s_qv[5 * Q + q], B = s_qv[6 * Q + q];
       const double pi = s_psiq[i * NQ + iq], dpi = s_dpsiq[i * NQ + iq];
 #pragma unroll
-      for (int j = 0; j < NGL; j++) {
+      for (int jj = 0; jj < JH; jj++) {
+        const int j = h * JH + jj;
+        if (j >= NGL) break;
         const double pj = s_psiq[j * NQ + jq], dpj = s_dpsiq[j * NQ + jq];
         const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
         const double dhdx = h_e * ex + h_n * nx;
@@ -1533,11 +1553,58 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     // the LDG fluxes run in D0
     constexpr int WTMAX = C::WTMAX;
     constexpr int OSUM = (P <= 64 && WTMAX <= BS - 64) ? BS - 64 : WTMAX;
+    // VSUM: thread OVS + (v*P + p) sums chain (v, p) of every chunk, the partial sum in vacc
+    double vacc = 0.0;
+    auto vsum_chunk = [&](int k) {
+      const int t = tid - C::OVS, v = t / P, p = t - v * P;
+      const int nq_k = (k == NCH - 1) ? Q - k * QC : QC;
+      const double *T = tbuf(k) + (v * P + p) * QCP;
+      constexpr int SBK = 9;
+#pragma unroll 1
+      for (int q0 = 0; q0 < nq_k; q0 += SBK) {
+        double tv[SBK];
+#pragma unroll
+        for (int qi = 0; qi < SBK; qi++) tv[qi] = q0 + qi < nq_k ? T[q0 + qi] : 0.0;
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int qi = 0; qi < SBK; qi++)
+          if (q0 + qi < nq_k) vacc = vacc + tv[qi];
+      }
+      if (k == NCH - 1) {
+        if (!(a.dbg & 1)) {  // the face projections of component v (sum_last_v's)
+#pragma unroll
+          for (int kf = 0; kf < 2; kf++) {
+            asm volatile("" ::: "memory");
+            const int r = s_pf[2 * p + kf];
+            if (r < 0) continue;
+            const int lf = r / NGL, n = r % NGL;
+            const double sg = s_side[lf] == 0 ? -1.0 : 1.0;
+            const double *fq = s_fq + lf * NQ * 4;
+            double c[NQ], fw[NQ], ps[NQ];
+#pragma unroll
+            for (int iq = 0; iq < NQ; iq++) {
+              fw[iq] = fq[iq * 4];
+              ps[iq] = s_psiq[n * NQ + iq];
+              c[iq] = fq[iq * 4 + 1 + v];
+            }
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int iq = 0; iq < NQ; iq++) vacc = vacc + sg * ((fw[iq] * ps[iq]) * c[iq]);
+          }
+        }
+        s_rhs[v * P + p] = vacc;
+      }
+    };
 #pragma unroll
     for (int k = 0; k <= NCH; k++) {
       asm volatile("" ::: "memory");  // keep LDS reads inside their phase (no hoisting)
       const int WT = (k < NCH) ? ((k == NCH - 1) ? (Q - k * QC) : QC) * NGL : 0;  // term tasks
       if (LATE && k == C::KP) issue_granule();
+      if constexpr (VSUM) {
+        // first node halves on [0, WT), second halves on [WTMAX, WTMAX + WT)
+        if (tid < WT || (tid >= WTMAX && tid < WTMAX + WT)) term_task(k, tid);
+        if (k >= 1 && tid >= C::OVS && !(a.dbg & 4)) vsum_chunk(k - 1);
+      } else {
       for_tasks<BS>(tid, 0, WT, [&](int t, bool) { term_task(k, t); });
       if (k >= 1 && k < NCH) for_tasks<BS>(tid, OSUM, P, [&](int t, bool) { sum_task(k - 1, t); });
       if (k == NCH && !(a.dbg & 4)) {
@@ -1546,7 +1613,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         else
           for_tasks<BS>(tid, OSUM, P, [&](int t, bool) { sum_task(k - 1, t); });
       }
-      if (k == (FD0 ? 1 : 0)) for_tasks<BS>(tid, WT, P, [&](int t, bool) { qq_task(t); });
+      }
+      if (k == (FD0 ? 1 : 0)) for_tasks<BS>(tid, VSUM ? 2 * WTMAX : WT, P, [&](int t, bool) { qq_task(t); });
       if (k == 0 && !LATE && !FD0) for_tasks<BS>(tid, C::OL, 4 * NGL, ldg_task);
       if (FD0 && k == 0 && tid >= BS - 64) {
         // the last wave: neighbour traces (persistent: checked now), face fluxes, LDG fluxes;
