@@ -1153,6 +1153,10 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   if (const char *sm = getenv("HNUMO_SUMMATION"))
     eng->summation = (sm[0] == 'r' || sm[0] == '0') ? HNUMO_SUM_REFERENCE : HNUMO_SUM_FACTORED;
   if (const char *sd = getenv("HNUMO_STAGE_DBG")) eng->stage_dbg = atoi(sd);
+  // per-stage kernel arena: on meshes that take several residency rounds per stage, the arena
+  // sized for 4 workgroups per CU (1-row term chunks) -- 1.566 -> 1.517 ms per stage at C4
+  // (tools/ab_env.py, round 2); small meshes keep the 3-per-CU arena
+  eng->stage_nb = eng->nelem_owned >= 2048 ? 4 : 0;
   if (const char *sn = getenv("HNUMO_STAGE_NB")) eng->stage_nb = atoi(sn);
   {
     const char *qv = getenv("HNUMO_QPQ");
