@@ -241,11 +241,12 @@ struct Launch {
                        e->lq_flux, e->lapq, e->fqLR, e->fqLR + e->FQ);
   }
   // layer mass update (owned elements); produces dp' (e->dpp) for the consistency step
-  static void mass(hnumo_engine *e, const double *qp, const double *qf, double *q) {
+  // (q_in: the layer thicknesses entering the update; q: where they are written)
+  static void mass(hnumo_engine *e, const double *qp, const double *qf, const double *q_in, double *q) {
     hipLaunchKernelGGL((mass_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
                        e->fmass, e->slmf_face);
     hipLaunchKernelGGL((mass_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(Blk<NGL, NQ>::BSW), 0, e->stream, e->m, qp,
-                       e->qacc, e->fmass, q, e->slmf, e->dpp, e->neg_flag);
+                       e->qacc, e->fmass, q_in, q, e->slmf, e->dpp, e->neg_flag);
   }
   static void cons(hnumo_engine *e, double *q, double *qp_out, int finalize_dp) {
     hipLaunchKernelGGL((cons_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, e->dpp,
@@ -259,14 +260,15 @@ struct Launch {
     hipLaunchKernelGGL((cons_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(Blk<NGL, NQ>::BSW), 0, e->stream, e->m, e->dpp,
                        e->qacc, e->slmf, e->fcons, q, qp_out, finalize_dp);
   }
-  static void momentum(hnumo_engine *e, const double *qf, const double *qp_in, const double *qb, double *q,
-                       double *qp_out, int mode) {
+  // (q_in: the momenta entering the update; mode 1 writes the final qprime, see mom_elem_kernel)
+  static void momentum(hnumo_engine *e, const double *qf, const double *qp_in, const double *qb, const double *q_in,
+                       double *q, double *qp_out, int mode) {
     if (e->lapq_on) lapq_bcl(e, qp_in);
     hipLaunchKernelGGL((mom_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
                        e->gdpp_face, e->gfacc, e->momL, e->momR, e->lapf);
     hipLaunchKernelGGL((mom_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(MomCfg<NGL, NQ>::BS), 0, e->stream, e->m, qp_in, e->qacc,
-                       e->nacc, e->dpp_graduv, e->dpprime_visc, e->momL, e->momR, e->lapf, qb, q, qp_out, mode,
-                       e->lapq_on ? e->lapq : nullptr);
+                       e->nacc, e->dpp_graduv, e->dpprime_visc, e->momL, e->momR, e->lapf, qb, q_in, q, qp_out, mode,
+                       e->lapq_on ? e->lapq : nullptr, e->dpp2, e->neg_flag);
   }
 };
 
@@ -293,21 +295,6 @@ __global__ void finite_check_kernel(const double *x, size_t n, int *flag) {
   const size_t s = (size_t)gridDim.x * blockDim.x;
   bool bad = false;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s) bad |= !isfinite(x[i]);
-  if (__any(bad) && (threadIdx.x % 64) == 0) atomicOr(flag, 2);
-}
-
-// qprime(1) = dpp2; qprime(2:3) = qprime2(2:3)   (ti_rk_bcl.F90:84-85), and in the same launch
-// the non-finite guard on the barotropic state x[nx] (finite_check_kernel)
-__global__ void qprime_final_kernel(double *qp, const double *qp2, const double *dpp2, size_t n, const double *x,
-                                    size_t nx, int *flag) {
-  const size_t s = (size_t)gridDim.x * blockDim.x;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s) {
-    qp[i * 3] = dpp2[i];
-    qp[i * 3 + 1] = qp2[i * 3 + 1];
-    qp[i * 3 + 2] = qp2[i * 3 + 2];
-  }
-  bool bad = false;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nx; i += s) bad |= !isfinite(x[i]);
   if (__any(bad) && (threadIdx.x % 64) == 0) atomicOr(flag, 2);
 }
 
@@ -570,15 +557,6 @@ static void subcycle_prologue(hnumo_engine *e, const double *qb_state, unsigned 
                      e->qbuf[0], qb_state, 4 * (size_t)e->npoin, epoch);
 }
 
-// three device copies in one launch (ti_rk_bcl.F90:53-55)
-__global__ void copy3_kernel(double *d0, const double *s0, size_t n0, double *d1, const double *s1, size_t n1,
-                             double *d2, const double *s2, size_t n2) {
-  const size_t s = (size_t)gridDim.x * blockDim.x, t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (size_t i = t0; i < n0; i += s) d0[i] = s0[i];
-  for (size_t i = t0; i < n1; i += s) d1[i] = s1[i];
-  for (size_t i = t0; i < n2; i += s) d2[i] = s2[i];
-}
-
 static void launch_bcl_coeffs(hnumo_engine *e, const double *qp, double *qf) {
   DISPATCH(e, extract(e, qp, qf, 0));
   DISPATCH(e, bcl_coeffs(e, qp, qf));
@@ -727,12 +705,14 @@ static void launch_step(hnumo_engine *e) {
   // prediction (ti_rk_bcl.F90:43-57)
   launch_bcl_coeffs(e, e->qp, e->qf);
   launch_subcycle(e, e->qbp, e->qp);
-  hipLaunchKernelGGL(copy3_kernel, dim3((int)std::min<size_t>((nf + 255) / 256, 2048)), dim3(256), 0, e->stream, e->q2,
-                     e->q, n3, e->qp2, e->qp, n3, e->qf2, e->qf, nf);
-  DISPATCH(e, mass(e, e->qp2, e->qf2, e->q2));
+  // (q_df2 = q_df, qprime_df2 = qprime_df, qprime_face2 = qprime_face (ti_rk_bcl.F90:53-55) without
+  // copies: the predictor's kernels read q_df, qprime_df and qprime_face and write q_df2 and
+  // qprime_df2 in full -- thicknesses by momentum_mass' mass and consistency updates, momenta and
+  // qprime by its momentum update -- before anything reads them)
+  DISPATCH(e, mass(e, e->qp, e->qf, e->q, e->q2));
   exchange_dpp(e);
   DISPATCH(e, cons(e, e->q2, nullptr, 0));
-  DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qbp, e->q2, e->qp2, 0));
+  DISPATCH(e, momentum(e, e->qf, e->qp, e->qbp, e->q, e->q2, e->qp2, 0));
   exchange_qp(e, e->qp2);
   DISPATCH(e, extract(e, e->qp2, e->qf2, 0));
   // correction (ti_rk_bcl.F90:62-85)
@@ -740,16 +720,16 @@ static void launch_step(hnumo_engine *e) {
                      e->qp2, e->qp, n3, e->qf2, e->qf, nf);
   DISPATCH(e, bcl_coeffs(e, e->qp2, e->qf2));
   launch_subcycle(e, e->qb, e->qp2, true);
-  DISPATCH(e, mass(e, e->qp2, e->qf2, e->q));
+  DISPATCH(e, mass(e, e->qp2, e->qf2, e->q, e->q));
   exchange_dpp(e);
   DISPATCH(e, cons(e, e->q, e->qp2, 1));
   exchange_qp(e, e->qp2);
   DISPATCH(e, extract(e, e->qp2, e->qf2, 1));
   hipLaunchKernelGGL(dp_average_face_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp2, e->qp, e->dpp2, nl, e->qf2,
                      e->qf, nf / 3);
-  DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qb, e->q, e->qp2, 1));
-  hipLaunchKernelGGL(qprime_final_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp, e->qp2, e->dpp2, nl, e->qb,
-                     4 * (size_t)e->npoin, e->neg_flag);
+  // (the corrector's momentum update writes the final qprime_df -- thickness dpp2, momenta of
+  // evaluate_bcl_v1 -- and checks the barotropic state, ti_rk_bcl.F90:81-84)
+  DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qb, e->q, e->q, e->qp, 1));
   exchange_qp(e, e->qp);
   // ad_mlswe > 0 with the reference's corrector input leaves NaN layer momenta (hnumo_params)
   if (e->p.ad_mlswe > 0.0)

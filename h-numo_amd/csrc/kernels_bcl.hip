@@ -674,8 +674,8 @@ __global__ void face_unpack_kernel(double *base, const double *buf, const int *s
 // :224-232), then dp' = q(1)/(sum_k q(1)/pb') for the consistency step (:350-353).
 template <int NGL, int NQ>
 __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
-    mass_elem_kernel(DevMesh m, const double *qp, const double *qacc, const double *fmass, double *q,
-                     double *slmf, double *dpp, int *neg_flag) {
+    mass_elem_kernel(DevMesh m, const double *qp, const double *qacc, const double *fmass, const double *q_in,
+                     double *q, double *slmf, double *dpp, int *neg_flag) {
   constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BSW;
   using QS = typename Blk<NGL, NQ>::QS;
   static_assert(MAXL * P <= BS, "one quad-point sum per thread");
@@ -745,7 +745,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     double r_mi = 0.0, r_q = 0.0;
     if (mine) {
       r_mi = m.nstat[NS_MINV * (size_t)npoin + I];
-      r_q = q[((size_t)k * npoin + I) * 3];
+      r_q = q_in[((size_t)k * npoin + I) * 3];  // (q_in: the predictor reads q_df, writes q_df2)
     }
     double acc = ordered_node_sums<NQ, P, MAXL, BS, QS>(s_tb, tid, L, [&](int pp, int qd, double *dst, int st) {
       weak_div_terms<NGL, NQ>(s_psiq, s_dpsiq, s_qm, s_f, L, pp, qd, dst, st);
@@ -1166,7 +1166,12 @@ template <int NGL, int NQ>
 __global__ void __launch_bounds__(256, 3)
     mom_elem_kernel(DevMesh m, const double *qp_in, const double *qacc, const double *nacc, const double *dpp_graduv,
                     const double *dpprime_visc, const double *momL, const double *momR, const double *lapf,
-                    const double *qb, double *q, double *qp_out, int mode, const double *lapx) {
+                    const double *qb, const double *q_in, double *q, double *qp_out, int mode, const double *lapx,
+                    const double *dpp2, int *flag) {
+  // q_in: the momenta entering the update (the predictor: q_df, its thicknesses already in q =
+  // q_df2); mode 1 (the corrector) writes the step's final qprime straight into qp_out = qprime_df
+  // (ti_rk_bcl.F90:81-84: thickness from dpp2 = the corrector's own, momenta from evaluate_bcl_v1)
+  // and flags a non-finite barotropic state (bit 2) of its element
   constexpr int P = MomCfg<NGL, NQ>::P, Q = MomCfg<NGL, NQ>::Q, BS = MomCfg<NGL, NQ>::BS;
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
   const double g = m.gravity, eps1 = 1.0e-20;
@@ -1224,7 +1229,7 @@ __global__ void __launch_bounds__(256, 3)
   for (int t = tid; t < L * 3 * P; t += BS) {
     int k = t / (3 * P), r = t % (3 * P);
     s_qp[k][r % 3][r / 3] = qp_in[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
-    if (r % 3) s_qm2[k][r % 3 - 1][r / 3] = q[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
+    if (r % 3) s_qm2[k][r % 3 - 1][r / 3] = q_in[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
   }
   for (int t = tid; t < 5 * Q; t += BS) {
     const int c = t / Q;
@@ -1796,9 +1801,13 @@ __global__ void __launch_bounds__(256, 3)
       qq[1] = nw[k][1];
       qq[2] = nw[k][2];
       double *o = qp_out + ((size_t)k * npoin + I) * 3;
-      if (mode == 0) o[0] = h[k] / ope;
+      o[0] = mode == 0 ? h[k] / ope : dpp2[(size_t)k * npoin + I];
       o[1] = uv[k][0] - b3 / b1;
       o[2] = uv[k][1] - b4 / b1;
+    }
+    if (mode == 1) {
+      const double b2 = qb[I * 4 + 1];
+      if (!(isfinite(b1) && isfinite(b2) && isfinite(b3) && isfinite(b4))) atomicOr(flag, 2);
     }
   }
   BCL_MARK(2, 5) BCL_WALL(2, 7)
