@@ -211,10 +211,13 @@ struct Launch {
                        only_dp);
     face_exchange_qf(e, qf, only_dp ? 1 : 3);
   }
-  static void bcl_coeffs(hnumo_engine *e, const double *qp, const double *qf) {
-    hipLaunchKernelGGL((bcl_coeffs_elem_kernel<NGL, NQ>), dim3(e->nelem), dim3(BSE), 0, e->stream, e->m, qp,
-                       e->qcoef, e->ncoef, e->dpp_graduv, e->dpprime_visc, e->ecoef);
-    hipLaunchKernelGGL((bcl_coeffs_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf,
+  // (qp_avg, qf_avg: the corrector's averages qp = 0.5*(qp + qp_avg), qf = 0.5*(qf_avg + qf) formed
+  // and written back by the two kernels, ti_rk_bcl.F90:64-65)
+  static void bcl_coeffs(hnumo_engine *e, double *qp, double *qf, const double *qp_avg = nullptr,
+                         const double *qf_avg = nullptr) {
+    hipLaunchKernelGGL((bcl_coeffs_elem_kernel<NGL, NQ>), dim3(e->nelem), dim3(Blk<NGL, NQ>::BSW), 0, e->stream, e->m, qp,
+                       qp_avg, e->qcoef, e->ncoef, e->dpp_graduv, e->dpprime_visc, e->ecoef);
+    hipLaunchKernelGGL((bcl_coeffs_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, qf_avg,
                        e->dpp_graduv, e->dpprime_visc, e->fcoef, e->fncoef, e->gdpp_face, e->efcoef);
     if (e->face_halo) {  // graduv_dpp_face halo (mod_barotropic_terms.F90:393) and its layer sums
       face_exchange_gdpp(e);
@@ -296,14 +299,6 @@ __global__ void finite_check_kernel(const double *x, size_t n, int *flag) {
   bool bad = false;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += s) bad |= !isfinite(x[i]);
   if (__any(bad) && (threadIdx.x % 64) == 0) atomicOr(flag, 2);
-}
-
-// The corrector's two averages in one launch (ti_rk_bcl.F90:64-65): a0 = 0.5*(a0 + b0) [n0],
-// a1 = 0.5*(b1 + a1) [n1]
-__global__ void average2_kernel(double *a0, const double *b0, size_t n0, double *a1, const double *b1, size_t n1) {
-  const size_t s = (size_t)gridDim.x * blockDim.x, t0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (size_t i = t0; i < n0; i += s) a0[i] = 0.5 * (a0[i] + b0[i]);
-  for (size_t i = t0; i < n1; i += s) a1[i] = 0.5 * (b1[i] + a1[i]);
 }
 
 // dpp2 = qp2(1); qp2(1) = 0.5*(qp(1) + dpp2) (ti_rk_bcl.F90:78-79) with, in the same launch, the
@@ -557,7 +552,7 @@ static void subcycle_prologue(hnumo_engine *e, const double *qb_state, unsigned 
                      e->qbuf[0], qb_state, 4 * (size_t)e->npoin, epoch);
 }
 
-static void launch_bcl_coeffs(hnumo_engine *e, const double *qp, double *qf) {
+static void launch_bcl_coeffs(hnumo_engine *e, double *qp, double *qf) {
   DISPATCH(e, extract(e, qp, qf, 0));
   DISPATCH(e, bcl_coeffs(e, qp, qf));
 }
@@ -716,9 +711,7 @@ static void launch_step(hnumo_engine *e) {
   exchange_qp(e, e->qp2);
   DISPATCH(e, extract(e, e->qp2, e->qf2, 0));
   // correction (ti_rk_bcl.F90:62-85)
-  hipLaunchKernelGGL(average2_kernel, dim3((int)std::min<size_t>((n3 + 255) / 256, 2048)), dim3(256), 0, e->stream,
-                     e->qp2, e->qp, n3, e->qf2, e->qf, nf);
-  DISPATCH(e, bcl_coeffs(e, e->qp2, e->qf2));
+  DISPATCH(e, bcl_coeffs(e, e->qp2, e->qf2, e->qp, e->qf));
   launch_subcycle(e, e->qb, e->qp2, true);
   DISPATCH(e, mass(e, e->qp2, e->qf2, e->q, e->q));
   exchange_dpp(e);

@@ -298,10 +298,12 @@ __global__ void extract_face_kernel(DevMesh m, const double *qp, double *qf, int
 // dpp_graduv, btp_dpp_graduv, pbprime_visc at nodes (:287-304).  dpprime_visc =
 // qprime(1,:,:) is stored for the layer LDG (ti_rk_bcl.F90:47,66).
 template <int NGL, int NQ>
-__global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
-    bcl_coeffs_elem_kernel(DevMesh m, const double *qp, double *qcoef, double *ncoef, double *dpp_graduv,
-                           double *dpprime_visc, double *ecoef) {
-  constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BS;
+__global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
+    bcl_coeffs_elem_kernel(DevMesh m, double *qp, const double *qp_avg, double *qcoef, double *ncoef,
+                           double *dpp_graduv, double *dpprime_visc, double *ecoef) {
+  // qp_avg (the corrector): qprime_df2 = 0.5*(qprime_df2 + qprime_df) of the element's nodes first
+  // (ti_rk_bcl.F90:64), written back
+  constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BSW;
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q;
   __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
   __shared__ double s_q[MAXL][3][P];
@@ -310,11 +312,19 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
   load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
   for (int t = tid; t < L * 3 * P; t += BS) {
     int k = t / (3 * P), r = t % (3 * P);
-    s_q[k][r % 3][r / 3] = qp[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
+    const size_t i = (size_t)k * 3 * npoin + (size_t)e * 3 * P + r;
+    double v = qp[i];
+    if (qp_avg) {
+      v = 0.5 * (v + qp_avg[i]);
+      qp[i] = v;
+    }
+    s_q[k][r % 3][r / 3] = v;
   }
   for (int t = tid; t < 4 * P; t += BS)
     s_nm[t / P][t % P] = m.nstat[(NS_EX + t / P) * (size_t)npoin + (size_t)e * P + t % P];
   __syncthreads();
+  // GSPLIT: quad-point tasks on threads [0, Q), the nodal gradient tasks on the threads past them
+  constexpr bool GSPLIT = BS - Q >= 128;
   for (int q = tid; q < Q; q += BS) {
     const int iq = q % NQ, jq = q / NQ;
     double quu = 0.0, quv = 0.0, qvv = 0.0, hb = 0.0, pk = 0.0;
@@ -348,7 +358,7 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
     ec[QC_HBCL * Q + q] = hb;
   }
   // compute_gradient_uv of (u'_k, v'_k), reference order, one thread per (layer, comp, node)
-  for (int t = tid; t < L * 4 * P; t += BS) {
+  for (int t = GSPLIT ? tid - Q : tid; t >= 0 && t < L * 4 * P; t += GSPLIT ? BS - Q : BS) {
     const int k = t / (4 * P), c = (t / P) % 4, p = t % P, i = p % NGL, j = p / NGL;
     const double *u = s_q[k][1 + (c >> 1)];
     const double ex = s_nm[(c & 1) ? 1 : 0][p], nx = s_nm[(c & 1) ? 3 : 2][p];
@@ -398,8 +408,11 @@ __global__ void __launch_bounds__(((NQ * NQ + 63) / 64) * 64)
 // face traces graduv_dpp_face + their layer sum btp_graduv_dpp_face (:339-407).
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(64)
-    bcl_coeffs_face_kernel(DevMesh m, const double *qf, const double *dpp_graduv, const double *dpprime_visc,
-                           double *fcoef, double *fncoef, double *gdpp_face, double *efcoef) {
+    bcl_coeffs_face_kernel(DevMesh m, double *qf, const double *qf_avg, const double *dpp_graduv,
+                           const double *dpprime_visc, double *fcoef, double *fncoef, double *gdpp_face,
+                           double *efcoef) {
+  // qf_avg (the corrector): qprime_face2 = 0.5*(qprime_face + qprime_face2) of the face first
+  // (ti_rk_bcl.F90:65), written back
   const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L, npoin = m.npoin;
   __shared__ double s_psiq[NGL * NQ];
   __shared__ double s_qf[MAXL][6 * NGL];
@@ -407,7 +420,16 @@ __global__ void __launch_bounds__(64)
   const size_t FQ = (size_t)F * NQ, FN = (size_t)F * NGL;
   const int erf = m.fer[f];
   for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
-  stage_qf<NGL>(s_qf, qf, f, F, L, tid, 64);
+  for (int t = tid; t < L * 6 * NGL; t += 64) {
+    const int k = t / (6 * NGL), r = t % (6 * NGL);
+    const size_t i = ((size_t)k * F + f) * NGL * 6 + r;
+    double v = qf[i];
+    if (qf_avg) {
+      v = 0.5 * (qf_avg[i] + v);
+      qf[i] = v;
+    }
+    s_qf[k][r] = v;
+  }
   for (int t = tid; t < L * 2 * 5 * NGL; t += 64) {
     const int k = t / (10 * NGL), sd = (t / (5 * NGL)) % 2, c = (t / NGL) % 5, n = t % NGL;
     if (sd == 1 && erf <= 0) continue;
@@ -1815,9 +1837,9 @@ __global__ void __launch_bounds__(256, 3)
 
 #define HNUMO_INSTANTIATE_BCL(NGL, NQ)                                                                              \
   template __global__ void extract_face_kernel<NGL>(DevMesh, const double *, double *, int);                      \
-  template __global__ void bcl_coeffs_elem_kernel<NGL, NQ>(DevMesh, const double *, double *, double *, double *,    \
-                                                           double *);                                              \
-  template __global__ void bcl_coeffs_face_kernel<NGL, NQ>(DevMesh, const double *, const double *, const double *,  \
-                                                           double *, double *, double *);
+  template __global__ void bcl_coeffs_elem_kernel<NGL, NQ>(DevMesh, double *, const double *, double *, double *,    \
+                                                           double *, double *, double *);                          \
+  template __global__ void bcl_coeffs_face_kernel<NGL, NQ>(DevMesh, double *, const double *, const double *,        \
+                                                           const double *, double *, double *, double *, double *);
 
 }  // namespace hnumo
