@@ -1429,7 +1429,7 @@ int hnumo_stage_path(hnumo_engine *eng) { return eng ? (use_persistent(eng) ? 1 
 #if HNUMO_BCL_PROF
 // diagnostics build only (not part of the ABI): the element kernels' phase clocks, see g_bcl_prof
 int hnumo_bcl_prof(unsigned long long *dst, int n) {
-  const size_t bytes = std::min<size_t>((size_t)n, 3 * 8192 * 8) * sizeof(unsigned long long);
+  const size_t bytes = std::min<size_t>((size_t)n, 4 * 8192 * 8) * sizeof(unsigned long long);
   return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_bcl_prof), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif

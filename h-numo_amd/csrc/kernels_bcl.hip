@@ -29,7 +29,7 @@ namespace hnumo {
 #define HNUMO_BCL_PROF 0
 #endif
 #if HNUMO_BCL_PROF
-__device__ unsigned long long g_bcl_prof[3][8192][8];
+__device__ unsigned long long g_bcl_prof[4][8192][8];
 #define BCL_MARK(kid, k) \
   if (threadIdx.x == 0 && blockIdx.x < 8192) g_bcl_prof[kid][blockIdx.x][k] = clock64();
 #define BCL_WALL(kid, k) \
@@ -904,6 +904,7 @@ __global__ void __launch_bounds__(64)
                          const double *gfacc, double *momL, double *momR, double *lap) {
   const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L;
   const size_t FQ = (size_t)F * NQ, FN = (size_t)F * NGL;
+  BCL_MARK(3, 0) BCL_WALL(3, 6)
   const int slot = m.fslotA[f];
   // every input of the face in one round of independent loads (the face's qf block per layer,
   // its 16 averages, the LDG face averages and coefficients, the face statics), then the
@@ -938,6 +939,7 @@ __global__ void __launch_bounds__(64)
     s_fn[c][n] = m.fnstat[fld[c] * FN + (size_t)f * NGL + n];
   }
   __syncthreads();
+  BCL_MARK(3, 1)
   const int er = m.fer[f];
   const double g = m.gravity, eps1 = 1.0e-20;
 #define FA(k) s_fa[(k) * NQ + iq]
@@ -1145,6 +1147,7 @@ __global__ void __launch_bounds__(64)
       momR[((size_t)k * 2 + 0) * FQ + fq] = hrx + flux_x;
       momR[((size_t)k * 2 + 1) * FQ + fq] = hry + flux_y;
     }
+    BCL_MARK(3, 2)
   } else if (tid >= 32 && tid < 32 + NGL) {
     // layer LDG flux at face node n for every layer
     const int n = tid - 32;
@@ -1168,6 +1171,7 @@ __global__ void __launch_bounds__(64)
       lap[((size_t)k * 2 + 1) * FN + fn] = wq * h1 * flux_qv;
     }
   }
+  BCL_MARK(3, 5) BCL_WALL(3, 7)
 #undef FA
 }
 

@@ -16,17 +16,20 @@ eng.set_resident(True)
 q, qb, qp = eng.state()
 for _ in range(2):
     eng.ti_rk_bcl(q, qb, qp)
-buf = np.zeros(3 * 8192 * 8, dtype=np.uint64)
+buf = np.zeros(4 * 8192 * 8, dtype=np.uint64)
 L = lib()
 L.hnumo_bcl_prof.argtypes = [ctypes.c_void_p, ctypes.c_int]
 assert L.hnumo_bcl_prof(buf.ctypes.data, buf.size) == 0
 E = case.scalars["nelem"]
-pr = buf.reshape(3, 8192, 8)[:, :E].astype(np.int64)
+pr4 = buf.reshape(4, 8192, 8).astype(np.int64)
+pr = pr4[:, :E]
 names = {0: ("mass_elem", ["loads", "quad", "node sums", "faces+store", "final"]),
          1: ("cons_elem", ["loads", "-", "quad", "node", "final"]),
-         2: ("mom_elem", ["loads", "ph1 interp", "ph2 couple+lap", "ph3 weak", "ph4 tail"])}
+         2: ("mom_elem", ["loads", "ph1 interp", "ph2 couple+lap", "ph3 weak", "ph4 tail"]),
+         3: ("mom_flux_face", ["loads", "quad lane", "-", "-", "end"])}
+NF = case.scalars["nface"] if "nface" in case.scalars else E
 for k, (nm, ph) in names.items():
-    a = pr[k]
+    a = pr4[k, :NF] if k == 3 else pr[k]
     tot = a[:, 5] - a[:, 0]
     w0, w1 = a[:, 6], a[:, 7]
     print(f"{nm}: block clocks mean {tot.mean():.0f} max {tot.max():.0f}; wall (100 MHz) start spread "
