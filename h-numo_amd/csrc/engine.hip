@@ -1044,7 +1044,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     const int fnmap[EFN_N] = {FN_NX, FN_NY, FN_W, FN_PBL, FN_PBR};
     for (int e = 0; e < E; e++) {
       for (int c = 0; c < QE_N; c++)
-        for (int q = 0; q < Qe; q++) qsE[((size_t)e * QE_N + c) * Qe + q] = qs[qmap[c] * npq + (size_t)e * Qe + q];
+        for (int q = 0; q < Qe; q++) qsE[(size_t)e * QE_N * Qe + qe_pos(c, q, Qe)] = qs[qmap[c] * npq + (size_t)e * Qe + q];
       for (int c = 0; c < NE_N; c++)
         for (int p = 0; p < P; p++) nsE[((size_t)e * NE_N + c) * P + p] = ns[nmap[c] * npoin + (size_t)e * P + p];
       for (int lf = 0; lf < 4; lf++) {

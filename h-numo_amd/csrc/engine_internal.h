@@ -67,6 +67,16 @@ enum FNStat { FN_NX = 0, FN_NY, FN_W, FN_PBL, FN_PBR, FN_N };
 // element-major quad statics order (qstatE): the first QE_KEEP rows live for the whole stage
 enum QStatE { QE_W = 0, QE_EX, QE_EY, QE_NX, QE_NY, QE_COR, QE_TW1, QE_TW2, QE_GZ1, QE_GZ2, QE_OOP, QE_N };
 constexpr int QE_KEEP = 5;
+// Positions in the first QE_KEEP rows of an element's qstatE record (Q quad points): W, then the
+// metric pairs interleaved per quad point -- (e_x, n_x), (e_y, n_y) adjacent, read together with
+// one ds_read2 where a row layout put them 2Q apart -- the later rows field-major (c*Q + q)
+__host__ __device__ constexpr int qe_pos(int c, int q, int Q) {
+  return c == QE_W ? q
+                   : c == QE_EX ? Q + 2 * q
+                   : c == QE_NX ? Q + 2 * q + 1
+                   : c == QE_EY ? 3 * Q + 2 * q
+                   : c == QE_NY ? 3 * Q + 2 * q + 1 : c * Q + q;
+}
 // element-major nodal statics order (nstatE); the first NE_LDS rows are the ones the stage
 // kernel's slim LDS arena (StageCfg::SLIM) stages -- its E1 reads massinv and pbprime into
 // registers from global memory

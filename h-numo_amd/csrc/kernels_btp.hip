@@ -399,7 +399,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   const int *s_nbe = s_er + EREC_NBE, *s_nblf = s_er + EREC_NBLF, *s_map = s_er + EREC_MAP, *s_pf = s_er + EREC_PF(NGL);
   const int *s_acc = s_er + EREC_ACC;
   double *s_qb = S + C::O_QB, *s_q0 = S + C::O_Q0, *s_q2 = S + C::O_Q2;  // [P][4]
-  double *s_qk = S + C::O_QK;      // [QE_KEEP][Q]: W, e_x, e_y, n_x, n_y
+  double *s_qk = S + C::O_QK;      // [QE_KEEP*Q]: W, (e_x, n_x), (e_y, n_y) pairs (qe_pos)
   double *s_ns = S + C::O_NS;      // [NE_N][P]
   double *s_nc = S + C::O_NC;      // [5][P] pbprime_visc, btp_dpp_graduv(4)
   double *s_u = S + C::O_UV, *s_v = s_u + P;  // u_bar = qb(3)/qb(1), v_bar = qb(4)/qb(1) at the nodes
@@ -992,8 +992,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         // weighted integrands of T(v) = wq*(hi*S_v + dhdx*X_v + dhdy*Y_v) split by basis
         // factor: psi*psi -> F_v = wq*S_v, dpsi*psi -> G_v = wq*(e_x X_v + e_y Y_v),
         // psi*dpsi -> H_v = wq*(n_x X_v + n_y Y_v)  (create_rhs_btp_volume_qdf, :194-206)
-        const double wq = s_qk[QE_W * Q + q], ex = s_qk[QE_EX * Q + q], ey = s_qk[QE_EY * Q + q];
-        const double nx = s_qk[QE_NX * Q + q], ny = s_qk[QE_NY * Q + q];
+        const double wq = s_qk[qe_pos(QE_W, q, Q)], ex = s_qk[qe_pos(QE_EX, q, Q)], ey = s_qk[qe_pos(QE_EY, q, Q)];
+        const double nx = s_qk[qe_pos(QE_NX, q, Q)], ny = s_qk[qe_pos(QE_NY, q, Q)];
         const double A = Hq + qu, B = Hq + qv;
         s_qv[0 * Q + q] = wq * sc_x;
         s_qv[1 * Q + q] = wq * sc_y;
@@ -1244,8 +1244,9 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       const int r1 = v == 2 ? 5 : 2, r2 = v == 0 ? 0 : (v == 1 ? 3 : 4), r3 = v == 0 ? 1 : (v == 1 ? 4 : 6);
       const bool z1 = v == 0;
       const double *Q1 = s_qv + r1 * Q, *Q2 = s_qv + r2 * Q, *Q3 = s_qv + r3 * Q;
-      const double *Wq = s_qk + QE_W * Q, *Ex = s_qk + QE_EX * Q, *Ey = s_qk + QE_EY * Q;
-      const double *Nx = s_qk + QE_NX * Q, *Ny = s_qk + QE_NY * Q;
+      // (qstatE: W rows, then e_x/n_x and e_y/n_y interleaved, qe_pos -- stride 2 for the metrics)
+      const double *Wq = s_qk + qe_pos(QE_W, 0, Q), *Ex = s_qk + qe_pos(QE_EX, 0, Q), *Ey = s_qk + qe_pos(QE_EY, 0, Q);
+      const double *Nx = s_qk + qe_pos(QE_NX, 0, Q), *Ny = s_qk + qe_pos(QE_NY, 0, Q);
       const double *Pi = s_psiq + i * NQ, *DPi = s_dpsiq + i * NQ, *Pj = s_psiq + j * NQ, *DPj = s_dpsiq + j * NQ;
       double acc = 0.0;
 #pragma unroll 1
@@ -1257,8 +1258,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           const int q = q0 + iq;
           const double pi = Pi[iq], dpi = DPi[iq];
           const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
-          const double dhdx = h_e * Ex[q] + h_n * Nx[q];
-          const double dhdy = h_e * Ey[q] + h_n * Ny[q];
+          const double dhdx = h_e * Ex[2 * q] + h_n * Nx[2 * q];
+          const double dhdy = h_e * Ey[2 * q] + h_n * Ny[2 * q];
           const double s1 = z1 ? 0.0 : Q1[q];
           acc = acc + Wq[q] * ((hi * s1 + dhdx * Q2[q]) + Q3[q] * dhdy);
         }
@@ -1273,8 +1274,9 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     auto otf_sum0 = [&](int p) {
       const int i = p % NGL, j = p / NGL;
       const double *U = s_qv + 0 * Q, *V = s_qv + 1 * Q;
-      const double *Wq = s_qk + QE_W * Q, *Ex = s_qk + QE_EX * Q, *Ey = s_qk + QE_EY * Q;
-      const double *Nx = s_qk + QE_NX * Q, *Ny = s_qk + QE_NY * Q;
+      // (qstatE: W rows, then e_x/n_x and e_y/n_y interleaved, qe_pos -- stride 2 for the metrics)
+      const double *Wq = s_qk + qe_pos(QE_W, 0, Q), *Ex = s_qk + qe_pos(QE_EX, 0, Q), *Ey = s_qk + qe_pos(QE_EY, 0, Q);
+      const double *Nx = s_qk + qe_pos(QE_NX, 0, Q), *Ny = s_qk + qe_pos(QE_NY, 0, Q);
       const double *Pi = s_psiq + i * NQ, *DPi = s_dpsiq + i * NQ, *Pj = s_psiq + j * NQ, *DPj = s_dpsiq + j * NQ;
       double acc = 0.0;
 #pragma unroll 1
@@ -1286,8 +1288,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           const int q = q0 + iq;
           const double pi = Pi[iq], dpi = DPi[iq];
           const double h_e = dpi * pj, h_n = pi * dpj;
-          const double dhdx = h_e * Ex[q] + h_n * Nx[q];
-          const double dhdy = h_e * Ey[q] + h_n * Ny[q];
+          const double dhdx = h_e * Ex[2 * q] + h_n * Nx[2 * q];
+          const double dhdy = h_e * Ey[2 * q] + h_n * Ny[2 * q];
           acc = acc + Wq[q] * (dhdx * U[q] + V[q] * dhdy);
         }
       }
@@ -1296,8 +1298,9 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     auto otf_sum12 = [&](int p, double &acc1, double &acc2) {
       const int i = p % NGL, j = p / NGL;
       const double *SX = s_qv + 2 * Q, *A_ = s_qv + 3 * Q, *UV = s_qv + 4 * Q, *SY = s_qv + 5 * Q, *B_ = s_qv + 6 * Q;
-      const double *Wq = s_qk + QE_W * Q, *Ex = s_qk + QE_EX * Q, *Ey = s_qk + QE_EY * Q;
-      const double *Nx = s_qk + QE_NX * Q, *Ny = s_qk + QE_NY * Q;
+      // (qstatE: W rows, then e_x/n_x and e_y/n_y interleaved, qe_pos -- stride 2 for the metrics)
+      const double *Wq = s_qk + qe_pos(QE_W, 0, Q), *Ex = s_qk + qe_pos(QE_EX, 0, Q), *Ey = s_qk + qe_pos(QE_EY, 0, Q);
+      const double *Nx = s_qk + qe_pos(QE_NX, 0, Q), *Ny = s_qk + qe_pos(QE_NY, 0, Q);
       const double *Pi = s_psiq + i * NQ, *DPi = s_dpsiq + i * NQ, *Pj = s_psiq + j * NQ, *DPj = s_dpsiq + j * NQ;
       double a1 = 0.0, a2 = 0.0;
 #pragma unroll 1
@@ -1309,8 +1312,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           const int q = q0 + iq;
           const double pi = Pi[iq], dpi = DPi[iq];
           const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
-          const double dhdx = h_e * Ex[q] + h_n * Nx[q];
-          const double dhdy = h_e * Ey[q] + h_n * Ny[q];
+          const double dhdx = h_e * Ex[2 * q] + h_n * Nx[2 * q];
+          const double dhdy = h_e * Ey[2 * q] + h_n * Ny[2 * q];
           const double w = Wq[q], uv = UV[q];
           a1 = a1 + w * ((hi * SX[q] + dhdx * A_[q]) + uv * dhdy);
           a2 = a2 + w * ((hi * SY[q] + dhdx * uv) + B_[q] * dhdy);
@@ -1421,8 +1424,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       const int h = (VSUM && t >= C::WTMAX) ? 1 : 0, tq = t - h * C::WTMAX;
       const int qi = tq / NGL, i = tq % NGL;
       const int q = k * QC + qi, iq = q % NQ, jq = q / NQ;
-      const double wq = s_qk[QE_W * Q + q], ex = s_qk[QE_EX * Q + q], ey = s_qk[QE_EY * Q + q];
-      const double nx = s_qk[QE_NX * Q + q], ny = s_qk[QE_NY * Q + q];
+      const double wq = s_qk[qe_pos(QE_W, q, Q)], ex = s_qk[qe_pos(QE_EX, q, Q)], ey = s_qk[qe_pos(QE_EY, q, Q)];
+      const double nx = s_qk[qe_pos(QE_NX, q, Q)], ny = s_qk[qe_pos(QE_NY, q, Q)];
       const double udp = s_qv[0 * Q + q], vdp = s_qv[1 * Q + q], scx = s_qv[2 * Q + q], A = s_qv[3 * Q + q];
       const double quv = s_qv[4 * Q + q], scy = s_qv[5 * Q + q], B = s_qv[6 * Q + q];
       const double pi = s_psiq[i * NQ + iq], dpi = s_dpsiq[i * NQ + iq];
