@@ -264,14 +264,17 @@ struct Launch {
                        e->qacc, e->slmf, e->fcons, q, qp_out, finalize_dp);
   }
   // (q_in: the momenta entering the update; mode 1 writes the final qprime, see mom_elem_kernel)
+  // (qp_avg0, qf_avg0: the corrector's thickness averages of ti_rk_bcl.F90:78-80, formed by the two
+  // kernels on load instead of by a launch before them; the final qprime(1) is then qp_in's own)
   static void momentum(hnumo_engine *e, const double *qf, const double *qp_in, const double *qb, const double *q_in,
-                       double *q, double *qp_out, int mode) {
+                       double *q, double *qp_out, int mode, const double *qp_avg0 = nullptr,
+                       const double *qf_avg0 = nullptr) {
     if (e->lapq_on) lapq_bcl(e, qp_in);
     hipLaunchKernelGGL((mom_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
-                       e->gdpp_face, e->gfacc, e->momL, e->momR, e->lapf);
+                       e->gdpp_face, e->gfacc, e->momL, e->momR, e->lapf, qf_avg0);
     hipLaunchKernelGGL((mom_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(MomCfg<NGL, NQ>::BS), 0, e->stream, e->m, qp_in, e->qacc,
                        e->nacc, e->dpp_graduv, e->dpprime_visc, e->momL, e->momR, e->lapf, qb, q_in, q, qp_out, mode,
-                       e->lapq_on ? e->lapq : nullptr, e->dpp2, e->neg_flag);
+                       e->lapq_on ? e->lapq : nullptr, e->dpp2, e->neg_flag, qp_avg0);
   }
 };
 
@@ -718,11 +721,17 @@ static void launch_step(hnumo_engine *e) {
   DISPATCH(e, cons(e, e->q, e->qp2, 1));
   exchange_qp(e, e->qp2);
   DISPATCH(e, extract(e, e->qp2, e->qf2, 1));
-  hipLaunchKernelGGL(dp_average_face_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp2, e->qp, e->dpp2, nl, e->qf2,
-                     e->qf, nf / 3);
   // (the corrector's momentum update writes the final qprime_df -- thickness dpp2, momenta of
-  // evaluate_bcl_v1 -- and checks the barotropic state, ti_rk_bcl.F90:81-84)
-  DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qb, e->q, e->q, e->qp, 1));
+  // evaluate_bcl_v1 -- and checks the barotropic state, ti_rk_bcl.F90:81-84; the thickness averages
+  // of :78-80 are formed by its kernels on load, except with the quad-point LDG Laplacian, which
+  // reads the averaged qprime before them)
+  if (e->lapq_on) {
+    hipLaunchKernelGGL(dp_average_face_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp2, e->qp, e->dpp2, nl,
+                       e->qf2, e->qf, nf / 3);
+    DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qb, e->q, e->q, e->qp, 1));
+  } else {
+    DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qb, e->q, e->q, e->qp, 1, e->qp, e->qf));
+  }
   exchange_qp(e, e->qp);
   // ad_mlswe > 0 with the reference's corrector input leaves NaN layer momenta (hnumo_params)
   if (e->p.ad_mlswe > 0.0)

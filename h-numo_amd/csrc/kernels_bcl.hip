@@ -901,7 +901,9 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(64)
     mom_flux_face_kernel(DevMesh m, const double *qf, const double *facc, const double *gdpp_face,
-                         const double *gfacc, double *momL, double *momR, double *lap) {
+                         const double *gfacc, double *momL, double *momR, double *lap, const double *qf_avg0) {
+  // qf_avg0 (the corrector): the face thickness traces enter as 0.5*(qf_avg0 + qf) (component 1,
+  // ti_rk_bcl.F90:80), formed on load
   const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L;
   const size_t FQ = (size_t)F * NQ, FN = (size_t)F * NGL;
   BCL_MARK(3, 0) BCL_WALL(3, 6)
@@ -920,7 +922,10 @@ __global__ void __launch_bounds__(64)
   for (int t = tid; t < NGL * NGL; t += 64) s_psi[t] = m.basis[2 * NGL * NQ + NGL * NGL + t];
   for (int t = tid; t < L * 6 * NGL; t += 64) {
     const int k = t / (6 * NGL), r = t % (6 * NGL);
-    s_qf[k][r] = qf[((size_t)k * F + f) * NGL * 6 + r];
+    const size_t i = ((size_t)k * F + f) * NGL * 6 + r;
+    double v = qf[i];
+    if (qf_avg0 && r % 3 == 0) v = 0.5 * (qf_avg0[i] + v);
+    s_qf[k][r] = v;
   }
   for (int t = tid; t < FA_N * NQ; t += 64) s_fa[t] = facc[FACC_I(0, slot, 0) + t];
   for (int t = tid; t < 8 * NGL; t += 64) s_gf[t] = gfacc[GFACC_I(0, slot, 0) + t];
@@ -1193,7 +1198,10 @@ __global__ void __launch_bounds__(256, 3)
     mom_elem_kernel(DevMesh m, const double *qp_in, const double *qacc, const double *nacc, const double *dpp_graduv,
                     const double *dpprime_visc, const double *momL, const double *momR, const double *lapf,
                     const double *qb, const double *q_in, double *q, double *qp_out, int mode, const double *lapx,
-                    const double *dpp2, int *flag) {
+                    const double *dpp2, int *flag, const double *qp_avg0) {
+  // qp_avg0 (the corrector, with dpp2 == nullptr): the layer thicknesses qprime(1) enter as
+  // 0.5*(qp_avg0 + qp_in) (ti_rk_bcl.F90:78-79, formed on load) and the final qprime(1) is qp_in's
+  // own (dpp2 of :78, read back from qp_in)
   // q_in: the momenta entering the update (the predictor: q_df, its thicknesses already in q =
   // q_df2); mode 1 (the corrector) writes the step's final qprime straight into qp_out = qprime_df
   // (ti_rk_bcl.F90:81-84: thickness from dpp2 = the corrector's own, momenta from evaluate_bcl_v1)
@@ -1254,7 +1262,8 @@ __global__ void __launch_bounds__(256, 3)
   }
   for (int t = tid; t < L * 3 * P; t += BS) {
     int k = t / (3 * P), r = t % (3 * P);
-    s_qp[k][r % 3][r / 3] = qp_in[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
+    const size_t i = (size_t)k * 3 * npoin + (size_t)e * 3 * P + r;
+    s_qp[k][r % 3][r / 3] = (qp_avg0 && r % 3 == 0) ? 0.5 * (qp_avg0[i] + qp_in[i]) : qp_in[i];
     if (r % 3) s_qm2[k][r % 3 - 1][r / 3] = q_in[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
   }
   for (int t = tid; t < 5 * Q; t += BS) {
@@ -1827,7 +1836,7 @@ __global__ void __launch_bounds__(256, 3)
       qq[1] = nw[k][1];
       qq[2] = nw[k][2];
       double *o = qp_out + ((size_t)k * npoin + I) * 3;
-      o[0] = mode == 0 ? h[k] / ope : dpp2[(size_t)k * npoin + I];
+      o[0] = mode == 0 ? h[k] / ope : (qp_avg0 ? qp_in[((size_t)k * npoin + I) * 3] : dpp2[(size_t)k * npoin + I]);
       o[1] = uv[k][0] - b3 / b1;
       o[2] = uv[k][1] - b4 / b1;
     }
