@@ -96,6 +96,17 @@ struct hnumo_engine {
   TraceGranule *gtr[2] = {nullptr, nullptr};  // tagged face traces of the persistent sub-cycle
   unsigned long long *epoch = nullptr;        // tag epoch, bumped by every persistent sub-cycle launch
   unsigned *sub_done = nullptr;               // its finished-workgroup counter
+  unsigned *sub_arrive = nullptr;             // its residency rendezvous word (residency_rendezvous)
+  unsigned *steps_done = nullptr, *h_steps = nullptr;  // steps completed in a run (DevMesh::steps_done)
+  // residency of the persistent launch: the occupancy estimate (workgroups per CU, per summation
+  // mode), the CU count, and the outcome of the creation-time trial launch (1 resident, 0 not,
+  // -1 not run).  HNUMO_PERSIST_LDS_PAD (bytes of dynamic LDS per workgroup) and
+  // HNUMO_PERSIST_GUARD (0: no estimate, no trial; estimate; trial) exist to test the in-launch
+  // fallback and each check alone.
+  int occ_blocks[2] = {0, 0}, occ_ncu = 0, probe_ok[2] = {-1, -1};
+  int persist_pad = 0;
+  int persist_guard = 3;                      // bit 1: occupancy estimate, bit 2: trial launch
+  int persist_aborts = 0;                     // runs that found a persistent launch not co-resident
   StageArgs *d_stages[2] = {nullptr, nullptr};  // per-stage arguments: predictor (qp), corrector (qp2)
   // processor-face halo: the reference's own partition contract (face(8) = 0 faces listed per
   // neighbour rank in nbh_send_recv; p4est.c:1686-1712, mod_parallel).  NS shared-face slots in
@@ -143,6 +154,7 @@ static T *dalloc(hnumo_engine *eng, size_t n) {
 }
 
 static void face_exchange_qf(hnumo_engine *e, double *qf, int nc);
+static const double *face_exchange_lapq(hnumo_engine *e, const double *flux, int nb, int nq, int Q);
 static void face_exchange_gdpp(hnumo_engine *e);
 static void face_exchange_cdef(hnumo_engine *e);
 
@@ -173,29 +185,45 @@ struct Launch {
       hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, true>), dim3(n), dim3(StageCfg<NGL, NQ, true>::BS), 0, st, a);
   }
   static void subcycle(hnumo_engine *e, const StageArgs *stages, int ns) {
-    SubArgs sa{stages, ns, e->epoch, e->sub_done};
+    SubArgs sa{stages, ns, e->epoch, e->sub_done, e->sub_arrive, e->neg_flag};
     if (e->summation == HNUMO_SUM_REFERENCE)
       hipLaunchKernelGGL((btp_subcycle_kernel<NGL, NQ, false>), dim3(e->nelem_owned),
-                         dim3(StageCfg<NGL, NQ, false>::BS), 0, e->stream, sa);
+                         dim3(StageCfg<NGL, NQ, false>::BS), e->persist_pad, e->stream, sa);
     else
       hipLaunchKernelGGL((btp_subcycle_kernel<NGL, NQ, true>), dim3(e->nelem_owned), dim3(StageCfg<NGL, NQ, true>::BS),
-                         0, e->stream, sa);
+                         e->persist_pad, e->stream, sa);
   }
-  // can every workgroup of the persistent sub-cycle kernel be resident at once?
+  // can every workgroup of the persistent sub-cycle kernel be resident at once?  The occupancy
+  // estimate first; the launch itself then checks (residency_rendezvous) and the engine runs one
+  // stage-less trial launch per summation mode at creation (probe)
   static void occupancy(hnumo_engine *e, int ncu) {
     int nb0 = 0, nb1 = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb0, btp_subcycle_kernel<NGL, NQ, false>,
-                                                       StageCfg<NGL, NQ, false>::BS, 0);
+                                                       StageCfg<NGL, NQ, false>::BS, e->persist_pad);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb1, btp_subcycle_kernel<NGL, NQ, true>,
-                                                       StageCfg<NGL, NQ, true>::BS, 0);
+                                                       StageCfg<NGL, NQ, true>::BS, e->persist_pad);
     (void)hipGetLastError();
-    e->persistent_ok[0] = (long)nb0 * ncu >= e->nelem_owned;
+    e->occ_blocks[0] = nb0;
+    e->occ_blocks[1] = nb1;
+    e->occ_ncu = ncu;
+    const bool est = e->persist_guard & 1;
+    e->persistent_ok[0] = !est || (long)nb0 * ncu >= e->nelem_owned;
     // the slim arena keeps the bottom-layer qprime only for the first stage: the later ones need
     // the per-sub-cycle quad-point scratch
     if (StageCfg<NGL, NQ, false>::SLIM && e->m.botfr && !e->qpq) e->persistent_ok[0] = false;
-    e->persistent_ok[1] = (long)nb1 * ncu >= e->nelem_owned;
+    e->persistent_ok[1] = !est || (long)nb1 * ncu >= e->nelem_owned;
     e->regacc[0] = StageCfg<NGL, NQ, false>::REGACC;
     e->regacc[1] = StageCfg<NGL, NQ, true>::REGACC;
+  }
+  // the trial launch: the persistent grid with no stages, i.e. the residency rendezvous alone
+  static void probe(hnumo_engine *e, int sum) {
+    SubArgs sa{e->d_stages[0], 0, e->epoch, e->sub_done, e->sub_arrive, e->neg_flag};
+    if (sum == HNUMO_SUM_REFERENCE)
+      hipLaunchKernelGGL((btp_subcycle_kernel<NGL, NQ, false>), dim3(e->nelem_owned),
+                         dim3(StageCfg<NGL, NQ, false>::BS), e->persist_pad, e->stream, sa);
+    else
+      hipLaunchKernelGGL((btp_subcycle_kernel<NGL, NQ, true>), dim3(e->nelem_owned), dim3(StageCfg<NGL, NQ, true>::BS),
+                         e->persist_pad, e->stream, sa);
   }
   // face traces of elements [e0, e0+n) into their neighbours' slots
   static void grad_trace(hnumo_engine *e, const double *qb, double *gt, int e0, int n, TraceGranule *gtr = nullptr) {
@@ -233,15 +261,20 @@ struct Launch {
   static void lapq_btp(hnumo_engine *e, const double *qb, const double *qp) {
     hipLaunchKernelGGL((lapq_flux_kernel<NGL, NQ>), dim3(e->nelem), dim3(256), 0, e->stream, e->m, qb, qp, e->nacc,
                        e->dpq, e->lq_flux, 0, 0);
+    // processor faces: the neighbour's side-1 fluxes (create_communicator_quad,
+    // mod_laplacian_quad.F90:214)
+    const double *recv = face_exchange_lapq(e, e->lq_flux, 1, NQ, NQ * NQ);
     hipLaunchKernelGGL((lapq_apply_kernel<NGL, NQ>), dim3(e->nelem_owned, 1), dim3(64), 0, e->stream, e->m, e->lq_flux,
-                       e->lapq, e->fqLR, e->fqLR + e->FQ);
+                       e->lapq, e->fqLR, e->fqLR + e->FQ, recv);
   }
   // method_visc == 1, baroclinic: bcl_create_laplacian_v2's per-layer Laplacians of qprime
   static void lapq_bcl(hnumo_engine *e, const double *qp) {
     hipLaunchKernelGGL((lapq_flux_kernel<NGL, NQ>), dim3(e->nelem), dim3(256), 0, e->stream, e->m, nullptr, qp,
                        e->nacc, e->dpq, e->lq_flux, 1, 0);
+    // (bcl_create_communicator of flux_uv_visc_face, mod_laplacian_quad.F90:342)
+    const double *recv = face_exchange_lapq(e, e->lq_flux, e->L, NQ, NQ * NQ);
     hipLaunchKernelGGL((lapq_apply_kernel<NGL, NQ>), dim3(e->nelem_owned, e->L), dim3(64), 0, e->stream, e->m,
-                       e->lq_flux, e->lapq, e->fqLR, e->fqLR + e->FQ);
+                       e->lq_flux, e->lapq, e->fqLR, e->fqLR + e->FQ, recv);
   }
   // layer mass update (owned elements); produces dp' (e->dpp) for the consistency step
   // (q_in: the layer thicknesses entering the update; q: where they are written)
@@ -429,23 +462,18 @@ static const hnumo_engine::FNbr *peer_entry(hnumo_engine *peer, int rank) {
   return nullptr;
 }
 
-// Baroclinic face exchange on the engine stream (bcl_create_communicator,
-// create_rhs_communicator.F90:384-438): side 1 of every shared face -> the neighbour's side 2.
-// Face array element (side 1) of layer k, component c < nc, point p < nn of face f:
-// base[k*sk + c*sc + f*sf + p*sn]; side 2 at + s2.
-static void face_exchange(hnumo_engine *e, double *base, int nc, int nn, size_t sk, size_t sc, size_t sf, size_t sn,
-                          size_t s2) {
-  // (a rank without shared faces still takes part in a local group's barriers)
-  if (!e->face_halo || (e->NS == 0 && e->comm_mode != 1)) return;
-  const int L = e->L;
-  const size_t per = (size_t)L * nc * nn, tot = per * e->NS;
-  const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>((tot + 255) / 256, 1024));
-  if (e->comm_mode == 1) {  // local group: my previous message must have been read by every peer
+// (a rank without shared faces still takes part in a local group's barriers)
+static bool face_tx_skip(const hnumo_engine *e) { return !e->face_halo || (e->NS == 0 && e->comm_mode != 1); }
+
+// before packing bx_sbuf: in a local group my previous message must have been read by every peer
+static void face_tx_begin(hnumo_engine *e) {
+  if (e->comm_mode == 1)
     for (auto &n : e->fnb) (void)hipStreamWaitEvent(e->stream, group_peer(e, n.rank)->ev_bdone, 0);
-  }
-  if (tot)
-    hipLaunchKernelGGL(face_pack_kernel, dim3(blocks), dim3(256), 0, e->stream, e->bx_sbuf, base, e->d_sface, e->NS,
-                       L, nc, nn, sk, sc, sf, sn);
+}
+
+// the packed messages bx_sbuf (`per` doubles per shared face, slots in nbh_send_recv order) into
+// the neighbours' bx_rbuf slots of the same faces, on the engine stream
+static void face_tx(hnumo_engine *e, size_t per) {
   if (e->comm_mode == 2) {
     nccl_check(e, ncclGroupStart(), "ncclGroupStart");
     for (auto &n : e->fnb) {
@@ -469,11 +497,45 @@ static void face_exchange(hnumo_engine *e, double *base, int nc, int nn, size_t 
         e->comm_err = "local group: hipMemcpyAsync of a face message failed";
     }
     (void)hipEventRecord(e->ev_bdone, e->stream);
-    if (!e->group->barrier()) return;
+    (void)e->group->barrier();
   }
+}
+
+// Baroclinic face exchange on the engine stream (bcl_create_communicator,
+// create_rhs_communicator.F90:384-438): side 1 of every shared face -> the neighbour's side 2.
+// Face array element (side 1) of layer k, component c < nc, point p < nn of face f:
+// base[k*sk + c*sc + f*sf + p*sn]; side 2 at + s2.
+static void face_exchange(hnumo_engine *e, double *base, int nc, int nn, size_t sk, size_t sc, size_t sf, size_t sn,
+                          size_t s2) {
+  if (face_tx_skip(e)) return;
+  const int L = e->L;
+  const size_t per = (size_t)L * nc * nn, tot = per * e->NS;
+  const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>((tot + 255) / 256, 1024));
+  face_tx_begin(e);
+  if (tot)
+    hipLaunchKernelGGL(face_pack_kernel, dim3(blocks), dim3(256), 0, e->stream, e->bx_sbuf, base, e->d_sface, e->NS,
+                       L, nc, nn, sk, sc, sf, sn);
+  face_tx(e, per);
+  if (e->group && e->group->aborted) return;
   if (tot)
     hipLaunchKernelGGL(face_unpack_kernel, dim3(blocks), dim3(256), 0, e->stream, base, e->bx_rbuf, e->d_sface,
                        e->NS, L, nc, nn, sk, sc, sf, sn, s2);
+}
+
+// method_visc == 1: the LDG fluxes at the quad points of every processor face's local side ->
+// the neighbour (create_communicator_quad, create_rhs_communicator.F90:82-134, and
+// bcl_create_communicator of flux_uv_visc_face; pack_data_dg_quad, send_receive_bound.F90:215-270:
+// side 1 of each listed face, quad point by quad point).  Returns the receive buffer,
+// [NS][nb][4][NQ] (nb layer blocks), or NULL without processor faces.
+static const double *face_exchange_lapq(hnumo_engine *e, const double *flux, int nb, int nq, int Q) {
+  if (face_tx_skip(e)) return nullptr;
+  const size_t per = (size_t)nb * 4 * nq, tot = per * e->NS;
+  face_tx_begin(e);
+  if (tot)
+    hipLaunchKernelGGL(lapq_pack_kernel, dim3((unsigned)std::min<size_t>((tot + 255) / 256, 1024)), dim3(256), 0,
+                       e->stream, e->bx_sbuf, flux, e->d_sface, e->m.fel, e->fqLR, e->NS, nb, e->nelem, nq, Q);
+  face_tx(e, per);
+  return e->NS ? e->bx_rbuf : nullptr;
 }
 
 // qprime_df_face-like arrays qf(3,2,ngl,F,L) (QF macro): components [0,nc)
@@ -621,8 +683,9 @@ static int stage_table(hnumo_engine *e, const double *qp, std::vector<StageArgs>
 }
 
 // (method_visc == 1 needs its Laplacian kernels between the stages: per-stage launches)
+// (single rank only: its stage tables send every trace to an element slot)
 static bool use_persistent(const hnumo_engine *e) {
-  return e->comm_mode == 0 && !e->lapq_on && e->persistent_ok[e->summation];
+  return e->comm_mode == 0 && e->nranks == 1 && !e->face_halo && !e->lapq_on && e->persistent_ok[e->summation];
 }
 
 // ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:19-151) on device state qb_state
@@ -646,7 +709,7 @@ static void launch_subcycle(hnumo_engine *e, double *dst, const double *qp, bool
     if (timed && e->kernel_events) (void)hipEventRecord(e->evk1, e->stream);
     if (racc) return;
     cur = -1;  // (the last stage wrote dst)
-  } else if (e->face_halo) {
+  } else if (e->face_halo && !e->lapq_on) {
     // Processor-face halo, two streams (the overlap of mod_rhs_btp.F90:40-46): elements with a
     // processor face ("boundary", B) run on stream2, which then ships their new face traces to
     // the neighbours; the interior elements (I) run on the engine stream meanwhile.  Stage s:
@@ -676,13 +739,19 @@ static void launch_subcycle(hnumo_engine *e, double *dst, const double *qp, bool
     (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
     if (timed && e->kernel_events) (void)hipEventRecord(e->evk1, e->stream);
   } else {
+    // one stream: a single rank, the ghost-element halo, or the processor-face halo with the
+    // quad-point LDG (method_visc == 1), whose per-stage Laplacian needs the neighbours' face
+    // fluxes of the stage (create_communicator_quad) before any element's stage can run
+    if (e->face_halo) trace_exchange(e, e->gtrace[0], e->stream);  // the sub-cycle input's traces
     std::vector<StageArgs> st;
     cur = stage_table(e, qp, st);
     if (timed && e->kernel_events) (void)hipEventRecord(e->evk0, e->stream);
     for (const StageArgs &a : st) {
       if (e->lapq_on) DISPATCH(e, lapq_btp(e, a.qb_in, a.qprime));
       DISPATCH(e, stage(e, a));
-      if (a.write_trace && e->comm_mode) {
+      if (a.write_trace && e->face_halo) {
+        trace_exchange(e, a.trace_out, e->stream);
+      } else if (a.write_trace && e->comm_mode) {
         // ghosts take the owners' new state; their traces go into the owned elements' slots
         exchange_qb(e, a.qb_out);
         DISPATCH(e, grad_trace(e, a.qb_out, a.trace_out, e->nelem_owned, e->nelem - e->nelem_owned));
@@ -696,11 +765,9 @@ static void launch_subcycle(hnumo_engine *e, double *dst, const double *qp, bool
                      1.0 / (double)(K * NB), dst, cur >= 0 ? e->qbuf[cur] : dst, 1);
 }
 
-// the full ti_rk_bcl on device state (e->q, e->qb, e->qp)
-static void launch_step(hnumo_engine *e) {
-  const size_t n3 = 3 * (size_t)e->npoin * e->L, nf = 6 * e->FN * e->L, nl = (size_t)e->npoin * e->L;
-  int blocks = (int)std::min<size_t>((nl + 255) / 256, 4096);
-  // prediction (ti_rk_bcl.F90:43-57)
+// the prediction half of ti_rk_bcl (ti_rk_bcl.F90:43-57) on device state (e->q, e->qb, e->qp):
+// results in e->q2 (q_df2), e->qbp (qb after the sub-cycle), e->qp2 (qprime_df2)
+static void launch_predict(hnumo_engine *e) {
   launch_bcl_coeffs(e, e->qp, e->qf);
   launch_subcycle(e, e->qbp, e->qp);
   // (q_df2 = q_df, qprime_df2 = qprime_df, qprime_face2 = qprime_face (ti_rk_bcl.F90:53-55) without
@@ -712,6 +779,13 @@ static void launch_step(hnumo_engine *e) {
   DISPATCH(e, cons(e, e->q2, nullptr, 0));
   DISPATCH(e, momentum(e, e->qf, e->qp, e->qbp, e->q, e->q2, e->qp2, 0));
   exchange_qp(e, e->qp2);
+}
+
+// the full ti_rk_bcl on device state (e->q, e->qb, e->qp)
+static void launch_step(hnumo_engine *e) {
+  const size_t n3 = 3 * (size_t)e->npoin * e->L, nf = 6 * e->FN * e->L, nl = (size_t)e->npoin * e->L;
+  int blocks = (int)std::min<size_t>((nl + 255) / 256, 4096);
+  launch_predict(e);
   DISPATCH(e, extract(e, e->qp2, e->qf2, 0));
   // correction (ti_rk_bcl.F90:62-85)
   DISPATCH(e, bcl_coeffs(e, e->qp2, e->qf2, e->qp, e->qf));
@@ -752,6 +826,7 @@ void hnumo_engine_destroy(hnumo_engine *eng) {
   if (eng->graph) (void)hipGraphDestroy(eng->graph);
   for (void *ptr : eng->allocs) (void)hipFree(ptr);
   if (eng->h_neg) (void)hipHostFree(eng->h_neg);
+  if (eng->h_steps) (void)hipHostFree(eng->h_steps);
   if (eng->stream && eng->own_stream) (void)hipStreamDestroy(eng->stream);
   if (LocalGroup *g = eng->group) {
     // the destroyed engine cannot take part in exchanges any more; the last one out frees
@@ -841,8 +916,9 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   }
   if (par->method_visc == 1) {
     if (!mesh->imapl_q || !mesh->imapr_q) return fail(eng, HNUMO_ERR_INVALID, "method_visc==1 needs imapl_q/imapr_q");
-    if (halo && halo->nranks > 1)
-      return fail(eng, HNUMO_ERR_INVALID, "method_visc==1 (quad-point LDG) is single-rank only in this build");
+    if (halo && halo->nranks > 1 && !eng->face_halo)
+      return fail(eng, HNUMO_ERR_INVALID,
+                  "method_visc==1 (quad-point LDG) runs on one rank or on the processor-face halo, not on ghost elements");
   }
   if (par->shear_corrector != HNUMO_SHEAR_CORRECTOR_REFERENCE && par->shear_corrector != HNUMO_SHEAR_CORRECTOR_PREDICTED)
     return fail(eng, HNUMO_ERR_INVALID, "shear_corrector must be HNUMO_SHEAR_CORRECTOR_REFERENCE or _PREDICTED");
@@ -1169,7 +1245,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     eng->d_elB = dalloc<int>(eng, elB.size());
     eng->d_elI = dalloc<int>(eng, elI.size());
     eng->cdef = dalloc<double>(eng, 4 * FQ * L);
-    eng->bx_per_max = (size_t)L * std::max(5 * ngl, 2 * nq);
+    eng->bx_per_max = (size_t)L * std::max({5 * ngl, 2 * nq, eng->lapq_on ? 4 * nq : 0});
     eng->bx_sbuf = dalloc<double>(eng, eng->bx_per_max * NS);
     eng->bx_rbuf = dalloc<double>(eng, eng->bx_per_max * NS);
     if (eng->alloc_failed) return fail(eng, HNUMO_ERR_DEVICE, "hipMalloc failed (halo buffers)");
@@ -1262,12 +1338,17 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   m.gravity = par->gravity; m.cd = par->cd_mlswe; m.visc = par->visc_mlswe; m.dt = par->dt; m.dt_btp = par->dt_btp;
   m.botfr = par->botfr;
   m.ad = par->ad_mlswe; m.max_shear_dz = par->max_shear_dz; m.shear_corr = par->shear_corrector;
+  m.runflag = eng->neg_flag;
+  eng->steps_done = dalloc<unsigned>(eng, 1);
+  m.steps_done = eng->steps_done;
+  HIPCHK(hipHostMalloc((void **)&eng->h_steps, sizeof(unsigned)));
 
   // persistent sub-cycle: stage tables for the two sub-cycles of a step and the residency check
   if (supported_ngl(ngl) && eng->K <= 8) {
     eng->epoch = dalloc<unsigned long long>(eng, 1);
     eng->qsv = dalloc<double>(eng, (size_t)E * 8 * ngl * ngl);
     eng->sub_done = dalloc<unsigned>(eng, 1);
+    eng->sub_arrive = dalloc<unsigned>(eng, 1);
     for (int b = 0; b < 2; b++) eng->gtr[b] = dalloc<TraceGranule>(eng, (size_t)E * 32 * ngl);
     const double *qps[2] = {eng->qp, eng->qp2};
     for (int v = 0; v < 2; v++) {
@@ -1282,9 +1363,25 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     }
     const char *pe = getenv("HNUMO_PERSISTENT");
     if (!(pe && pe[0] == '0')) {
+      if (const char *pp = getenv("HNUMO_PERSIST_LDS_PAD")) eng->persist_pad = std::max(0, atoi(pp));
+      // HNUMO_PERSIST_GUARD: 0 none (the in-launch rendezvous alone), 'estimate', 'trial', 1 both
+      if (const char *pg = getenv("HNUMO_PERSIST_GUARD"))
+        eng->persist_guard = pg[0] == '0' ? 0 : pg[0] == 'e' ? 1 : pg[0] == 't' ? 2 : 3;
       int ncu = 0;
       HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, eng->device));
       DISPATCH(eng, occupancy(eng, ncu));
+      // the trial launches: what the dispatcher does, not what the estimate says, decides
+      for (int sm = 0; sm < 2 && (eng->persist_guard & 2); sm++) {
+        if (!eng->persistent_ok[sm] || eng->comm_mode != 0 || eng->nranks != 1) continue;
+        HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
+        DISPATCH(eng, probe(eng, sm));
+        HIPCHK(hipMemcpyAsync(eng->h_neg, eng->neg_flag, sizeof(int), hipMemcpyDeviceToHost, eng->stream));
+        HIPCHK(hipStreamSynchronize(eng->stream));
+        HIPCHK(hipGetLastError());
+        eng->probe_ok[sm] = (*eng->h_neg & RUN_ABORT) ? 0 : 1;
+        if (!eng->probe_ok[sm]) eng->persistent_ok[sm] = false;
+        HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
+      }
     }
   }
   // tau_wind_ave = (N_btp times tau_wind summed) / N_btp (mod_rk_mlswe.F90:148) is constant: formed
@@ -1350,12 +1447,27 @@ static int ensure_graph(hnumo_engine *eng) {
 }
 
 // error bits of the device flag word (neg_flag): 1 negative thickness, 2 non-finite
-// state, 8 a persistent sub-cycle trace wait timed out (workgroups not co-resident)
+// state, 8 a persistent sub-cycle trace wait timed out, 16 (RUN_ABORT) a persistent launch found
+// its workgroups not co-resident -- handled by the callers (persistent_abort), never an error
 static int flag_error(hnumo_engine *eng, int flags) {
   if (flags & 1) return fail(eng, HNUMO_ERR_NEGATIVE_THICKNESS, "Negative mass in thickness at some points");
   if (flags & 2) return fail(eng, HNUMO_ERR_NONFINITE, "non-finite barotropic state");
   if (flags & 8) return fail(eng, HNUMO_ERR_DEVICE, "persistent sub-cycle: a trace granule wait timed out");
   return 0;
+}
+
+// A persistent launch of the run was not co-resident (RUN_ABORT): it did no work, and neither
+// did anything after it that writes the step state, so the state is that of the last completed
+// step.  The engine drops the persistent path for good (the captured step holds it) and the
+// caller repeats what is left on per-stage launches.
+static void persistent_abort(hnumo_engine *eng) {
+  eng->persistent_ok[0] = eng->persistent_ok[1] = false;
+  eng->persist_aborts++;
+  if (eng->graph_exec) (void)hipGraphExecDestroy(eng->graph_exec);
+  if (eng->graph) (void)hipGraphDestroy(eng->graph);
+  eng->graph_exec = nullptr;
+  eng->graph = nullptr;
+  if (eng->comm_mode != 1) eng->no_graph = false;
 }
 
 static int transport_error(hnumo_engine *eng) {
@@ -1382,20 +1494,35 @@ static int launch_steps(hnumo_engine *eng, int nsteps) {
 
 static int run_steps(hnumo_engine *eng, int nsteps) {
   HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
+  HIPCHK(hipMemsetAsync(eng->steps_done, 0, sizeof(unsigned), eng->stream));
   int rc = launch_steps(eng, nsteps);
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(eng->h_neg, eng->neg_flag, sizeof(int), hipMemcpyDeviceToHost, eng->stream));
+  HIPCHK(hipMemcpyAsync(eng->h_steps, eng->steps_done, sizeof(unsigned), hipMemcpyDeviceToHost, eng->stream));
   HIPCHK(hipStreamSynchronize(eng->stream));
   HIPCHK(hipGetLastError());
   if ((rc = transport_error(eng))) return rc;
+  if ((*eng->h_neg & RUN_ABORT) && !use_persistent(eng)) return fail(eng, HNUMO_ERR_DEVICE, "run aborted off the persistent path");
+  if (*eng->h_neg & RUN_ABORT) {
+    const int done = (int)*eng->h_steps;
+    persistent_abort(eng);
+    return done < nsteps ? run_steps(eng, nsteps - done) : 0;
+  }
   return flag_error(eng, *eng->h_neg);
+}
+
+// A multi-rank engine exchanges halos inside these calls: it needs its RCCL transport (a local
+// group's engines run together, through hnumo_group_ti_rk_bcl only)
+static int component_transport_check(hnumo_engine *eng) {
+  if (eng->comm_mode == 1) return fail(eng, HNUMO_ERR_INVALID, "engine is in a local group: use hnumo_group_ti_rk_bcl");
+  if (eng->nranks > 1 && eng->comm_mode == 0)
+    return fail(eng, HNUMO_ERR_INVALID, "multi-rank engine without transport (comm_id or hnumo_local_group)");
+  return 0;
 }
 
 int hnumo_ti_rk_bcl(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df) {
   if (!eng) return HNUMO_ERR_INVALID;
-  if (eng->comm_mode == 1) return fail(eng, HNUMO_ERR_INVALID, "engine is in a local group: use hnumo_group_ti_rk_bcl");
-  if (eng->nranks > 1 && eng->comm_mode == 0)
-    return fail(eng, HNUMO_ERR_INVALID, "multi-rank engine without transport (comm_id or hnumo_local_group)");
+  if (int rc = component_transport_check(eng)) return rc;
   HIPCHK(hipSetDevice(eng->device));
   if (!eng->resident || !eng->uploaded) {
     int rc = upload_state(eng, q_df, qb_df, qprime_df);
@@ -1435,6 +1562,34 @@ int hnumo_get_summation(hnumo_engine *eng) { return eng ? eng->summation : -1; }
 
 int hnumo_stage_path(hnumo_engine *eng) { return eng ? (use_persistent(eng) ? 1 : 0) : -1; }
 
+extern "C++" template <int NGL, int NQ>
+static int subcycle_lds_bytes(const hnumo_engine *e) {
+  hipFuncAttributes fa{};
+  if (e->summation == HNUMO_SUM_REFERENCE)
+    (void)hipFuncGetAttributes(&fa, (const void *)btp_subcycle_kernel<NGL, NQ, false>);
+  else
+    (void)hipFuncGetAttributes(&fa, (const void *)btp_subcycle_kernel<NGL, NQ, true>);
+  return (int)fa.sharedSizeBytes + e->persist_pad;
+}
+
+int hnumo_persistent_info(hnumo_engine *eng, int32_t *out) {
+  if (!eng || !out) return HNUMO_ERR_INVALID;
+  int lds = 0;
+  switch (eng->ngl) {
+    case 3: lds = subcycle_lds_bytes<3, 5>(eng); break;
+    case 4: lds = subcycle_lds_bytes<4, 7>(eng); break;
+    case 5: lds = subcycle_lds_bytes<5, 9>(eng); break;
+    case 6: lds = subcycle_lds_bytes<6, 11>(eng); break;
+    case 8: lds = subcycle_lds_bytes<8, 15>(eng); break;
+    default: break;
+  }
+  (void)hipGetLastError();
+  const int32_t v[8] = {use_persistent(eng) ? 1 : 0, eng->occ_blocks[0], eng->occ_blocks[1], eng->occ_ncu,
+                        eng->probe_ok[0], eng->probe_ok[1], eng->persist_aborts, lds};
+  std::memcpy(out, v, sizeof(v));
+  return 0;
+}
+
 #if HNUMO_BCL_PROF
 // diagnostics build only (not part of the ABI): the element kernels' phase clocks, see g_bcl_prof
 int hnumo_bcl_prof(unsigned long long *dst, int n) {
@@ -1451,8 +1606,10 @@ int hnumo_sync(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df
 
 int hnumo_btp_bcl_coeffs(hnumo_engine *eng, const double *qprime_df) {
   if (!eng) return HNUMO_ERR_INVALID;
+  int rc = component_transport_check(eng);
+  if (rc) return rc;
   HIPCHK(hipSetDevice(eng->device));
-  int rc = upload_state(eng, nullptr, nullptr, qprime_df);
+  rc = upload_state(eng, nullptr, nullptr, qprime_df);
   if (rc) return rc;
   launch_bcl_coeffs(eng, eng->qp, eng->qf);
   HIPCHK(hipStreamSynchronize(eng->stream));
@@ -1462,19 +1619,58 @@ int hnumo_btp_bcl_coeffs(hnumo_engine *eng, const double *qprime_df) {
 
 int hnumo_ti_barotropic_ssprk(hnumo_engine *eng, double *qb_df, const double *qprime_df) {
   if (!eng) return HNUMO_ERR_INVALID;
-  HIPCHK(hipSetDevice(eng->device));
-  int rc = upload_state(eng, nullptr, qb_df, qprime_df);
+  int rc = component_transport_check(eng);
   if (rc) return rc;
-  launch_subcycle(eng, eng->qbp, eng->qp);
+  HIPCHK(hipSetDevice(eng->device));
+  rc = upload_state(eng, nullptr, qb_df, qprime_df);
+  if (rc) return rc;
+  for (;;) {
+    HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
+    launch_subcycle(eng, eng->qbp, eng->qp);
+    HIPCHK(hipMemcpyAsync(eng->h_neg, eng->neg_flag, sizeof(int), hipMemcpyDeviceToHost, eng->stream));
+    HIPCHK(hipStreamSynchronize(eng->stream));
+    HIPCHK(hipGetLastError());
+    if ((rc = transport_error(eng))) return rc;
+    if (!(*eng->h_neg & RUN_ABORT) || !use_persistent(eng)) break;
+    persistent_abort(eng);  // (the launch did no work: qb is still the input)
+  }
+  if ((rc = flag_error(eng, *eng->h_neg & ~RUN_ABORT))) return rc;
   launch_copy(eng, eng->qb, eng->qbp, 4 * (size_t)eng->npoin);
-  HIPCHK(hipGetLastError());
   return download_state(eng, nullptr, qb_df, nullptr);
+}
+
+int hnumo_predict(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df) {
+  if (!eng) return HNUMO_ERR_INVALID;
+  int rc = component_transport_check(eng);
+  if (rc) return rc;
+  HIPCHK(hipSetDevice(eng->device));
+  rc = upload_state(eng, q_df, qb_df, qprime_df);
+  if (rc) return rc;
+  for (;;) {
+    HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
+    launch_predict(eng);
+    HIPCHK(hipMemcpyAsync(eng->h_neg, eng->neg_flag, sizeof(int), hipMemcpyDeviceToHost, eng->stream));
+    HIPCHK(hipStreamSynchronize(eng->stream));
+    HIPCHK(hipGetLastError());
+    if ((rc = transport_error(eng))) return rc;
+    if (!(*eng->h_neg & RUN_ABORT) || !use_persistent(eng)) break;
+    persistent_abort(eng);  // (the predictor writes only q_df2, qbp, qprime_df2: redo it)
+  }
+  if ((rc = flag_error(eng, *eng->h_neg & ~RUN_ABORT))) return rc;
+  const size_t n3 = 3 * (size_t)eng->npoin * eng->L;
+  HIPCHK(hipMemcpyAsync(q_df, eng->q2, n3 * 8, hipMemcpyDeviceToHost, eng->stream));
+  HIPCHK(hipMemcpyAsync(qb_df, eng->qbp, 4 * (size_t)eng->npoin * 8, hipMemcpyDeviceToHost, eng->stream));
+  HIPCHK(hipMemcpyAsync(qprime_df, eng->qp2, n3 * 8, hipMemcpyDeviceToHost, eng->stream));
+  HIPCHK(hipStreamSynchronize(eng->stream));
+  return 0;
 }
 
 int hnumo_create_rhs_btp(hnumo_engine *eng, double *rhs, const double *qb_df, const double *qprime_df) {
   if (!eng) return HNUMO_ERR_INVALID;
+  int rc = component_transport_check(eng);
+  if (rc) return rc;
   HIPCHK(hipSetDevice(eng->device));
-  int rc = upload_state(eng, nullptr, qb_df, qprime_df);
+  rc = upload_state(eng, nullptr, qb_df, qprime_df);
   if (rc) return rc;
   subcycle_prologue(eng, eng->qb, nullptr, true);  // zeroed time averages (qbuf[0] is the rhs-only output slot)
   DISPATCH(eng, grad_trace(eng, eng->qb, eng->gtrace[0], 0, eng->nelem));
@@ -1647,6 +1843,11 @@ int hnumo_bench_steps(hnumo_engine *eng, int nsteps, double *ms_total, double *m
   HIPCHK(hipGetLastError());
   // a timed run whose state went bad (or whose persistent hand-offs timed out) is no result
   if ((rc = transport_error(eng))) return rc;
+  if ((*eng->h_neg & RUN_ABORT) && use_persistent(eng)) {
+    // (not co-resident: drop the persistent path and time the run again on per-stage launches)
+    persistent_abort(eng);
+    return hnumo_bench_steps(eng, nsteps, ms_total, ms_kernel_avg, kernel_launches);
+  }
   if ((rc = flag_error(eng, *eng->h_neg))) return rc;
   float ms = 0.f;
   HIPCHK(hipEventElapsedTime(&ms, eng->ev0, eng->ev1));
@@ -1674,6 +1875,7 @@ int hnumo_time_stage_kernel(hnumo_engine *eng, int nsubcycles, double *ms_kernel
   // the corrector sub-cycle of the current device state, on a scratch copy of qb
   const bool ke = eng->kernel_events;
   eng->kernel_events = true;
+  HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
   double total = 0.0;
   for (int s = 0; s < nsubcycles; s++) {
     launch_subcycle(eng, eng->qbp, eng->qp, true);
@@ -1686,6 +1888,11 @@ int hnumo_time_stage_kernel(hnumo_engine *eng, int nsubcycles, double *ms_kernel
   HIPCHK(hipMemcpyAsync(eng->h_neg, eng->neg_flag, sizeof(int), hipMemcpyDeviceToHost, eng->stream));
   HIPCHK(hipStreamSynchronize(eng->stream));
   HIPCHK(hipGetLastError());
+  if ((*eng->h_neg & RUN_ABORT) && use_persistent(eng)) {
+    persistent_abort(eng);
+    HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
+    return hnumo_time_stage_kernel(eng, nsubcycles, ms_kernel_avg);
+  }
   int rc = transport_error(eng);
   if (!rc) rc = flag_error(eng, *eng->h_neg & 8);
   if (rc) return rc;

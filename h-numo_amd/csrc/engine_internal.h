@@ -129,6 +129,16 @@ struct DevMesh {
   // element slots, then the send slots the stage writes processor-face traces into, then the
   // receive slots the transport fills)
   const int *etsrc;
+  // the run's device flag word (engine neg_flag): a persistent sub-cycle that found its
+  // workgroups not co-resident sets RUN_ABORT and did no work; the kernels that write the step's
+  // final state (mass_elem, cons_elem, mom_elem) then leave it untouched, so the host can redo
+  // the step on per-stage launches.  steps_done counts the steps whose corrector completed.
+  const int *runflag;
+  unsigned *steps_done;
 };
+
+// device flag word bits (engine.hip flag_error): 1 negative thickness, 2 non-finite state,
+// 8 a persistent trace wait timed out, 16 a persistent launch was not co-resident (no work done)
+constexpr int RUN_ABORT = 16;
 
 }  // namespace hnumo

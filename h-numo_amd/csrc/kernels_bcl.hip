@@ -728,6 +728,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     s_qm[c][t % Q] = m.qstat[(c < 4 ? QS_EX + c : QS_W) * (size_t)npq + (size_t)e * Q + t % Q];
   }
   __syncthreads();
+  if (*m.runflag & RUN_ABORT) return;  // (a persistent sub-cycle of this run did no work: DevMesh)
   BCL_MARK(0, 1)
   for (int q = tid; q < Q; q += BS) {
     const int iq = q % NQ, jq = q / NQ;
@@ -831,6 +832,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     s_qm[c][t % Q] = m.qstat[(c < 4 ? QS_EX + c : QS_W) * (size_t)npq + (size_t)e * Q + t % Q];
   }
   __syncthreads();
+  if (*m.runflag & RUN_ABORT) return;  // (a persistent sub-cycle of this run did no work: DevMesh)
   BCL_MARK(1, 1)
   for (int q = tid; q < Q; q += BS) {
     const int iq = q % NQ, jq = q / NQ;
@@ -1275,6 +1277,9 @@ __global__ void __launch_bounds__(256, 3)
     s_nm[c][t % P] = m.nstat[(c < 4 ? NS_EX + c : NS_W) * (size_t)npoin + (size_t)e * P + t % P];
   }
   __syncthreads();
+  if (*m.runflag & RUN_ABORT) return;  // (a persistent sub-cycle of this run did no work: DevMesh)
+  // the corrector of a completed step (mode 1) counts it: the host's retry point after an abort
+  if (mode == 1 && e == 0 && tid == 0 && m.steps_done) atomicAdd(m.steps_done, 1u);
   BCL_MARK(2, 1)
 
   // ---- 1: per (layer, quad point) interpolations of dp', u', v', u*dp, v*dp (reference

@@ -1814,7 +1814,42 @@ struct SubArgs {
   int NS;
   unsigned long long *epoch;       // tag base of this launch; the last workgroup to finish bumps it
   unsigned *done;                  // finished-workgroup counter (back to 0 after every launch)
+  unsigned *arrive;                // residency rendezvous word (back to 0 after every launch)
+  int *err;                        // the run's flag word: RUN_ABORT (see residency_rendezvous)
 };
+
+// Residency rendezvous of a persistent launch (one thread per workgroup).  The sub-cycle's
+// workgroups wait on each other's traces, so they must all be resident at once; whatever the
+// occupancy estimate said at engine creation (co-resident work of another process, a CU count
+// or LDS allocation granule the estimate did not see), a launch whose workgroups are not all
+// resident must end, not spin.  Every workgroup adds 1 to the arrival word and waits until the
+// count reaches the grid size.  A workgroup that waited RDV_TICKS (constant 100 MHz clock) sets
+// RDV_ABORT with a compare-and-swap -- only while the count is still short, so the outcome is
+// one for the whole launch: the grid-th arrival precedes any abort (every workgroup proceeds)
+// or an abort precedes it (every workgroup, including the ones dispatched later as the aborting
+// ones leave, sees the bit and leaves without work).  An abort also sets RUN_ABORT in the run's
+// flag word; the later launches of the same run see it and leave at once.  Returns true: go.
+constexpr unsigned RDV_ABORT = 0x80000000u;
+constexpr unsigned long long RDV_TICKS = 2000000ull;  // 20 ms; a full grid dispatches in ~0.05 ms
+__device__ __forceinline__ bool residency_rendezvous(unsigned *arrive, int *err, unsigned grid) {
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & RUN_ABORT) return false;
+  const unsigned old = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old & RDV_ABORT) return false;
+  if (old + 1 == grid) return true;
+  const unsigned long long t0 = wall_clock64();
+  for (;;) {
+    unsigned w = __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (w & RDV_ABORT) return false;
+    if (w == grid) return true;
+    if (wall_clock64() - t0 > RDV_TICKS &&
+        __hip_atomic_compare_exchange_strong(arrive, &w, w | RDV_ABORT, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT)) {
+      __hip_atomic_fetch_or(err, RUN_ABORT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
 
 template <int NGL, int NQ, bool SF>
 __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ, SF>::MINW))
@@ -1826,11 +1861,15 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
   const unsigned long long ep = *sa.epoch;
   typedef const __attribute__((address_space(4))) StageArgs CStageArgs;
   CStageArgs *tab = (CStageArgs *)sa.stages;
+  __shared__ int s_go;
+  if (tid == 0) s_go = residency_rendezvous(sa.arrive, sa.err, gridDim.x);
+  __syncthreads();
+  const int NS = s_go ? sa.NS : 0;  // (not resident: no stage, straight to the exit count)
   double pacc[16];  // this thread's time averages (StageCfg::REGACC)
 #pragma unroll
   for (int k = 0; k < 16; k++) pacc[k] = 0.0;
 #pragma unroll 1
-  for (int stage = 0; stage < sa.NS; stage++) {
+  for (int stage = 0; stage < NS; stage++) {
     if (stage > 0) __syncthreads();
     // opaque per stage: keeps the body's per-thread index math from being hoisted out of the
     // stage loop (it would stay live across every phase)
@@ -1840,11 +1879,13 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
     stage_body<NGL, NQ, SF, true>(tab[stage], s_arena, s_prof, stage == 0, e_s, tid_s, ep, pacc);
   }
   // the next launch's tags: every workgroup read the epoch at its start, so the last one to
-  // finish (agent-scope counter) moves it on and resets the counter
+  // finish (agent-scope counter) moves it on and resets the counters (every workgroup has passed
+  // the rendezvous before it counts itself out)
   if (tid == 0) {
     const unsigned prev = __hip_atomic_fetch_add(sa.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev == gridDim.x - 1) {
       __hip_atomic_store(sa.epoch, ep + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sa.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(sa.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }

@@ -113,9 +113,12 @@ __global__ void __launch_bounds__(256) lapq_flux_kernel(DevMesh m, const double 
 // with the face values of :156-212 (neighbour quad point, or the wall reflection) and the
 // central flux beta = 0.5.  fqL/fqR [F][NQ]: element-local quad point of face quad point iq
 // on the face's left / right element (imapl_q / imapr_q).
+// recv (processor-face halo): the neighbours' side-1 fluxes of the shared faces, [NS][nb][4][NQ]
+// (lapq_pack_kernel on the other rank), the processor face's side 2 (create_nbhs_face_quad,
+// create_rhs_dynamics_flux.F90:61-100); NULL on a single rank.
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(64) lapq_apply_kernel(DevMesh m, const double *flux, double *lap, const int *fqL,
-                                                        const int *fqR) {
+                                                        const int *fqR, const double *recv) {
   constexpr int P = NGL * NGL, Q = NQ * NQ, ERS = EREC_SIZE(NGL);
   const int e = blockIdx.x, k = blockIdx.y, tid = threadIdx.x, E = m.nelem;
   const size_t npoin = m.npoin, npq = m.npoin_q, FQ = (size_t)m.nface * NQ;
@@ -163,6 +166,11 @@ __global__ void __launch_bounds__(64) lapq_apply_kernel(DevMesh m, const double 
           const int qn = side == 0 ? fqR[fq] : fqL[fq];
 #pragma unroll
           for (int v = 0; v < 4; v++) oth[v] = fk[((size_t)nb * 4 + v) * Q + qn];
+        } else if (er == 0 && recv) {
+          // processor face (the local element is its left side): shared slot (nb - E)*4 + nblf
+          const size_t sl = (size_t)(nb - E) * 4 + s_er[EREC_NBLF + lf];
+#pragma unroll
+          for (int v = 0; v < 4; v++) oth[v] = recv[((sl * gridDim.y + k) * 4 + v) * NQ + iq];
         } else {
 #pragma unroll
           for (int v = 0; v < 4; v++) oth[v] = own[v];
@@ -184,6 +192,19 @@ __global__ void __launch_bounds__(64) lapq_apply_kernel(DevMesh m, const double 
       }
     }
     lap[((size_t)k * 2 + c) * npoin + (size_t)e * P + p] = acc;
+  }
+}
+
+// Processor-face message of the LDG fluxes (pack_data_dg_quad, send_receive_bound.F90:215-270):
+// buf[s][k][v][iq] = flux of layer block k, component v at the quad point of face sface[s]'s
+// side 1 (its left, local element) that face quad point iq maps to (imapl_q)
+__global__ void lapq_pack_kernel(double *buf, const double *flux, const int *sface, const int *fel, const int *fqL,
+                                 int NS, int nb, int E, int NQ, int Q) {
+  const size_t n = (size_t)NS * nb * 4 * NQ, st = (size_t)gridDim.x * blockDim.x;
+  for (size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += st) {
+    const int iq = (int)(t % NQ), v = (int)((t / NQ) % 4), k = (int)((t / (4 * (size_t)NQ)) % nb);
+    const int s = (int)(t / (4 * (size_t)NQ * nb)), f = sface[s];
+    buf[t] = flux[(((size_t)k * E + fel[f]) * 4 + v) * Q + fqL[(size_t)f * NQ + iq]];
   }
 }
 

@@ -41,6 +41,7 @@ def lib():
         L.hnumo_last_error.restype = C.c_char_p
         L.hnumo_ti_rk_bcl.argtypes = [vp, dp, dp, dp]
         L.hnumo_ti_barotropic_ssprk.argtypes = [vp, dp, dp]
+        L.hnumo_predict.argtypes = [vp, dp, dp, dp]
         L.hnumo_btp_bcl_coeffs.argtypes = [vp, dp]
         L.hnumo_create_rhs_btp.argtypes = [vp, dp, dp, dp]
         L.hnumo_get_field.argtypes = [vp, C.c_char_p, dp, C.c_int64]
@@ -58,6 +59,7 @@ def lib():
         L.hnumo_get_summation.restype = C.c_int
         L.hnumo_stage_path.argtypes = [vp]
         L.hnumo_stage_path.restype = C.c_int
+        L.hnumo_persistent_info.argtypes = [vp, C.POINTER(C.c_int32)]
         _lib = L
     return _lib
 
@@ -126,6 +128,11 @@ class Engine:
     def ti_rk_bcl(self, q, qb, qp):
         self._check(lib().hnumo_ti_rk_bcl(self.h, *self._state_ptrs(q, qb, qp)))
 
+    # = the prediction half of ti_rk_bcl (ti_rk_bcl.F90:43-57): q, qb, qp become q_df2, the
+    # sub-cycled qb_df and qprime_df2
+    def predict(self, q, qb, qp):
+        self._check(lib().hnumo_predict(self.h, *self._state_ptrs(q, qb, qp)))
+
     def btp_bcl_coeffs(self, qp):
         self._check(lib().hnumo_btp_bcl_coeffs(self.h, _dp(qp, self._sizes()[2], "qprime_df")))
 
@@ -158,6 +165,15 @@ class Engine:
     def stage_path(self) -> str:
         """'persistent' (one launch per sub-cycle) or 'per-stage' (one launch per stage)."""
         return "persistent" if lib().hnumo_stage_path(self.h) == 1 else "per-stage"
+
+    @property
+    def persistent_info(self) -> dict:
+        """Residency of the persistent sub-cycle launch (hnumo_persistent_info)."""
+        out = (C.c_int32 * 8)()
+        self._check(lib().hnumo_persistent_info(self.h, out))
+        v = list(out)
+        return {"persistent": v[0] == 1, "occupancy_blocks_per_cu": (v[1], v[2]), "cus": v[3],
+                "trial_launch": (v[4], v[5]), "fallbacks": v[6], "lds_bytes_per_workgroup": v[7]}
 
     def set_resident(self, on: bool):
         self._check(lib().hnumo_set_resident(self.h, int(on)))

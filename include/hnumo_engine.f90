@@ -17,7 +17,7 @@ module hnumo_engine_c
         HNUMO_ERR_NONFINITE = 2, HNUMO_ERR_DEVICE = 3, HNUMO_ERR_INVALID = 4
     integer(c_int32_t), parameter, public :: HNUMO_SHEAR_CORRECTOR_REFERENCE = 0, &
         HNUMO_SHEAR_CORRECTOR_PREDICTED = 1
-    integer(c_int), parameter, public :: HNUMO_ABI_EXPECTED = 5   ! must equal hnumo_abi_version()
+    integer(c_int), parameter, public :: HNUMO_ABI_EXPECTED = 6   ! must equal hnumo_abi_version()
     integer(c_int), parameter, public :: HNUMO_SUM_REFERENCE = 0, HNUMO_SUM_FACTORED = 1
 
     ! = hnumo_mesh_desc (mod_grid, mod_face, mod_basis, mod_metrics; optional dense tables)
@@ -82,7 +82,8 @@ module hnumo_engine_c
     public :: hnumo_engine_create, hnumo_engine_destroy, hnumo_abi_version, hnumo_ti_rk_bcl, &
         hnumo_ti_barotropic_ssprk, hnumo_btp_bcl_coeffs, hnumo_create_rhs_btp, hnumo_get_field_c, &
         hnumo_set_resident, hnumo_sync, hnumo_last_error_c, hnumo_last_error, hnumo_get_field, &
-        hnumo_set_summation, hnumo_get_summation, hnumo_stage_path, hnumo_rccl_unique_id
+        hnumo_set_summation, hnumo_get_summation, hnumo_stage_path, hnumo_persistent_info, hnumo_predict, &
+        hnumo_rccl_unique_id
 
     interface
         integer(c_int) function hnumo_engine_create(mesh, statics, params, halo, device, eng) &
@@ -179,6 +180,20 @@ module hnumo_engine_c
             import :: c_int, c_ptr
             type(c_ptr), value :: eng
         end function hnumo_stage_path
+
+        ! residency of the persistent launch, out(8): see hnumo_engine.h
+        integer(c_int) function hnumo_persistent_info(eng, out) bind(C, name='hnumo_persistent_info')
+            import :: c_int, c_int32_t, c_ptr
+            type(c_ptr), value :: eng
+            integer(c_int32_t), intent(out) :: out(8)
+        end function hnumo_persistent_info
+
+        ! the prediction half of ti_rk_bcl (ti_rk_bcl.F90:43-57): out q_df2, qb_df, qprime_df2
+        integer(c_int) function hnumo_predict(eng, q_df, qb_df, qprime_df) bind(C, name='hnumo_predict')
+            import :: c_int, c_ptr, c_double
+            type(c_ptr), value :: eng
+            real(c_double), intent(inout) :: q_df(*), qb_df(*), qprime_df(*)
+        end function hnumo_predict
 
         integer(c_int) function hnumo_sync(eng, q_df, qb_df, qprime_df) bind(C, name='hnumo_sync')
             import :: c_int, c_ptr, c_double

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define HNUMO_ABI_VERSION 5
+#define HNUMO_ABI_VERSION 6
 
 enum {
   HNUMO_OK = 0,
@@ -194,6 +194,11 @@ int hnumo_ti_barotropic_ssprk(hnumo_engine *eng, double *qb_df, const double *qp
  *   and qprime_df_face from extract_qprime_df_face (ti_rk_bcl.F90:43-50).           */
 int hnumo_btp_bcl_coeffs(hnumo_engine *eng, const double *qprime_df);
 
+/* = the prediction half of ti_rk_bcl (ti_rk_bcl.F90:43-57): btp_bcl_coeffs_qdf, the
+ *   barotropic sub-cycle, momentum_mass (ABI v6).  In: the step-start state; out: q_df2,
+ *   qb_df after the sub-cycle, qprime_df2 (the reference's arrays after :57).           */
+int hnumo_predict(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df);
+
 /* = create_rhs_btp(rhs, qb_df, qprime_df) (mod_rhs_btp.F90:28-59); rhs(3,npoin).    */
 int hnumo_create_rhs_btp(hnumo_engine *eng, double *rhs, const double *qb_df,
                          const double *qprime_df);
@@ -227,6 +232,17 @@ int hnumo_get_summation(hnumo_engine *eng);
  * unless HNUMO_PERSISTENT=0 at create), 0 = one launch per stage (btp_stage_kernel).
  * Both give the same bits.                                                            */
 int hnumo_stage_path(hnumo_engine *eng);
+
+/* Residency of the persistent sub-cycle launch (ABI v6).  The launch is used only when
+ * every element's workgroup can be resident at once: the occupancy estimate says so, a
+ * stage-less trial launch at create finds all workgroups resident, and every launch
+ * checks again (a rendezvous that gives up after 20 ms instead of waiting on a workgroup
+ * that cannot start).  A launch that gives up does no work; the engine then drops the
+ * persistent path and repeats the affected steps on per-stage launches (same bits).
+ * out[8] = {stage path (as hnumo_stage_path), estimated workgroups per CU (reference /
+ * factored summation), CU count, trial launch outcome (reference / factored: 1 resident,
+ * 0 not, -1 not run), runs that fell back, LDS bytes per workgroup}.                   */
+int hnumo_persistent_info(hnumo_engine *eng, int32_t *out8);
 
 /* RCCL unique id (128 bytes) for hnumo_halo_desc.comm_id: generated by one rank and
  * broadcast by the host (MPI / torch.distributed) before hnumo_engine_create.        */

@@ -40,8 +40,11 @@ if [ $left -ne 0 ]; then
   echo "reference build failed; see $OBJ/*.err" >&2; exit 1
 fi
 $FC $FLAGS -I. -c "$HERE/ref_driver.F90" -o ref_driver.o
-REFOBJ=$(ls *.o | grep -v -e '^ref_driver.o$' -e '^dropin_driver.o$' -e '^hnumo_')
-$FC -O2 -o "$OUT/ref_driver" ref_driver.o $REFOBJ \
+# -finit-real=zero for the one never-assigned automatic array the path reads (zero_init_wrap.c)
+gcc -O2 -c "$HERE/zero_init_wrap.c" -o zero_init_wrap.o
+WRAP="-Wl,--wrap=_QMmod_create_rhs_mlswePrhs_layer_shear_stress"
+REFOBJ=$(ls *.o | grep -v -e '^ref_driver.o$' -e '^dropin_driver.o$' -e '^hnumo_' -e '^zero_init_wrap.o$')
+$FC -O2 -o "$OUT/ref_driver" ref_driver.o zero_init_wrap.o $REFOBJ $WRAP \
     -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi -Wl,--gc-sections
 echo "built $OUT/ref_driver"
 
@@ -53,7 +56,7 @@ if [ -f "$ENGINE" ]; then
   $FC $FLAGS -I. -c "$REPO/include/hnumo_engine.f90" -o hnumo_engine_f.o
   $FC $FLAGS -I. -c "$REPO/h-numo_amd/fortran/hnumo_bridge.F90" -o hnumo_bridge.o
   $FC $FLAGS -DHNUMO_DROPIN -I. -c "$HERE/ref_driver.F90" -o dropin_driver.o
-  $FC -O2 -o "$OUT/dropin_driver" dropin_driver.o hnumo_bridge.o hnumo_engine_f.o $REFOBJ \
+  $FC -O2 -o "$OUT/dropin_driver" dropin_driver.o hnumo_bridge.o hnumo_engine_f.o zero_init_wrap.o $REFOBJ $WRAP \
       -L"$REPO/h-numo_amd" -Wl,-rpath,'$ORIGIN/../../h-numo_amd' -lhnumo_engine \
       -L"$MPI_LIB" -Wl,-rpath,"$MPI_LIB" -lmpifort -lmpi -Wl,--gc-sections
   echo "built $OUT/dropin_driver"

@@ -47,6 +47,13 @@ GOLDEN = [
     # f3: general bilinear quadrilaterals, neighbours along shared edges in both directions
     ("qmbump8_step2", "qmbump8", "step", 2, 1),
     ("qmdg8L3_step1", "qmdg8L3", "step", 1, 1),
+    # C1 at its stated size (~256 elements)
+    ("bump16_step1", "bump16", "step", 1, 1),
+    # ad_mlswe > 0: the predictor (ref_driver mode 4, momentum_mass with the implicit vertical
+    # shear stress); the harness zero-fills rhs_layer_shear_stress's never-assigned tau_u(nlayers+1)
+    # as the reference's -finit-real=zero build does (oracle/zero_init_wrap.c)
+    ("bump10s_predict", "bump10s", "predict", 1, 1),
+    ("dg8L3s_predict", "dg8L3s", "predict", 1, 1),
 ]
 FIELDS_KEPT = ["ope_ave", "H_ave", "Qu_ave", "btp_mass_flux_ave", "uvb_face_ave", "H_face_ave",
                "graduvb_ave", "Q_uu_dp", "H_bcl_edge", "btp_graduv_dpp_face"]
@@ -66,6 +73,12 @@ GOLDEN_MPI = [
     ("lake10_mpi2b_step1", "lake10", {}, 2, "block", 1),
     ("dg8L3_mpi2b_step2", "dg8L3q", dict(method_visc=3), 2, "block", 2),
     ("dg8L3_mpi4m_step2", "dg8L3q", dict(method_visc=3), 4, "morton", 2),
+    # method_visc == 1: the quad-point LDG fluxes cross the processor faces every stage
+    # (create_communicator_quad) and every baroclinic Laplacian (bcl_create_communicator)
+    ("bump10q_mpi2b_step1", "bump10q", {}, 2, "block", 1),
+    ("dg8L3q_mpi4m_step2", "dg8L3q", {}, 4, "morton", 2),
+    # C5 (lake at rest) on 4 ranks
+    ("lake10_mpi4m_step2", "lake10", {}, 4, "morton", 2),
 ]
 
 
@@ -159,7 +172,7 @@ def main(only=None):
         if mode == "rhs":
             keep["rhs"] = out["rhs"]
         keep["qb_df"] = out["qb_df"][:, ::stride]
-        if mode == "step":
+        if mode in ("step", "predict"):
             keep["q_df"] = out["q_df"][:, ::stride, :]
             keep["qprime_df"] = out["qprime_df"][:, ::stride, :]
         for f in FIELDS_KEPT:

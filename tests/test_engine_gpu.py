@@ -159,7 +159,7 @@ def test_shear_stress_reference_corrector_is_nonfinite(case_factory):
 
 GOLDEN_STEPS = ["bump10_step2", "lake10_step1", "dg25_step1", "dg25L3_step1", "bump10q_step1", "dg8L3q_step1",
                 "dg8N7L3_step1", "bump10_b2ns_step1", "bump10_mixed_step1", "lake10L3_step1", "bump10q_ns_step1",
-                "dg8L3q_mixed_step1", "qmbump8_step2", "qmdg8L3_step1"]
+                "dg8L3q_mixed_step1", "qmbump8_step2", "qmdg8L3_step1", "bump16_step1"]
 
 
 @pytest.mark.parametrize("name", GOLDEN_STEPS)
@@ -181,6 +181,23 @@ def test_engine_matches_reference_golden(name, case_factory, engines):
     # the engine reproduces the reference arithmetic: the state is bit-identical
     assert np.array_equal(q[:, ::s, :], g["q_df"]) and np.array_equal(qb[:, ::s], g["qb_df"])
     assert np.array_equal(qp[:, ::s, :], g["qprime_df"])
+
+
+@pytest.mark.parametrize("name", ["bump10s_predict", "dg8L3s_predict"])
+def test_predictor_matches_reference_golden(name, case_factory):
+    """ad_mlswe > 0 (implicit vertical shear stress, mod_create_rhs_mlswe.F90:146-279): the
+    prediction half of ti_rk_bcl through hnumo_predict against the reference Fortran's own
+    predictor (ref_driver mode 4, its never-assigned tau_u(nlayers+1) zero as under the
+    reference's -finit-real=zero build; oracle/zero_init_wrap.c) -- bit for bit."""
+    from util import overrides_of
+    from hnumo.engine import Engine
+    g = dict(np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False))
+    case = case_factory(str(g["config"]), **overrides_of(g))
+    e = Engine(case)
+    q, qb, qp = e.state()
+    e.predict(q, qb, qp)
+    assert np.array_equal(qb, g["qb_df"]) and np.array_equal(q, g["q_df"]) and np.array_equal(qp, g["qprime_df"])
+    e.close()
 
 
 BRANCH_VARIANTS = {

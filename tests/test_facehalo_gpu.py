@@ -16,7 +16,9 @@ GOLD = os.path.join(HERE, "golden")
 
 
 @pytest.mark.parametrize("name", ["bump10_mpi3m_step2", "lake10_mpi2b_step1", "dg8L3_mpi2b_step2",
-                                  "dg8L3_mpi4m_step2"])
+                                  "dg8L3_mpi4m_step2", "lake10_mpi4m_step2",
+                                  # method_visc == 1: quad-point LDG fluxes across processor faces
+                                  "bump10q_mpi2b_step1", "dg8L3q_mpi4m_step2"])
 def test_face_halo_matches_reference_mpi(name):
     from util import overrides_of
     from hnumo.case import build_case, make_config

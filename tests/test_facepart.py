@@ -23,7 +23,8 @@ from hnumo.facepart import face_partition, halo_lists
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = os.path.join(HERE, "golden")
-MPI_FIXTURES = ["bump10_mpi3m_step2", "lake10_mpi2b_step1", "dg8L3_mpi2b_step2", "dg8L3_mpi4m_step2"]
+MPI_FIXTURES = ["bump10_mpi3m_step2", "lake10_mpi2b_step1", "dg8L3_mpi2b_step2", "dg8L3_mpi4m_step2",
+                "lake10_mpi4m_step2", "bump10q_mpi2b_step1", "dg8L3q_mpi4m_step2"]
 
 
 @pytest.mark.parametrize("nranks,order", [(2, "block"), (4, "block"), (3, "morton"), (5, "morton")])

@@ -1,0 +1,118 @@
+"""The persistent sub-cycle launch (btp_subcycle_kernel, one launch per barotropic sub-cycle of
+mod_rk_mlswe.F90:82-116) needs every element's workgroup resident at once.  These tests give
+the launch more LDS per workgroup than fits (HNUMO_PERSIST_LDS_PAD, dynamic LDS the kernel does
+not use) and check each of the three guards (csrc/engine.hip, kernels_btp.hip
+residency_rendezvous):
+  * the occupancy estimate at create rejects the launch;
+  * the stage-less trial launch at create rejects it when the estimate is bypassed;
+  * with both bypassed, the launch itself finds its workgroups not co-resident, does no work
+    and ends; the engine drops the persistent path and repeats the step on per-stage launches.
+Every case must then reproduce the reference Fortran's step bit for bit (golden fixtures)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+PAD = 30000  # bytes: ~84 KB of LDS per workgroup, one per CU -- 256 slots for 625 elements
+
+
+def golden_case(name, case_factory):
+    from util import overrides_of
+    g = dict(np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False))
+    return g, case_factory(str(g["config"]), **overrides_of(g))
+
+
+def assert_golden(g, q, qb, qp):
+    s = int(g["stride"])
+    assert np.array_equal(q[:, ::s, :], g["q_df"]) and np.array_equal(qb[:, ::s], g["qb_df"])
+    assert np.array_equal(qp[:, ::s, :], g["qprime_df"])
+
+
+def make_engine(case, monkeypatch, guard):
+    from hnumo.engine import Engine
+    monkeypatch.setenv("HNUMO_PERSIST_LDS_PAD", str(PAD))
+    monkeypatch.setenv("HNUMO_PERSIST_GUARD", guard)
+    try:
+        return Engine(case)
+    finally:
+        monkeypatch.delenv("HNUMO_PERSIST_LDS_PAD")
+        monkeypatch.delenv("HNUMO_PERSIST_GUARD")
+
+
+def test_default_engine_is_persistent_and_resident(case_factory):
+    """dg25L3 (625 elements, 3 workgroups per CU): all three checks pass."""
+    from hnumo.engine import Engine
+    g, case = golden_case("dg25L3_step1", case_factory)
+    e = Engine(case)
+    info = e.persistent_info
+    assert e.stage_path == "persistent", info
+    assert info["trial_launch"][0] == 1 and info["occupancy_blocks_per_cu"][0] * info["cus"] >= 625, info
+    q, qb, qp = e.state()
+    e.ti_rk_bcl(q, qb, qp)
+    assert_golden(g, q, qb, qp)
+    assert e.persistent_info["fallbacks"] == 0
+    e.close()
+
+
+def test_estimate_rejects_oversized_arena(case_factory, monkeypatch):
+    g, case = golden_case("dg25L3_step1", case_factory)
+    e = make_engine(case, monkeypatch, "estimate")
+    info = e.persistent_info
+    assert e.stage_path == "per-stage", info
+    assert info["occupancy_blocks_per_cu"][0] * info["cus"] < 625, info
+    q, qb, qp = e.state()
+    e.ti_rk_bcl(q, qb, qp)
+    assert_golden(g, q, qb, qp)
+    e.close()
+
+
+def test_trial_launch_rejects_oversized_arena(case_factory, monkeypatch):
+    g, case = golden_case("dg25L3_step1", case_factory)
+    e = make_engine(case, monkeypatch, "trial")
+    info = e.persistent_info
+    assert e.stage_path == "per-stage", info
+    assert info["trial_launch"][0] == 0, info
+    q, qb, qp = e.state()
+    e.ti_rk_bcl(q, qb, qp)
+    assert_golden(g, q, qb, qp)
+    e.close()
+
+
+def test_launch_falls_back_when_not_coresident(case_factory, monkeypatch):
+    """No estimate, no trial: the first step's persistent launch is not co-resident.  It must
+    end (rendezvous abort, not a hang), leave the state untouched, and the engine must redo
+    the step on per-stage launches -- the reference's bits."""
+    g, case = golden_case("dg25L3_step1", case_factory)
+    e = make_engine(case, monkeypatch, "0")
+    assert e.stage_path == "persistent"
+    q, qb, qp = e.state()
+    e.ti_rk_bcl(q, qb, qp)
+    assert_golden(g, q, qb, qp)
+    info = e.persistent_info
+    assert e.stage_path == "per-stage" and info["fallbacks"] == 1, info
+    e.close()
+
+
+def test_resident_run_falls_back(case_factory, monkeypatch):
+    """Resident mode (state kept on the device), 3 steps in one run: the aborted first step
+    leaves the device state as it was and the retried steps continue from it -- the same bits
+    as an engine on per-stage launches from the start (HNUMO_PERSISTENT=0)."""
+    from hnumo.engine import Engine
+    _, case = golden_case("dg25L3_step1", case_factory)
+    e = make_engine(case, monkeypatch, "0")
+    monkeypatch.setenv("HNUMO_PERSISTENT", "0")
+    e0 = Engine(case)
+    monkeypatch.delenv("HNUMO_PERSISTENT")
+    a, b = e.state(), e0.state()
+    e.set_resident(True)
+    for _ in range(3):
+        e.ti_rk_bcl(*a)
+        e0.ti_rk_bcl(*b)
+    e.sync(*a)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    assert e.persistent_info["fallbacks"] == 1
+    e.close()
+    e0.close()
