@@ -869,7 +869,10 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   // ghost-element lists (num_ghost_send / num_ghost_recv) -- one of the two
   std::vector<int> sface;                 // processor-face halo: shared slot -> local face
   std::vector<int> face_slot(mesh->nface > 0 ? mesh->nface : 0, -1);
-  if (halo && halo->nranks > 1) {
+  // (nranks == 1 with processor-face lists: the self-neighbour test contract -- every listed face
+  // is shared with this rank itself, so each receives its own side 1 as side 2 over the same
+  // transport code as a real neighbour's; tests/test_rccl_self_gpu.py)
+  if (halo && (halo->nranks > 1 || halo->num_nbh > 0)) {
     if (halo->rank < 0 || halo->rank >= halo->nranks) return fail(eng, HNUMO_ERR_INVALID, "bad rank");
     bool any_face = false, any_ghost = false;
     for (int k = 0; k < halo->num_nbh; k++) {
@@ -891,7 +894,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
         nb.rank = halo->nbh_proc[k] - 1;  // mod_parallel nbh_proc is 1-based (p4est.c:1357)
         nb.off = (int)sface.size();
         nb.n = halo->num_send_recv[k];
-        if (nb.rank < 0 || nb.rank >= halo->nranks || nb.rank == halo->rank)
+        if (nb.rank < 0 || nb.rank >= halo->nranks || (nb.rank == halo->rank && halo->nranks > 1))
           return fail(eng, HNUMO_ERR_INVALID, "nbh_proc: bad neighbour rank (1-based ranks expected)");
         if (nb.n < 0) return fail(eng, HNUMO_ERR_INVALID, "num_send_recv < 0");
         for (int i = 0; i < nb.n; i++) {
@@ -910,6 +913,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
       }
       eng->NS = (int)sface.size();
     } else {
+      if (halo->nranks < 2) return fail(eng, HNUMO_ERR_INVALID, "ghost-element lists need nranks > 1");
       if (halo->nelem_owned < 1 || halo->nelem_owned > mesh->nelem)
         return fail(eng, HNUMO_ERR_INVALID, "nelem_owned must be in 1..nelem (owned elements first)");
     }
@@ -1222,7 +1226,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   }
   if (const char *sp = getenv("HNUMO_STAGE_PROF"))
     if (sp[0] == '1') eng->stage_prof = dalloc<unsigned long long>(eng, (size_t)eng->nelem * 32);
-  if (halo && halo->nranks > 1 && eng->face_halo) {
+  if (eng->face_halo) {
     eng->rank = halo->rank;
     eng->nranks = halo->nranks;
     const int NS = eng->NS;
@@ -1515,7 +1519,7 @@ static int run_steps(hnumo_engine *eng, int nsteps) {
 // group's engines run together, through hnumo_group_ti_rk_bcl only)
 static int component_transport_check(hnumo_engine *eng) {
   if (eng->comm_mode == 1) return fail(eng, HNUMO_ERR_INVALID, "engine is in a local group: use hnumo_group_ti_rk_bcl");
-  if (eng->nranks > 1 && eng->comm_mode == 0)
+  if ((eng->nranks > 1 || eng->face_halo) && eng->comm_mode == 0)
     return fail(eng, HNUMO_ERR_INVALID, "multi-rank engine without transport (comm_id or hnumo_local_group)");
   return 0;
 }

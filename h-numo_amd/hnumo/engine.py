@@ -92,7 +92,7 @@ class Engine:
         self.desc = Descriptors(case, dense=False)
         self.dims = _bundle.dims(case)
         self.h = C.c_void_p()
-        if halo is None and getattr(case, "nranks", 1) > 1:
+        if halo is None and (getattr(case, "nranks", 1) > 1 or getattr(case, "fneighbours", None)):
             self._halo = Halo(case, comm_id)
             halo = self._halo.desc
         self.halo = halo

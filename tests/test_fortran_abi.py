@@ -53,3 +53,38 @@ def test_fortran_interface_binds_every_abi_function():
                "hnumo_ti_rk_bcl", "hnumo_ti_barotropic_ssprk", "hnumo_btp_bcl_coeffs", "hnumo_create_rhs_btp",
                "hnumo_get_field", "hnumo_set_resident", "hnumo_sync"):
         assert f"name='{fn}'" in src, fn
+
+
+@pytest.mark.ref
+def test_bridge_multirank_branch_compiles_links_and_runs_to_the_device():
+    """The Fortran bridge's multi-rank branch (hnumo_bridge.F90: mod_parallel's processor-face
+    lists, the RCCL id from rank 0 broadcast with MPI_Bcast) is compiled and linked into
+    oracle/_ref/dropin_driver with the reference and libhnumo_engine (oracle/build_ref.sh).
+    On this GPU-less host a 2-rank mpiexec run must get through the reference's start-up into
+    that branch and stop at its first device call -- rank 0's hnumo_rccl_unique_id -- with the
+    bridge's own message (on a GPU box the same run is tests/test_dropin_gpu.py's territory)."""
+    import subprocess
+    import tempfile
+    import oracle as O
+    from hnumo import bundle as B
+    from hnumo.case import build_case, make_config
+    from hnumo.facepart import face_partition
+    if not os.path.exists(O.DROPIN_DRIVER):
+        pytest.skip("dropin_driver not built")
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is present: the run would not stop at the device boundary")
+    except ImportError:
+        pass
+    nm = subprocess.run(["nm", "-u", O.DROPIN_DRIVER], capture_output=True, text=True).stdout
+    assert "hnumo_rccl_unique_id" in nm and "hnumo_engine_create" in nm
+    case = build_case(make_config("bump10"))
+    parts = [face_partition(case, 2, r, "block") for r in range(2)]
+    with tempfile.TemporaryDirectory() as d:
+        fin, fout = os.path.join(d, "bundle.bin"), os.path.join(d, "out.bin")
+        for r, pc in enumerate(parts):
+            B.write_bundle(f"{fin}.{r}", pc, "step", 1, metrics=True)
+        r = subprocess.run([O.MPIEXEC, "-launcher", "fork", "-n", "2", O.DROPIN_DRIVER, fin, fout], cwd=d,
+                           capture_output=True, text=True, timeout=300)
+    assert "hnumo_bridge: hnumo_rccl_unique_id failed" in r.stdout + r.stderr, (r.stdout[-1000:], r.stderr[-1000:])
