@@ -1201,9 +1201,12 @@ __global__ void __launch_bounds__(256, 3)
                     const double *dpprime_visc, const double *momL, const double *momR, const double *lapf,
                     const double *qb, const double *q_in, double *q, double *qp_out, int mode, const double *lapx,
                     const double *dpp2, int *flag, const double *qp_avg0) {
-  // qp_avg0 (the corrector, with dpp2 == nullptr): the layer thicknesses qprime(1) enter as
-  // 0.5*(qp_avg0 + qp_in) (ti_rk_bcl.F90:78-79, formed on load) and the final qprime(1) is qp_in's
-  // own (dpp2 of :78, read back from qp_in)
+  // qp_avg0 (the corrector, non-NULL: dpp2 is then not read): the layer thicknesses qprime(1)
+  // enter as 0.5*(qp_avg0 + qp_in) (ti_rk_bcl.F90:78-79, formed on load) and the final qprime(1)
+  // is qp_in's own (dpp2 of :78, read back from qp_in).  The engine passes qp_avg0 == qp_out (both
+  // qprime_df): safe because every access is element-local -- each workgroup reads its own
+  // element's nodes of qp_avg0 into LDS in the load phase and writes the same nodes of qp_out only
+  // in its last phase; no workgroup touches another element's nodes of either.
   // q_in: the momenta entering the update (the predictor: q_df, its thicknesses already in q =
   // q_df2); mode 1 (the corrector) writes the step's final qprime straight into qp_out = qprime_df
   // (ti_rk_bcl.F90:81-84: thickness from dpp2 = the corrector's own, momenta from evaluate_bcl_v1)

@@ -30,17 +30,6 @@
 //       next stage, written straight into the neighbours' trace slots.
 #include "engine_internal.h"
 
-// Layout/schedule variants kept for A/B measurement (tools/ab3.sh), both off by default: at
-// dg25L3 they measured slower (18.2 / 17.4 us per stage against 15.1) because the resident B
-// inputs leave room for 2-row term chunks only, i.e. two more D phases per stage.
-//   HNUMO_RES   B inputs (face statics, coefficients, traces) resident in LDS for the launch
-//   HNUMO_LATE  (with RES) face fluxes beside the volume terms, neighbour traces polled late
-#ifndef HNUMO_LATE
-#define HNUMO_LATE 0
-#endif
-#ifndef HNUMO_RES
-#define HNUMO_RES 0
-#endif
 // Reference-order volume integral without term buffers ("on the fly", OTF) from this NGL on:
 // one thread per (component v, node p) computes its terms T(v,p,q) itself, in quad order, as
 // it sums them.  Same terms, same order, same bits as the chunked term buffers; no [3P][Q]
@@ -61,14 +50,6 @@
 #endif
 #ifndef HNUMO_OTF_UNROLL
 #define HNUMO_OTF_UNROLL 5
-#endif
-// Face fluxes in D0 on the last wave, neighbour traces checked there (StageCfg::FD0).  Off:
-// measured slower at dg25L3 (15.4 against 14.5 us per persistent stage, bitwise unchanged) --
-// checking the traces one phase (B) later shortened the trace wait by only ~0.5k of ~5k clocks,
-// while the last wave's serial poll + face + LDG work lengthened D0 by ~2k: the wait is the
-// neighbours' stage-to-stage skew, not a fixed hand-off latency that later checking could hide.
-#ifndef HNUMO_FD0
-#define HNUMO_FD0 0
 #endif
 // Chunked D phases (StageCfg::VSUM): term tasks split in two node halves, and one summing thread
 // per (component, node) for the whole volume integral (its partial sum in a register)
@@ -217,14 +198,12 @@ struct StageCfg {
                        QN_END_W = W_END0 - O_W,
                        W_END = (SLIM && !SLATE && O_W + 32 * NQ > W_END0) ? O_W + 32 * NQ : W_END0,
                        O_BIN = (SF && O_Y + NYV * NGL * NQ > W_END) ? O_Y + NYV * NGL * NQ : W_END;
-  // B inputs: the bottom-layer qprime, face statics, neighbour traces, face coefficients.
-  // RES: resident for the whole launch (the persistent sub-cycle loads them once), the work
-  // region (term buffers / contraction partials) follows; otherwise reloaded every stage and
-  // overlaid by term buffer 1 once B and the LDG fluxes (D0) are done.  (SLIM: the qprime of
-  // A2 in the nodal-gradient slot, written only from B on)
-  static constexpr bool RES = HNUMO_RES;
+  // B inputs: the bottom-layer qprime, face statics, neighbour traces, face coefficients,
+  // reloaded every stage (the persistent kernel: re-fetched behind E1) and overlaid by term
+  // buffer 1 once B and the LDG fluxes (D0) are done.  (SLIM: the qprime of A2 in the
+  // nodal-gradient slot, written only from B on)
   static constexpr int B_QP = 0, B_EF = B_QP + (SLIM ? 0 : 3 * P), B_TR = B_EF + 4 * FBLK, B_EC = B_TR + 32 * NGL,
-                       B_SIZE = B_EC + 4 * EFC, O_B = RES ? O_BIN + B_SIZE : O_BIN;
+                       B_SIZE = B_EC + 4 * EFC, O_B = O_BIN;
   // exact: term chunks of RC quad rows, two buffers of [3P][QCP] (odd pitch against bank
   // conflicts), as many rows as the LDS budget allows
   static constexpr int TAV = (BUDGET - O_B) / 2;
@@ -237,50 +216,36 @@ struct StageCfg {
   static constexpr int RCM = RC0 < 1 ? 1 : (RC0 > NQ ? NQ : RC0);
   static constexpr int NCH = (NQ + RCM - 1) / RCM, RC = (NQ + NCH - 1) / NCH, QC = RC * NQ;
   static constexpr int QCP = QC | 1, TSZ = OTF ? 0 : 3 * P * QCP;
-  static constexpr int TB0 = RES ? 0 : (TSZ > B_SIZE ? TSZ : B_SIZE), TB1 = RES ? TSZ : 0;
+  static constexpr int TB0 = TSZ > B_SIZE ? TSZ : B_SIZE, TB1 = 0;
   // SF: first-pass contraction partials U, W [3][2][NGL][NQ] (C1 runs the LDG face fluxes)
-  static constexpr int UWSZ = 3 * 2 * NGL * NQ, B_UW = RES ? 0 : B_SIZE;
+  static constexpr int UWSZ = 3 * 2 * NGL * NQ, B_UW = B_SIZE;
   static constexpr int ARENA = O_B + (SF ? B_UW + UWSZ : TB0 + TSZ);
-  // LATE (exact, >= 3 chunks): the neighbour traces are needed only from chunk phase KP+1 on,
-  // where the face fluxes and the LDG face fluxes run beside the volume terms; the
-  // persistent kernel polls the traces in phase KP, late in the stage, so the hand-off
-  // latency and the neighbours' skew hide behind the volume work.  Otherwise (SF, or too few
-  // chunks) the face fluxes run in B and the traces are polled after the interpolation.
-  static constexpr bool LATE = HNUMO_LATE && RES && !SF && NCH >= 3;
-  static constexpr int KP = NCH - 3;
-  // FD0 (exact, chunked D, not LATE): the face fluxes run in D0 on the last wave, beside the first
-  // chunk's terms, followed by the LDG face fluxes (qq moves to D1: FPRE's face-quad traces share
-  // its LDS).  The persistent kernel's last wave issues the neighbour-trace granule loads before
-  // A2 and checks them only there, one phase (B) later than after A2: more of the hand-off latency
-  // hides behind the element's own work, and only one wave waits for it.
-  static constexpr bool FD0 = HNUMO_FD0 && !SF && !LATE && !OTF && NCH >= 2 && 4 * NQ <= 64 && 4 * NGL <= 64;
-  static constexpr int NGR = (32 * NGL + 63) / 64;  // granules per lane of the polling wave
-  // B task ranges: quad points [0,Q) | face points [OF,OF+4NQ) (early only) | nodal grad
+  static constexpr int NGR = (32 * NGL + 63) / 64;  // granules per lane of the polling wave (SLATE)
+  // B task ranges: quad points [0,Q) | face points [OF,OF+4NQ) (not SLATE) | nodal grad
   // [OG,OG+P) | LDG face nodes [OL,OL+4NGL) (SF: C1), on their own
   // waves when they fit
   static constexpr int RU = 64, OFa = ((Q + RU - 1) / RU) * RU,
-                       OGa = (LATE || SLATE) ? OFa : ((OFa + 4 * NQ + RU - 1) / RU) * RU;
+                       OGa = SLATE ? OFa : ((OFa + 4 * NQ + RU - 1) / RU) * RU;
   static constexpr bool WIDE = OGa + P + (SF ? 4 * NGL : 0) <= BS;  // (exact: the LDG range runs in D0)
-  static constexpr int OF = WIDE ? OFa : Q, OG = WIDE ? OGa : ((LATE || SLATE) ? Q : OF + 4 * NQ), OL = OG + P,
+  static constexpr int OF = WIDE ? OFa : Q, OG = WIDE ? OGa : (SLATE ? Q : OF + 4 * NQ), OL = OG + P,
                        WEND = OL + 4 * NGL, BEND = OL;
-  // FPRE (exact, not LATE): A2 also interpolates each face's own-side traces and, on physical
+  // FPRE (exact): A2 also interpolates each face's own-side traces and, on physical
   // boundaries, the ghost-side traces to the face quad points, into s_fi [4][NQ][8] (in the
   // W region, dead from A to D0), so B's face fluxes interpolate only the neighbour traces
-  static constexpr bool FPRE = !SF && !LATE && !SLATE && (SLIM || 4 * NQ * 8 <= QN_END_W);
-  // LATE chunk phase KP+1: face fluxes from OFD, LDG fluxes from OLD, past the term tasks
-  static constexpr int WTMAX = QC * NGL, OFD = ((WTMAX + RU - 1) / RU) * RU, OLD = OFD + 4 * NQ;
+  static constexpr bool FPRE = !SF && !SLATE && (SLIM || 4 * NQ * 8 <= QN_END_W);
+  static constexpr int WTMAX = QC * NGL;  // term tasks of a full chunk
   // VSUM (exact, chunked D): a chunk's term tasks split in two node halves on threads
   // [0, 2*WTMAX) (the longest lane forms ceil(NGL/2) nodes' terms instead of NGL), and the 3P
   // ordered chains summed by threads [OVS, BS), one per (component, node) and the same in every
   // phase, the partial sum in a register (instead of 3 chains per thread through s_rhs); qq and
   // the LDG face fluxes (D0, no sums yet) after the terms
   static constexpr int OVS = BS - 3 * P;
-  static constexpr bool VSUM = HNUMO_VSUM && !SF && !OTF && !LATE && !FD0 && 2 * WTMAX <= OVS &&
+  static constexpr bool VSUM = HNUMO_VSUM && !SF && !OTF && 2 * WTMAX <= OVS &&
                                2 * WTMAX + P <= BS && OL >= 2 * WTMAX + P && OL + 4 * NGL <= BS;
   // REGACC (persistent sub-cycle): every accumulating task (quad point, face quad point, node,
   // LDG face node) has its own thread, the same in every stage, so the time averages can live in
   // that thread's registers for the whole launch and be written once, scaled, at the end
-  static constexpr bool REGACC = WIDE && !LATE && !FD0 && OL + 4 * NGL <= BS;
+  static constexpr bool REGACC = WIDE && OL + 4 * NGL <= BS;
 };
 
 // Nodal derivatives at node (i,j) keep the reference's 2*NGL-1 nonzero terms (mm==j or
@@ -419,7 +384,6 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   double *s_ef = SI + C::B_EF;     // [4][FBLK]
   double *s_tr = SI + C::B_TR;     // [4][8][NGL]
   double *s_ec = SI + C::B_EC;     // [4][EFC]
-  constexpr bool LATE = C::LATE;
 
   // ------------------------------------------------------------- A: async loads
   if (a.prof && tid == 0) s_prof[30] = wall_clock64();
@@ -455,7 +419,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       }
     }
     // qprime, the face statics and the face coefficients are constant over a sub-cycle
-    // (persistent, not RES: the previous stage re-fetched them in E1, see there)
+    // (persistent: the previous stage re-fetched them in E1, see there)
     if (!PERSIST || first) {
       if (m.botfr && qpm != 2)
         glds_copy<BS>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
@@ -506,10 +470,10 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     load_pre();
     __syncthreads();  // the async LDS copies have landed
   } else {
-    // persistent, later stages: RES: nothing was loaded; otherwise the B inputs re-fetched in
-    // the previous stage's E1 must have landed (this wave's copies; the barrier covers the
+    // persistent, later stages: the B inputs re-fetched in the previous stage's E1 must have
+    // landed (this wave's copies; the barrier covers the
     // others').  The register loads go out after the wait, so it does not cover them.
-    if constexpr (!C::RES) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     LDS_BARRIER();
     load_pre();
   }
@@ -588,12 +552,11 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       if (a.prof) atomicMax(&s_prof[22], clock64() - c0);  // longest trace wait of the stage
     }
   };
-  // FD0: the last wave loads every granule of the element (NGR per lane) now and checks them in
-  // D0 (poll_wave), before the face fluxes it runs there
-  constexpr bool FD0 = C::FD0;
+  // SLATE: the last wave loads every granule of the element (NGR per lane) and checks them in D
+  // (poll_wave), before the face fluxes it runs there
   granule_u4 gxr[C::NGR];
   auto issue_granules_wave = [&]() {
-    if constexpr (PERSIST && (FD0 || C::SLATE)) {
+    if constexpr (PERSIST && C::SLATE) {
       if (tid >= BS - 64) {
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
             (void *)(a.gtr_in + (size_t)e * 32 * NGL), 0, 32 * NGL * (int)sizeof(TraceGranule), 0x00020000);
@@ -604,7 +567,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     }
   };
   auto poll_wave = [&]() {
-    if constexpr (PERSIST && (FD0 || C::SLATE)) {
+    if constexpr (PERSIST && C::SLATE) {
       const unsigned long long want = (ep << 20) | a.tag_in;
       const unsigned long long c0 = a.prof ? clock64() : 0;
 #pragma unroll
@@ -627,10 +590,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       if (a.prof) atomicMax(&s_prof[22], clock64() - c0);
     }
   };
-  if constexpr (FD0)
-    issue_granules_wave();
-  else if constexpr (!LATE && !C::SLATE)
-    issue_granule();
+  if constexpr (!C::SLATE) issue_granule();
   {
     // persistent, after the first stage: the wall normals and u_bar, v_bar of this state are in
     // LDS already (E1 formed u_bar, v_bar of the new state); qpm == 2: pp, up, vp are loaded
@@ -780,7 +740,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       }
     }
   }
-  if constexpr (!LATE && !FD0 && !C::SLATE) poll_traces();  // (the granule was issued before the interpolation)
+  if constexpr (!C::SLATE) poll_traces();  // (the granule was issued before the interpolation)
   LDS_BARRIER();
   STAGE_MARK(1);
 
@@ -1012,7 +972,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         s_qv[5 * Q + q] = sc_y;
         s_qv[6 * Q + q] = Hq + qv;
       }
-    } else if (!LATE && !FD0 && !C::SLATE && w >= C::OF && w < C::OF + 4 * NQ) {
+    } else if (!C::SLATE && w >= C::OF && w < C::OF + 4 * NQ) {
       face_task(w - C::OF);
     } else if (w >= C::OG && w < C::OL) {
       const int p = w - C::OG, i = p % NGL, j = p / NGL;
@@ -1550,10 +1510,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     constexpr int OSV = ((2 * P + 63) / 64) * 64;
     constexpr bool VSPLIT = OSV + 3 * P <= BS;
     // lanes: terms from 0, the sums on the last wave when they fit beside the terms, qq
-    // after the terms (D0), the Laplacian from 0 in the last phase (no terms there).  Face
-    // fluxes and LDG face fluxes: LATE, in chunk phase KP+1 past the terms (the persistent
-    // kernel polls the neighbour traces in phase KP); otherwise the face fluxes ran in B and
-    // the LDG fluxes run in D0
+    // after the terms (D0), the Laplacian from 0 in the last phase (no terms there); the face
+    // fluxes ran in B, the LDG fluxes run in D0
     constexpr int WTMAX = C::WTMAX;
     constexpr int OSUM = (P <= 64 && WTMAX <= BS - 64) ? BS - 64 : WTMAX;
     // VSUM: thread OVS + (v*P + p) sums chain (v, p) of every chunk, the partial sum in vacc
@@ -1602,7 +1560,6 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     for (int k = 0; k <= NCH; k++) {
       asm volatile("" ::: "memory");  // keep LDS reads inside their phase (no hoisting)
       const int WT = (k < NCH) ? ((k == NCH - 1) ? (Q - k * QC) : QC) * NGL : 0;  // term tasks
-      if (LATE && k == C::KP) issue_granule();
       if constexpr (VSUM) {
         // first node halves on [0, WT), second halves on [WTMAX, WTMAX + WT)
         if (tid < WT || (tid >= WTMAX && tid < WTMAX + WT)) term_task(k, tid);
@@ -1617,35 +1574,21 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           for_tasks<BS>(tid, OSUM, P, [&](int t, bool) { sum_task(k - 1, t); });
       }
       }
-      if (k == (FD0 ? 1 : 0)) for_tasks<BS>(tid, VSUM ? 2 * WTMAX : WT, P, [&](int t, bool) { qq_task(t); });
-      if (k == 0 && !LATE && !FD0) for_tasks<BS>(tid, C::OL, 4 * NGL, ldg_task);
-      if (FD0 && k == 0 && tid >= BS - 64) {
-        // the last wave: neighbour traces (persistent: checked now), face fluxes, LDG fluxes;
-        // its own LDS writes of the traces are complete before its lanes read them
-        poll_wave();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        for (int t = tid & 63; t < 4 * NQ; t += 64) face_task(t);
-        asm volatile("" ::: "memory");
-        for (int t = tid & 63; t < 4 * NGL; t += 64) ldg_task(t, false);
-      }
-      if (LATE && k == C::KP + 1) {
-        for_tasks<BS>(tid, C::OFD, 4 * NQ, [&](int t, bool) { face_task(t); });
-        for_tasks<BS>(tid, C::OLD, 4 * NGL, ldg_task);
-      }
+      if (k == 0) for_tasks<BS>(tid, VSUM ? 2 * WTMAX : WT, P, [&](int t, bool) { qq_task(t); });
+      if (k == 0) for_tasks<BS>(tid, C::OL, 4 * NGL, ldg_task);
       if (k == NCH && !(a.dbg & 2)) for_tasks<BS>(tid, 0, 2 * P, [&](int t, bool) { lap_task(t / P, t % P); });
-      if (LATE && k == C::KP) poll_traces();
       LDS_BARRIER();
       if (k < 6) STAGE_MARK(6 + k);
     }
   }
   STAGE_MARK(3);
 
-  // persistent, B inputs not resident: the term buffers are dead now, so the next stage's
+  // persistent: the term buffers are dead now, so the next stage's
   // bottom-layer qprime, face statics and face coefficients (constant over the sub-cycle,
   // overlaid by term buffer 1 in D1..D2) are re-fetched here, behind E1/E2, instead of at
   // the start of the next stage (the traces' slot is not touched: A2 of the next stage
   // fills it)
-  if constexpr (PERSIST && !C::RES) {
+  if constexpr (PERSIST) {
     if (a.write_trace) {  // a next stage follows
       int rot = 0;
       if (!C::SLIM && m.botfr && qpm == 0) glds_copy<BS>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);

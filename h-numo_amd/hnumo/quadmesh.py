@@ -186,6 +186,15 @@ class QuadMesh:
                     rec[f][3] = e + 1
                     rec[f][5] = va != rec[f][4]       # runs the other way along the edge
                     side[f][1] = k
+        # a :BC_ tag belongs on a boundary edge: p4est_bc_read_inp (p4est.c:1121-1133) attaches
+        # it to the one element side on that edge -- an interior edge or an edge of no element
+        # is an inconsistent grid file, not something to drop silently
+        for key in bc:
+            f = seen.get(frozenset(key))
+            if f is None:
+                raise ValueError(f"boundary line element {sorted(key)}: no element has this edge")
+            if rec[f][3] > 0:
+                raise ValueError(f"boundary line element {sorted(key)}: the edge is interior (two elements)")
         nface = len(rec)
         self.nface = nface
         face = np.zeros((8, nface), dtype=np.int32, order="F")

@@ -1,0 +1,42 @@
+"""C5 at its stated size (lakeAtrest, 2 layers, N=4, 200x200 elements on the
+lake domain, 4 ranks).  The reference's lake at rest (initial_conditions.F90:130-169: a
+bottom bump under flat interfaces) is well balanced: the state must stay at rest and every
+layer's mass must be conserved to round-off.  Bitwise parity at 4 ranks is pinned at the
+fixture size (tests/test_facehalo_gpu.py, lake10_mpi4m_step2, the reference under mpiexec);
+here the 200x200 mesh runs as 4 processor-face partitions (Morton) in one local exchange
+group on this GPU.  (Time steps scaled with the element size, 10/200 of the 10x10 lake's
+dt = 100 s, dt_btp = 1.8 s: the 10x10 steps exceed the CFL bound by ~20x on 10-m elements.)"""
+import numpy as np
+import pytest
+
+from util import layer_mass
+
+pytestmark = pytest.mark.gpu
+
+
+def test_lake200_four_ranks_at_rest_and_conservative():
+    from hnumo.case import build_case, make_config
+    from hnumo.engine import Engine, group_ti_rk_bcl, local_group
+    from hnumo.facepart import face_partition
+    case = build_case(make_config("lake10", nelx=200, nely=200, dt=5.0, dt_btp=0.09), dense=False)
+    R = 4
+    parts = [face_partition(case, R, r, "morton") for r in range(R)]
+    engines = [Engine(p) for p in parts]
+    local_group(engines)
+    states = [e.state() for e in engines]
+    m0 = sum(layer_mass(p, s[0]) for p, s in zip(parts, states))
+    q0 = [s[0].copy() for s in states]
+    for _ in range(2):
+        group_ti_rk_bcl(engines, states)
+    g = case.scalars["gravity"]
+    m1 = sum(layer_mass(p, s[0]) for p, s in zip(parts, states))
+    assert (np.abs(m1 - m0) / m0 <= 1e-12).all(), np.abs(m1 - m0) / m0
+    for p, (q, qb, qp), qi in zip(parts, states, q0):
+        assert np.isfinite(q).all() and np.isfinite(qb).all() and np.isfinite(qp).all()
+        for k in range(case.scalars["nlayers"]):
+            dp = np.abs(qi[0, :, k]).max()
+            # thickness unchanged, momenta zero, to round-off of the layer's own scales
+            assert np.abs(q[0, :, k] - qi[0, :, k]).max() / dp <= 1e-12, k
+            assert np.abs(q[1:, :, k]).max() / (dp * np.sqrt(g * dp)) <= 1e-12, k
+    for e in engines:
+        e.close()

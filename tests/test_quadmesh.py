@@ -90,3 +90,16 @@ def test_clockwise_element_is_rejected():
     V = np.array([[0.0, 0.0], [1.0, 0.0], [1.0, 1.0], [0.0, 1.0]])
     with pytest.raises(ValueError):
         QuadMesh(V, np.array([[0, 3, 2, 1]]), {}, 5, 9)
+
+
+def test_inconsistent_boundary_tags_are_rejected():
+    """A :BC_ line element must lie on a boundary edge (p4est_bc_read_inp attaches it to the one
+    element side there): one on an interior edge, or on an edge no element has, is an error."""
+    from hnumo.quadmesh import QuadMesh
+    V = np.array([[0.0, 0.0], [1.0, 0.0], [2.0, 0.0], [0.0, 1.0], [1.0, 1.0], [2.0, 1.0]])
+    Qd = np.array([[0, 1, 4, 3], [1, 2, 5, 4]])
+    QuadMesh(V, Qd, {frozenset((0, 1)): 2}, 5, 9)                  # a boundary edge: fine
+    with pytest.raises(ValueError, match="interior"):
+        QuadMesh(V, Qd, {frozenset((1, 4)): 2}, 5, 9)              # the shared edge
+    with pytest.raises(ValueError, match="no element"):
+        QuadMesh(V, Qd, {frozenset((0, 5)): 2}, 5, 9)              # not an edge

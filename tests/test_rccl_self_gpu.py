@@ -24,9 +24,13 @@ def self_neighbour_case(cfg, **ov):
     return pc
 
 
-# (nodal LDG: the two-stream schedule; method_visc 1: one stream, LDG fluxes exchanged per stage)
+# (nodal LDG: the two-stream schedule; method_visc 1: one stream, LDG fluxes exchanged per stage.
+# Not bump10q: its viscosity is strong enough on 200-m elements that the mirror halo of the
+# self-neighbour contract, with the reference's face flux that is not antisymmetric in the two
+# sides' orientation (mod_laplacian_quad.F90:485-486), runs away in the first step on both
+# transports alike -- DESIGN.md §8)
 @pytest.mark.parametrize("cfg,ov,graph", [("bump10", {}, "0"), ("dg8L3q", dict(method_visc=3), "0"),
-                                          ("dg8L3q", dict(method_visc=3), "1"), ("bump10q", {}, "0"),
+                                          ("dg8L3q", dict(method_visc=3), "1"), ("dg8L3q", {}, "0"),
                                           ("dg8L3q", {}, "1")])
 def test_rccl_self_exchange_matches_local_group(cfg, ov, graph, monkeypatch):
     from hnumo.engine import Engine, group_ti_rk_bcl, local_group
