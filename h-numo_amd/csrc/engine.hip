@@ -1218,7 +1218,9 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   // per-stage kernel arena: on meshes that take several residency rounds per stage, the arena
   // sized for 4 workgroups per CU (1-row term chunks) -- 1.566 -> 1.517 ms per stage at C4
   // (tools/ab_env.py, round 2); small meshes keep the 3-per-CU arena
-  eng->stage_nb = eng->nelem_owned >= 2048 ? 4 : 0;
+  // large meshes: the LEAN 5-per-CU arena (C4: 1.331 ms per stage against 1.409 for the 4-per-CU
+  // one with 2-row term chunks and 1.501 for round 2's, profiles/r03f)
+  eng->stage_nb = eng->nelem_owned >= 2048 ? 5 : 0;
   if (const char *sn = getenv("HNUMO_STAGE_NB")) eng->stage_nb = atoi(sn);
   {
     const char *qv = getenv("HNUMO_QPQ");

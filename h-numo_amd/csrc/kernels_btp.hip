@@ -56,6 +56,10 @@
 #ifndef HNUMO_VSUM
 #define HNUMO_VSUM 1
 #endif
+// The lean per-stage arenas of large meshes (StageCfg::LEAN); 0 keeps the round-2 layout for A/B.
+#ifndef HNUMO_LEAN
+#define HNUMO_LEAN 1
+#endif
 namespace hnumo {
 
 // A trace value with the tag of the stage it is for: one 16-byte write-through store makes
@@ -180,11 +184,19 @@ struct StageCfg {
   // launch from 65.0 to 57.0 us, but the persistent sub-cycle from 56.4 to 63.6 us
   static constexpr bool OPAIR = SLATE && HNUMO_OTF_PAIR;
   static constexpr int EW = BS / 64 - 1;
+  // LEAN (the per-stage kernel's arenas for large meshes, NBK != 0): less fixed LDS so that more
+  // workgroups fit a CU or more quad rows fit a term chunk -- E1 on the last wave (the volume-sum
+  // lanes of D) with the Shu-Osher states qb0 / qb2 in its registers (loaded from global memory
+  // during D) instead of LDS; the right-hand side and the Laplacian in the term buffer that is dead
+  // in the last D phase, the new state in the other one (dead after D), the face-quad traces of
+  // FPRE in term buffer 0 (A2 -> B; D0 writes it first)
+  static constexpr bool LEAN = HNUMO_LEAN && NBK != 0 && !SF && !OTF;
   static_assert(!SLIM || (P <= 64 && 3 * P <= EW * 64), "SLIM: one node per lane of the last wave");
   // LDS arena (doubles).  Persistent (A..E); the wall normals of the face nodes are copied
   // out of the face statics (which live in the B region) for E1:
   static constexpr int O_BASIS = 0, O_EREC = O_BASIS + NB + 1, O_QB = O_EREC + ERSD, O_Q0 = O_QB + 4 * P,
-                       O_Q2 = O_Q0 + (SLIM ? 0 : 4 * P), O_QK = O_Q2 + (SLIM ? 0 : 4 * P), O_NS = O_QK + QE_KEEP * Q,
+                       O_Q2 = O_Q0 + ((SLIM || LEAN) ? 0 : 4 * P), O_QK = O_Q2 + ((SLIM || LEAN) ? 0 : 4 * P),
+                       O_NS = O_QK + QE_KEEP * Q,
                        O_NC = O_NS + (SLIM ? NE_LDS : NE_N) * P, O_UV = O_NC + (SLIM ? 0 : 5 * P), O_WN = O_UV + 2 * P;
   // working arrays: quad-point values (exact: the 7 integrand factors; SF: the 8 weighted
   // integrands F1,F2,G0..G2,H0..H2), B outputs, then a region written only after B that the
@@ -193,8 +205,9 @@ struct StageCfg {
   // (SLIM: no Laplacian / new-state buffers; the face-quad traces of FPRE, A2 -> B, share the W
   // region with qq and rhs, D -> E)
   static constexpr int O_QV = O_WN + 8 * NGL, O_GR = O_QV + NQV * Q, O_FQ = O_GR + 4 * P, O_FL = O_FQ + 16 * NQ,
-                       O_W = O_FL + 8 * NGL, O_QQ = O_W, O_RHS = O_QQ + 4 * P, O_LAP = O_RHS + 3 * P,
-                       O_QN = O_LAP + (SLIM ? 0 : 2 * P), O_Y = O_W, W_END0 = O_QN + (SLIM ? 0 : 4 * P),
+                       O_W = O_FL + 8 * NGL, O_QQ = O_W, O_RHS = O_QQ + 4 * P, O_LAP = O_RHS + (LEAN ? 0 : 3 * P),
+                       O_QN = O_LAP + ((SLIM || LEAN) ? 0 : 2 * P), O_Y = O_W,
+                       W_END0 = O_QN + ((SLIM || LEAN) ? 0 : 4 * P),
                        QN_END_W = W_END0 - O_W,
                        W_END = (SLIM && !SLATE && O_W + 32 * NQ > W_END0) ? O_W + 32 * NQ : W_END0,
                        O_BIN = (SF && O_Y + NYV * NGL * NQ > W_END) ? O_Y + NYV * NGL * NQ : W_END;
@@ -232,7 +245,7 @@ struct StageCfg {
   // FPRE (exact): A2 also interpolates each face's own-side traces and, on physical
   // boundaries, the ghost-side traces to the face quad points, into s_fi [4][NQ][8] (in the
   // W region, dead from A to D0), so B's face fluxes interpolate only the neighbour traces
-  static constexpr bool FPRE = !SF && !SLATE && (SLIM || 4 * NQ * 8 <= QN_END_W);
+  static constexpr bool FPRE = !SF && !SLATE && (SLIM || LEAN || 4 * NQ * 8 <= QN_END_W);
   static constexpr int WTMAX = QC * NGL;  // term tasks of a full chunk
   // VSUM (exact, chunked D): a chunk's term tasks split in two node halves on threads
   // [0, 2*WTMAX) (the longest lane forms ceil(NGL/2) nodes' terms instead of NGL), and the 3P
@@ -242,6 +255,9 @@ struct StageCfg {
   static constexpr int OVS = BS - 3 * P;
   static constexpr bool VSUM = HNUMO_VSUM && !SF && !OTF && 2 * WTMAX <= OVS &&
                                2 * WTMAX + P <= BS && OL >= 2 * WTMAX + P && OL + 4 * NGL <= BS;
+  // (LEAN: the rhs is written only in the last D phase, by the VSUM lanes)
+  static_assert(!LEAN || (VSUM && TSZ >= 32 * NQ && TSZ >= 5 * P && 3 * P <= 64 * EW + 64), "LEAN layout");
+  static constexpr int TB_LAST = (NCH & 1) ? TB1 : TB0, TB_PREV = (NCH & 1) ? TB0 : TB1;
   // REGACC (persistent sub-cycle): every accumulating task (quad point, face quad point, node,
   // LDG face node) has its own thread, the same in every stage, so the time averages can live in
   // that thread's registers for the whole launch and be written once, scaled, at the end
@@ -375,9 +391,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   double *s_grad = S + C::O_GR, *s_qq = S + C::O_QQ;  // [4][P]
   double *s_fq = S + C::O_FQ;      // [4][NQ][4]: wq, flux, H_kx+flux_x, H_ky+flux_y
   double *s_fl = S + C::O_FL;      // [4][NGL][2]
-  double *s_rhs = S + C::O_RHS, *s_lap = S + C::O_LAP;  // [3][P], [2][P]
-  double *s_qn = C::SLIM ? s_qb : S + C::O_QN;  // [P][4] (SLIM: in place of the input, E1)
-  double *s_fi = S + C::O_W;       // FPRE: [4][NQ][8] face-quad traces, own side | ghost side (A2 -> B)
+  // [3][P], [2][P] (LEAN: in the term buffer that is dead in the last D phase)
+  double *s_rhs = C::LEAN ? S + C::O_B + C::TB_LAST : S + C::O_RHS;
+  double *s_lap = C::LEAN ? s_rhs + 3 * P : S + C::O_LAP;
+  // [P][4] (SLIM: in place of the input; LEAN: the other term buffer, dead after D)
+  double *s_qn = C::SLIM ? s_qb : (C::LEAN ? S + C::O_B + C::TB_PREV : S + C::O_QN);
+  // FPRE: [4][NQ][8] face-quad traces, own side | ghost side (A2 -> B; LEAN: in term buffer 0)
+  double *s_fi = C::LEAN ? S + C::O_B + C::TB0 : S + C::O_W;
   double *SI = S + C::O_BIN;       // B inputs
   double *SB = S + C::O_B;         // term buffers / partials
   double *s_qp = C::SLIM ? S + C::O_GR : SI + C::B_QP;  // [P][3] qprime of the bottom layer (A2)
@@ -406,8 +426,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     }
     if (!PERSIST) {
       glds_copy<BS>(a.qb_in + (size_t)e * 4 * P, s_qb, 8 * P, tid, rot);
-      if (!C::SLIM && use_q0) glds_copy<BS>(a.qb0 + (size_t)e * 4 * P, s_q0, 8 * P, tid, rot);
-      if (!C::SLIM && use_q2) glds_copy<BS>(a.qb2 + (size_t)e * 4 * P, s_q2, 8 * P, tid, rot);
+      if (!C::SLIM && !C::LEAN && use_q0) glds_copy<BS>(a.qb0 + (size_t)e * 4 * P, s_q0, 8 * P, tid, rot);
+      if (!C::SLIM && !C::LEAN && use_q2) glds_copy<BS>(a.qb2 + (size_t)e * 4 * P, s_q2, 8 * P, tid, rot);
       if (m.etsrc) {
         // processor-face halo: each face's neighbour trace from its own slot (the receive
         // slot of a processor face); the slot ids are uniform, scalar loads
@@ -1556,6 +1576,17 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         s_rhs[v * P + p] = vacc;
       }
     };
+    if constexpr (C::LEAN) {
+      // the E1 lanes' Shu-Osher states (qb0, qb2 components 1..3), in flight during D
+      const int p = tid - C::EW * 64;
+      if (p >= 0 && p < P) {
+#pragma unroll
+        for (int v = 0; v < 3; v++) {
+          if (use_q0) r_q0[v] = a.qb0[((size_t)e * P + p) * 4 + 1 + v];
+          if (use_q2) r_q2[v] = a.qb2[((size_t)e * P + p) * 4 + 1 + v];
+        }
+      }
+    }
 #pragma unroll
     for (int k = 0; k <= NCH; k++) {
       asm volatile("" ::: "memory");  // keep LDS reads inside their phase (no hoisting)
@@ -1599,7 +1630,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
 
   // ------------------------------------------------------------- E1: update + wall fix
   // (SLIM: on the last wave, with its registers; otherwise wave 0)
-  constexpr int EW0 = C::SLIM ? C::EW * 64 : 0;
+  constexpr int EW0 = (C::SLIM || C::LEAN) ? C::EW * 64 : 0;
   static_assert(P <= 64, "E1 and the nodal gradients run on one wave");
   for (int p = tid - EW0; p >= 0 && p < P; p += BS) {
     const size_t I = (size_t)e * P + p;
@@ -1621,9 +1652,9 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
 #pragma unroll
     for (int v = 1; v < 4; v++) {
       double x = 0.0;
-      if (a.a1 != 0.0) x = a.a1 * (C::SLIM ? r_q0[v - 1] : s_q0[p * 4 + v]);
+      if (a.a1 != 0.0) x = a.a1 * ((C::SLIM || C::LEAN) ? r_q0[v - 1] : s_q0[p * 4 + v]);
       x = x + a.a2 * s_qb[p * 4 + v];
-      if (a.a3 != 0.0) x = x + a.a3 * (C::SLIM ? r_q2[v - 1] : s_q2[p * 4 + v]);
+      if (a.a3 != 0.0) x = x + a.a3 * ((C::SLIM || C::LEAN) ? r_q2[v - 1] : s_q2[p * 4 + v]);
       qn[v] = x + a.dtt * rh[v - 1];
     }
     qn[0] = qn[1] + (C::SLIM ? r_pb : s_ns[NE_PB * P + p]);

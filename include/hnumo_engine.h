@@ -158,7 +158,10 @@ typedef struct hnumo_params {
  *
  * Transport: RCCL point-to-point over xGMI when comm_id (from hnumo_rccl_unique_id,
  * broadcast by the host) is given; engines of one process on one device joined with
- * hnumo_local_group otherwise.  NULL halo or nranks == 1: single rank.                */
+ * hnumo_local_group otherwise.  NULL halo or nranks == 1 without lists: single rank.
+ * (Test contract: nranks == 1 WITH processor-face lists whose neighbour is the rank itself --
+ * each listed face receives its own side 1 -- drives the RCCL code on one GPU.  RCCL across
+ * GPUs is verified by bench.py's halo check in a multi-GPU run, INTEGRATION.md.)       */
 typedef struct hnumo_halo_desc {
   int32_t rank, nranks;                 /* 0-based rank of this engine, number of ranks */
   int32_t num_nbh;

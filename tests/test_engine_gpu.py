@@ -340,3 +340,26 @@ def test_persistent_subcycle_matches_stage_launches(cfg, case_factory, monkeypat
         assert np.array_equal(e1.field(f), e0.field(f)), f
     e1.close()
     e0.close()
+
+
+@pytest.mark.parametrize("nb", ["0", "4", "5"])
+def test_stage_arenas_match_reference_golden(nb, case_factory, monkeypatch):
+    """The per-stage kernel in each of its LDS arenas (StageCfg NBK: 0 = the 3-per-CU arena of
+    small meshes, 4 and 5 = the LEAN arenas of large meshes, e.g. C4) on dg25L3 -- one launch per
+    stage, HNUMO_STAGE_NB forcing the arena -- equals the reference Fortran's step bit for bit."""
+    from util import overrides_of
+    from hnumo.engine import Engine
+    g = dict(np.load(os.path.join(GOLD, "dg25L3_step1.npz"), allow_pickle=False))
+    case = case_factory(str(g["config"]), **overrides_of(g))
+    monkeypatch.setenv("HNUMO_PERSISTENT", "0")
+    monkeypatch.setenv("HNUMO_STAGE_NB", nb)
+    e = Engine(case)
+    monkeypatch.delenv("HNUMO_PERSISTENT")
+    monkeypatch.delenv("HNUMO_STAGE_NB")
+    assert e.stage_path == "per-stage"
+    q, qb, qp = e.state()
+    e.ti_rk_bcl(q, qb, qp)
+    s = int(g["stride"])
+    assert np.array_equal(q[:, ::s, :], g["q_df"]) and np.array_equal(qb[:, ::s], g["qb_df"])
+    assert np.array_equal(qp[:, ::s, :], g["qprime_df"])
+    e.close()
