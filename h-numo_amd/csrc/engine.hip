@@ -1125,7 +1125,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   }
   // element-major statics (engine_internal.h)
   const int Qe = nq * nq, FBLK = EF_N * nq + EFN_N * ngl;
-  std::vector<double> qsE((size_t)E * QE_N * Qe), nsE((size_t)E * NE_N * P), efs((size_t)E * 4 * FBLK);
+  std::vector<double> qsE((size_t)E * qe_stride(Qe)), nsE((size_t)E * NE_N * P), efs((size_t)E * 4 * FBLK);
   {
     const int qmap[QE_N] = {QS_W, QS_EX, QS_EY, QS_NX, QS_NY, QS_COR, QS_TW1, QS_TW2, QS_GZ1, QS_GZ2, QS_OOP};
     const int nmap[NE_N] = {NS_EX, NS_EY, NS_NX, NS_NY, NS_W, NS_OOP, NS_MINV, NS_PB};
@@ -1133,7 +1133,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     const int fnmap[EFN_N] = {FN_NX, FN_NY, FN_W, FN_PBL, FN_PBR};
     for (int e = 0; e < E; e++) {
       for (int c = 0; c < QE_N; c++)
-        for (int q = 0; q < Qe; q++) qsE[(size_t)e * QE_N * Qe + qe_pos(c, q, Qe)] = qs[qmap[c] * npq + (size_t)e * Qe + q];
+        for (int q = 0; q < Qe; q++) qsE[(size_t)e * qe_stride(Qe) + qe_pos(c, q, Qe)] = qs[qmap[c] * npq + (size_t)e * Qe + q];
       for (int c = 0; c < NE_N; c++)
         for (int p = 0; p < P; p++) nsE[((size_t)e * NE_N + c) * P + p] = ns[nmap[c] * npoin + (size_t)e * P + p];
       for (int lf = 0; lf < 4; lf++) {
@@ -1167,7 +1167,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   eng->qstatE = dalloc<double>(eng, qsE.size());
   eng->nstatE = dalloc<double>(eng, nsE.size());
   eng->efstat = dalloc<double>(eng, efs.size());
-  eng->ecoef = dalloc<double>(eng, (size_t)E * (4 * Qe + 5 * P));
+  eng->ecoef = dalloc<double>(eng, (size_t)E * eco_stride(Qe, P));
   eng->efcoef = dalloc<double>(eng, (size_t)E * 4 * (4 * nq + 10 * ngl));
   eng->alpha = dalloc<double>(eng, L);
   eng->tau_wind = dalloc<double>(eng, 2 * npq);

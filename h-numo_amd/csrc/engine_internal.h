@@ -19,10 +19,10 @@
 // so a stage loads everything it needs with one round of async global->LDS copies):
 //   erec   int  [E][ERS]              faces, side, bc, nbr elem, nbr local face, keeps-averages flag, face->node map,
 //                                     node->(lf*NGL+n) of the <=2 faces through each node
-//   qstatE      [E][QE_N][Q]          W, e_x, e_y, n_x, n_y, coriolis, tau_wind(2), grad_zbot(2), 1/pb
+//   qstatE      [E][QE_N][Q] (+1 pad)  W, e_x, e_y, n_x, n_y, coriolis, tau_wind(2), grad_zbot(2), 1/pb
 //   nstatE      [E][NE_N][P]          e_x, e_y, n_x, n_y, w, 1/pbprime, massinv, pbprime
 //   efstat      [E][4][FBLK]          face statics at face quad points (EF_*) and face nodes (EFN_*)
-//   ecoef       [E][4Q + 5P]          per-sub-cycle Q_uu/uv/vv_dp, H_bcl | pbprime_visc, btp_dpp_graduv
+//   ecoef       [E][4Q + 5P] (even)    per-sub-cycle Q_uu/uv/vv_dp, H_bcl | pbprime_visc, btp_dpp_graduv
 //   efcoef      [E][4][4NQ + 10NGL]   per-sub-cycle face Q_*_edge, H_bcl_edge | btp_graduv_dpp_face
 //   accumulators (element-major)      qacc [E][QA_N][Q], nacc [E][NA_N][P],
 //                                     facc [E][4][FA_N][NQ], gfacc [E][4][8][NGL]
@@ -96,7 +96,11 @@ enum EFNStat { EFN_NX = 0, EFN_NY, EFN_W, EFN_PBL, EFN_PBR, EFN_N };
 #define EREC_ACC 20   /* 1: this element keeps the face time averages of local face lf */
 #define EREC_MAP 24
 #define EREC_PF(ngl) (24 + 4 * (ngl))
-#define EREC_SIZE(ngl) (24 + 4 * (ngl) + 2 * (ngl) * (ngl))
+// (records padded to 16 bytes: the stage kernel copies them into LDS with 16-byte LDS-DMA)
+#define EREC_SIZE(ngl) ((24 + 4 * (ngl) + 2 * (ngl) * (ngl) + 3) & ~3)
+// per-element strides of the element-major double records, even (16-byte aligned records)
+__host__ __device__ constexpr int qe_stride(int Q) { return (QE_N * Q + 1) & ~1; }
+__host__ __device__ constexpr int eco_stride(int Q, int P) { return (4 * Q + 5 * P + 1) & ~1; }
 
 // element-major accumulator indices
 #define QACC_I(k, e, q) ((((size_t)(e)) * QA_N + (k)) * Q + (q))

@@ -351,7 +351,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     qcoef[QC_QUV * (size_t)npq + Iq] = quv;
     qcoef[QC_QVV * (size_t)npq + Iq] = qvv;
     qcoef[QC_HBCL * (size_t)npq + Iq] = hb;
-    double *ec = ecoef + (size_t)e * (4 * Q + 5 * P);  // element-major copy for the stage kernel
+    double *ec = ecoef + (size_t)e * eco_stride(Q, P);  // element-major copy for the stage kernel
     ec[QC_QUU * Q + q] = quu;
     ec[QC_QUV * Q + q] = quv;
     ec[QC_QVV * Q + q] = qvv;
@@ -397,7 +397,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     }
     ncoef[NC_PV * (size_t)npoin + I] = pv;
     for (int c = 0; c < 4; c++) ncoef[(NC_D1 + c) * (size_t)npoin + I] = sum[c];
-    double *ec = ecoef + (size_t)e * (4 * Q + 5 * P) + 4 * Q;
+    double *ec = ecoef + (size_t)e * eco_stride(Q, P) + 4 * Q;
     ec[NC_PV * P + p] = pv;
     for (int c = 0; c < 4; c++) ec[(NC_D1 + c) * P + p] = sum[c];
   }

@@ -132,18 +132,36 @@ typedef __attribute__((address_space(1))) void glb_void_t;
 
 // Block-cooperative async copy of ndw dwords, global -> LDS, both contiguous.  One
 // global_load_lds_dword per lane; chunks of 64 dwords rotate over the waves.
-template <int BS>
+// G16: a 16-byte aligned source and destination move in whole 16-byte pieces first
+// (global_load_lds_dwordx4, 1 KiB per wave-instruction: a quarter of the instructions, and of
+// their address processing, of the dword form), the rest dword by dword
+template <int BS, bool G16 = false>
 __device__ __forceinline__ void glds_copy(const void *g, void *l, int ndw, int tid, int &rot) {
   constexpr int NW = BS / 64;
   const int wave = tid >> 6, lane = tid & 63;
-  const int nch = (ndw + 63) >> 6;
+  int d0 = 0;
+  if (G16 && (((uintptr_t)g | (uintptr_t)l) & 15) == 0) {
+    const int n4 = ndw >> 2;
+    const int nch = (n4 + 63) >> 6;
+    int c = (wave - rot) % NW;
+    if (c < 0) c += NW;
+    for (; c < nch; c += NW) {
+      const int i = (c << 6) + lane;
+      if (i < n4)
+        __builtin_amdgcn_global_load_lds((glb_void_t *)((const uint4 *)g + i), (lds_void_t *)((uint4 *)l + (c << 6)),
+                                         16, 0, 0);
+    }
+    rot = (rot + nch) % NW;
+    d0 = n4 << 2;
+  }
+  const int nch = (ndw - d0 + 63) >> 6;
   int c = (wave - rot) % NW;
   if (c < 0) c += NW;
   for (; c < nch; c += NW) {
-    const int i = (c << 6) + lane;
+    const int i = d0 + (c << 6) + lane;
     if (i < ndw)
-      __builtin_amdgcn_global_load_lds((glb_void_t *)((const unsigned *)g + i), (lds_void_t *)((unsigned *)l + (c << 6)),
-                                       4, 0, 0);
+      __builtin_amdgcn_global_load_lds((glb_void_t *)((const unsigned *)g + i),
+                                       (lds_void_t *)((unsigned *)l + d0 + (c << 6)), 4, 0, 0);
   }
   rot = (rot + nch) % NW;
 }
@@ -162,7 +180,7 @@ struct StageCfg {
   static constexpr int ERS = EREC_SIZE(NGL), ERSD = (ERS + 1) / 2;
   static constexpr int FBLK = EF_N * NQ + EFN_N * NGL;      // efstat block per element side
   static constexpr int EFC = 4 * NQ + 10 * NGL;             // efcoef block per element side
-  static constexpr int ECO = 4 * Q + 5 * P;                 // ecoef record per element
+  static constexpr int ECO = eco_stride(Q, P);              // ecoef record per element (4Q + 5P, even)
   static constexpr int NB = 2 * NGL * NQ + NGL * NGL;       // psiq, dpsiq, dpsi (+ a zero slot)
   static_assert(Q <= BS, "one quad-point task per thread");
   static constexpr bool OTF = !SF && NGL >= HNUMO_OTF_MIN_NGL;
@@ -191,31 +209,38 @@ struct StageCfg {
   // in the last D phase, the new state in the other one (dead after D), the face-quad traces of
   // FPRE in term buffer 0 (A2 -> B; D0 writes it first)
   static constexpr bool LEAN = HNUMO_LEAN && NBK != 0 && !SF && !OTF;
+  // G16: 16-byte LDS-DMA for the element's records (glds_copy).  Not in the slim N=7 arena: there
+  // it measured slower (dg25N7L3 persistent 50.2 -> 53.0 us per stage, while dg25L3 persistent
+  // 13.0 -> 12.7 and C4 1.322 -> 1.296 ms; profiles/r03h)
+  static constexpr bool G16 = !SLIM;
   static_assert(!SLIM || (P <= 64 && 3 * P <= EW * 64), "SLIM: one node per lane of the last wave");
   // LDS arena (doubles).  Persistent (A..E); the wall normals of the face nodes are copied
   // out of the face statics (which live in the B region) for E1:
-  static constexpr int O_BASIS = 0, O_EREC = O_BASIS + NB + 1, O_QB = O_EREC + ERSD, O_Q0 = O_QB + 4 * P,
+  // (the regions LDS-DMA writes start on 16 bytes: ev; not the slim arena, which keeps the dword
+  // copies -- see G16)
+  static constexpr int ev(int x) { return SLIM ? x : (x + 1) & ~1; }
+  static constexpr int O_BASIS = 0, O_EREC = ev(O_BASIS + NB + 1), O_QB = ev(O_EREC + ERSD), O_Q0 = O_QB + 4 * P,
                        O_Q2 = O_Q0 + ((SLIM || LEAN) ? 0 : 4 * P), O_QK = O_Q2 + ((SLIM || LEAN) ? 0 : 4 * P),
-                       O_NS = O_QK + QE_KEEP * Q,
-                       O_NC = O_NS + (SLIM ? NE_LDS : NE_N) * P, O_UV = O_NC + (SLIM ? 0 : 5 * P), O_WN = O_UV + 2 * P;
+                       O_NS = ev(O_QK + QE_KEEP * Q),
+                       O_NC = ev(O_NS + (SLIM ? NE_LDS : NE_N) * P), O_UV = O_NC + (SLIM ? 0 : 5 * P), O_WN = O_UV + 2 * P;
   // working arrays: quad-point values (exact: the 7 integrand factors; SF: the 8 weighted
   // integrands F1,F2,G0..G2,H0..H2), B outputs, then a region written only after B that the
   // SF variant also uses for the interpolation partials Y [NYV][NGL][NQ] (A2 -> B)
   static constexpr int NQV = SF ? 8 : 7, NYV = 7;
   // (SLIM: no Laplacian / new-state buffers; the face-quad traces of FPRE, A2 -> B, share the W
   // region with qq and rhs, D -> E)
-  static constexpr int O_QV = O_WN + 8 * NGL, O_GR = O_QV + NQV * Q, O_FQ = O_GR + 4 * P, O_FL = O_FQ + 16 * NQ,
+  static constexpr int O_QV = O_WN + 8 * NGL, O_GR = ev(O_QV + NQV * Q), O_FQ = O_GR + 4 * P, O_FL = O_FQ + 16 * NQ,
                        O_W = O_FL + 8 * NGL, O_QQ = O_W, O_RHS = O_QQ + 4 * P, O_LAP = O_RHS + (LEAN ? 0 : 3 * P),
                        O_QN = O_LAP + ((SLIM || LEAN) ? 0 : 2 * P), O_Y = O_W,
                        W_END0 = O_QN + ((SLIM || LEAN) ? 0 : 4 * P),
                        QN_END_W = W_END0 - O_W,
                        W_END = (SLIM && !SLATE && O_W + 32 * NQ > W_END0) ? O_W + 32 * NQ : W_END0,
-                       O_BIN = (SF && O_Y + NYV * NGL * NQ > W_END) ? O_Y + NYV * NGL * NQ : W_END;
+                       O_BIN = ev((SF && O_Y + NYV * NGL * NQ > W_END) ? O_Y + NYV * NGL * NQ : W_END);
   // B inputs: the bottom-layer qprime, face statics, neighbour traces, face coefficients,
   // reloaded every stage (the persistent kernel: re-fetched behind E1) and overlaid by term
   // buffer 1 once B and the LDG fluxes (D0) are done.  (SLIM: the qprime of A2 in the
   // nodal-gradient slot, written only from B on)
-  static constexpr int B_QP = 0, B_EF = B_QP + (SLIM ? 0 : 3 * P), B_TR = B_EF + 4 * FBLK, B_EC = B_TR + 32 * NGL,
+  static constexpr int B_QP = 0, B_EF = ev(B_QP + (SLIM ? 0 : 3 * P)), B_TR = B_EF + 4 * FBLK, B_EC = B_TR + 32 * NGL,
                        B_SIZE = B_EC + 4 * EFC, O_B = O_BIN;
   // exact: term chunks of RC quad rows, two buffers of [3P][QCP] (odd pitch against bank
   // conflicts), as many rows as the LDS budget allows
@@ -229,7 +254,7 @@ struct StageCfg {
   static constexpr int RCM = RC0 < 1 ? 1 : (RC0 > NQ ? NQ : RC0);
   static constexpr int NCH = (NQ + RCM - 1) / RCM, RC = (NQ + NCH - 1) / NCH, QC = RC * NQ;
   static constexpr int QCP = QC | 1, TSZ = OTF ? 0 : 3 * P * QCP;
-  static constexpr int TB0 = TSZ > B_SIZE ? TSZ : B_SIZE, TB1 = 0;
+  static constexpr int TB0 = ev(TSZ > B_SIZE ? TSZ : B_SIZE), TB1 = 0;
   // SF: first-pass contraction partials U, W [3][2][NGL][NQ] (C1 runs the LDG face fluxes)
   static constexpr int UWSZ = 3 * 2 * NGL * NQ, B_UW = B_SIZE;
   static constexpr int ARENA = O_B + (SF ? B_UW + UWSZ : TB0 + TSZ);
@@ -418,33 +443,33 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   {
     int rot = 0;
     if (!PERSIST || first) {
-      glds_copy<BS>(m.basis, S + C::O_BASIS, 2 * C::NB, tid, rot);
-      glds_copy<BS>(m.erec + (size_t)e * C::ERS, S + C::O_EREC, C::ERS, tid, rot);
-      glds_copy<BS>(m.qstatE + (size_t)e * QE_N * Q, s_qk, 2 * QE_KEEP * Q, tid, rot);
-      if constexpr (!C::SLIM) glds_copy<BS>(a.ecoef + (size_t)e * C::ECO + 4 * Q, s_nc, 2 * 5 * P, tid, rot);
-      glds_copy<BS>(m.nstatE + (size_t)e * NE_N * P, s_ns, 2 * (C::SLIM ? NE_LDS : NE_N) * P, tid, rot);
+      glds_copy<BS, C::G16>(m.basis, S + C::O_BASIS, 2 * C::NB, tid, rot);
+      glds_copy<BS, C::G16>(m.erec + (size_t)e * C::ERS, S + C::O_EREC, C::ERS, tid, rot);
+      glds_copy<BS, C::G16>(m.qstatE + (size_t)e * qe_stride(Q), s_qk, 2 * QE_KEEP * Q, tid, rot);
+      if constexpr (!C::SLIM) glds_copy<BS, C::G16>(a.ecoef + (size_t)e * C::ECO + 4 * Q, s_nc, 2 * 5 * P, tid, rot);
+      glds_copy<BS, C::G16>(m.nstatE + (size_t)e * NE_N * P, s_ns, 2 * (C::SLIM ? NE_LDS : NE_N) * P, tid, rot);
     }
     if (!PERSIST) {
-      glds_copy<BS>(a.qb_in + (size_t)e * 4 * P, s_qb, 8 * P, tid, rot);
-      if (!C::SLIM && !C::LEAN && use_q0) glds_copy<BS>(a.qb0 + (size_t)e * 4 * P, s_q0, 8 * P, tid, rot);
-      if (!C::SLIM && !C::LEAN && use_q2) glds_copy<BS>(a.qb2 + (size_t)e * 4 * P, s_q2, 8 * P, tid, rot);
+      glds_copy<BS, C::G16>(a.qb_in + (size_t)e * 4 * P, s_qb, 8 * P, tid, rot);
+      if (!C::SLIM && !C::LEAN && use_q0) glds_copy<BS, C::G16>(a.qb0 + (size_t)e * 4 * P, s_q0, 8 * P, tid, rot);
+      if (!C::SLIM && !C::LEAN && use_q2) glds_copy<BS, C::G16>(a.qb2 + (size_t)e * 4 * P, s_q2, 8 * P, tid, rot);
       if (m.etsrc) {
         // processor-face halo: each face's neighbour trace from its own slot (the receive
         // slot of a processor face); the slot ids are uniform, scalar loads
 #pragma unroll
         for (int lf = 0; lf < 4; lf++)
-          glds_copy<BS>(a.trace_in + (size_t)m.etsrc[4 * e + lf] * 8 * NGL, s_tr + lf * 8 * NGL, 2 * 8 * NGL, tid, rot);
+          glds_copy<BS, C::G16>(a.trace_in + (size_t)m.etsrc[4 * e + lf] * 8 * NGL, s_tr + lf * 8 * NGL, 2 * 8 * NGL, tid, rot);
       } else {
-        glds_copy<BS>(a.trace_in + (size_t)e * 32 * NGL, s_tr, 2 * 32 * NGL, tid, rot);
+        glds_copy<BS, C::G16>(a.trace_in + (size_t)e * 32 * NGL, s_tr, 2 * 32 * NGL, tid, rot);
       }
     }
     // qprime, the face statics and the face coefficients are constant over a sub-cycle
     // (persistent: the previous stage re-fetched them in E1, see there)
     if (!PERSIST || first) {
       if (m.botfr && qpm != 2)
-        glds_copy<BS>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
-      glds_copy<BS>(m.efstat + (size_t)e * 4 * C::FBLK, s_ef, 2 * 4 * C::FBLK, tid, rot);
-      glds_copy<BS>(a.efcoef + (size_t)e * 4 * C::EFC, s_ec, 2 * 4 * C::EFC, tid, rot);
+        glds_copy<BS, C::G16>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
+      glds_copy<BS, C::G16>(m.efstat + (size_t)e * 4 * C::FBLK, s_ef, 2 * 4 * C::FBLK, tid, rot);
+      glds_copy<BS, C::G16>(a.efcoef + (size_t)e * 4 * C::EFC, s_ec, 2 * 4 * C::EFC, tid, rot);
     }
   }
   if constexpr (PERSIST) {
@@ -473,7 +498,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   double pre[NPRE];
   auto load_pre = [&]() {
     if (tid < Q) {
-      const double *qse = m.qstatE + (size_t)e * QE_N * Q + tid;
+      const double *qse = m.qstatE + (size_t)e * qe_stride(Q) + tid;
 #pragma unroll
       for (int k = 0; k < NST; k++) pre[k] = qse[(QE_KEEP + k) * Q];
       const double *eco = a.ecoef + (size_t)e * C::ECO + tid;
@@ -1622,9 +1647,9 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   if constexpr (PERSIST) {
     if (a.write_trace) {  // a next stage follows
       int rot = 0;
-      if (!C::SLIM && m.botfr && qpm == 0) glds_copy<BS>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
-      glds_copy<BS>(m.efstat + (size_t)e * 4 * C::FBLK, s_ef, 2 * 4 * C::FBLK, tid, rot);
-      glds_copy<BS>(a.efcoef + (size_t)e * 4 * C::EFC, s_ec, 2 * 4 * C::EFC, tid, rot);
+      if (!C::SLIM && m.botfr && qpm == 0) glds_copy<BS, C::G16>(a.qprime + (size_t)(m.L - 1) * 3 * npoin + (size_t)e * 3 * P, s_qp, 6 * P, tid, rot);
+      glds_copy<BS, C::G16>(m.efstat + (size_t)e * 4 * C::FBLK, s_ef, 2 * 4 * C::FBLK, tid, rot);
+      glds_copy<BS, C::G16>(a.efcoef + (size_t)e * 4 * C::EFC, s_ec, 2 * 4 * C::EFC, tid, rot);
     }
   }
 
