@@ -268,7 +268,7 @@ struct StageCfg {
   static constexpr int OF = WIDE ? OFa : Q, OG = WIDE ? OGa : (SLATE ? Q : OF + 4 * NQ), OL = OG + P,
                        WEND = OL + 4 * NGL, BEND = OL;
   // FPRE (exact): A2 also interpolates each face's own-side traces and, on physical
-  // boundaries, the ghost-side traces to the face quad points, into s_fi [4][NQ][8] (in the
+  // boundaries, the ghost-side traces to the face quad points, into s_fi [8][4*NQ] (in the
   // W region, dead from A to D0), so B's face fluxes interpolate only the neighbour traces
   static constexpr bool FPRE = !SF && !SLATE && (SLIM || LEAN || 4 * NQ * 8 <= QN_END_W);
   static constexpr int WTMAX = QC * NGL;  // term tasks of a full chunk
@@ -414,14 +414,17 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   double *s_pq = s_qv + 4 * Q;     // [3][Q] bottom-layer pp, up, vp (exact, A2 -> B)
   double *s_y = S + C::O_Y;        // SF: [NYV][NGL][NQ] interpolation partials
   double *s_grad = S + C::O_GR, *s_qq = S + C::O_QQ;  // [4][P]
-  double *s_fq = S + C::O_FQ;      // [4][NQ][4]: wq, flux, H_kx+flux_x, H_ky+flux_y
+  // [4][4*NQ]: wq, flux, H_kx+flux_x, H_ky+flux_y at (face lf, quad iq) = lf*NQ + iq, component-major
+  // so the face tasks' lanes (consecutive lf*NQ + iq) write consecutive doubles
+  double *s_fq = S + C::O_FQ;
+  constexpr int FQS = 4 * NQ;
   double *s_fl = S + C::O_FL;      // [4][NGL][2]
   // [3][P], [2][P] (LEAN: in the term buffer that is dead in the last D phase)
   double *s_rhs = C::LEAN ? S + C::O_B + C::TB_LAST : S + C::O_RHS;
   double *s_lap = C::LEAN ? s_rhs + 3 * P : S + C::O_LAP;
   // [P][4] (SLIM: in place of the input; LEAN: the other term buffer, dead after D)
   double *s_qn = C::SLIM ? s_qb : (C::LEAN ? S + C::O_B + C::TB_PREV : S + C::O_QN);
-  // FPRE: [4][NQ][8] face-quad traces, own side | ghost side (A2 -> B; LEAN: in term buffer 0)
+  // FPRE: [8][4*NQ] face-quad traces, own side | ghost side (A2 -> B; LEAN: in term buffer 0)
   double *s_fi = C::LEAN ? S + C::O_B + C::TB0 : S + C::O_W;
   double *SI = S + C::O_BIN;       // B inputs
   double *SB = S + C::O_B;         // term buffers / partials
@@ -756,7 +759,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
 #pragma unroll
             for (int c = 0; c < 4; c++) acc[c] = acc[c] + hv[n] * x[c][n];
 #pragma unroll
-          for (int c = 0; c < 4; c++) s_fi[(lf * NQ + iq) * 8 + 4 * part + c] = acc[c];
+          for (int c = 0; c < 4; c++) s_fi[(4 * part + c) * FQS + lf * NQ + iq] = acc[c];
         }
       }
     }
@@ -801,10 +804,10 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     const double pbl = ef[EF_PBLQ * NQ + iq], pbr = ef[EF_PBRQ * NQ + iq];
     if constexpr (C::FPRE) {
       // own side and ghost side interpolated in A2; the neighbour side here
-      const double *fi = s_fi + (lf * NQ + iq) * 8;
+      const double *fi = s_fi + lf * NQ + iq;  // [8][4*NQ]
       double fo[4], fr[4];
 #pragma unroll
-      for (int c = 0; c < 4; c++) fo[c] = fi[c];
+      for (int c = 0; c < 4; c++) fo[c] = fi[c * FQS];
       if (er >= 0) {  // interior or processor face: the neighbour's trace
         double tv[4][NGL], hv[NGL];
 #pragma unroll
@@ -822,7 +825,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           for (int c = 0; c < 4; c++) fr[c] = fr[c] + hv[n] * tv[c][n];
       } else {
 #pragma unroll
-        for (int c = 0; c < 4; c++) fr[c] = fi[4 + c];
+        for (int c = 0; c < 4; c++) fr[c] = fi[(4 + c) * FQS];
       }
 #pragma unroll
       for (int c = 0; c < 4; c++) {
@@ -899,11 +902,11 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     const double flux_x = nxl * quu + nyl * quv - dispu;
     const double flux_y = nxl * qvu + nyl * qvv - dispv;
     const double flux = nxl * fex + nyl * fey;
-    double *fq = s_fq + (lf * NQ + iq) * 4;
+    double *fq = s_fq + lf * NQ + iq;
     fq[0] = ef[EF_W * NQ + iq];
-    fq[1] = flux;
-    fq[2] = H_kx + flux_x;
-    fq[3] = H_ky + flux_y;
+    fq[FQS] = flux;
+    fq[2 * FQS] = H_kx + flux_x;
+    fq[3 * FQS] = H_ky + flux_y;
   };
 
   // ------------------------------------------------------------- B
@@ -1063,9 +1066,9 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       if (r < 0) continue;
       const int lf = r / NGL, n = r % NGL;
       const double sg = s_side[lf] == 0 ? -1.0 : 1.0;  // acc - c == acc + (-c)
-      const double *fq = s_fq + lf * NQ * 4;
+      const double *fq = s_fq + lf * NQ;
 #pragma unroll
-      for (int iq = 0; iq < NQ; iq++) acc = acc + sg * (fq[iq * 4] * s_psiq[n * NQ + iq] * fq[iq * 4 + 1 + v]);
+      for (int iq = 0; iq < NQ; iq++) acc = acc + sg * (fq[iq] * s_psiq[n * NQ + iq] * fq[(1 + v) * FQS + iq]);
     }
     return acc;
   };
@@ -1427,7 +1430,11 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     auto term_task = [&](int k, int t) {
       double *T = tbuf(k);
       const int h = (VSUM && t >= C::WTMAX) ? 1 : 0, tq = t - h * C::WTMAX;
-      const int qi = tq / NGL, i = tq % NGL;
+      // task tq = i*nq_k + qi: consecutive lanes write consecutive quad points of one node's row
+      // of the term buffer (pitch QCP = QC | 1), so a wave's ds_write_b64 lanes hit distinct banks
+      // (qi-major, the lanes were QCP doubles apart: 2-way conflicts)
+      const int nq_k = (k == NCH - 1) ? Q - k * QC : QC;
+      const int i = tq / nq_k, qi = tq - i * nq_k;
       const int q = k * QC + qi, iq = q % NQ, jq = q / NQ;
       const double wq = s_qk[qe_pos(QE_W, q, Q)], ex = s_qk[qe_pos(QE_EX, q, Q)], ey = s_qk[qe_pos(QE_EY, q, Q)];
       const double nx = s_qk[qe_pos(QE_NX, q, Q)], ny = s_qk[qe_pos(QE_NY, q, Q)];
@@ -1485,17 +1492,17 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           if (r < 0) continue;
           const int lf = r / NGL, n = r % NGL;
           const double sg = s_side[lf] == 0 ? -1.0 : 1.0;
-          const double *fq = s_fq + lf * NQ * 4;
+          const double *fq = s_fq + lf * NQ;
           constexpr int FB = (NQ + 1) / 2;  // points per load batch
 #pragma unroll
           for (int i0 = 0; i0 < NQ; i0 += FB) {
             double c[3][FB], fw[FB], ps[FB];
 #pragma unroll
             for (int iq = i0; iq < i0 + FB && iq < NQ; iq++) {
-              fw[iq - i0] = fq[iq * 4];
+              fw[iq - i0] = fq[iq];
               ps[iq - i0] = s_psiq[n * NQ + iq];
 #pragma unroll
-              for (int v = 0; v < 3; v++) c[v][iq - i0] = fq[iq * 4 + 1 + v];
+              for (int v = 0; v < 3; v++) c[v][iq - i0] = fq[(1 + v) * FQS + iq];
             }
             asm volatile("" ::: "memory");
 #pragma unroll
@@ -1536,13 +1543,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           if (r < 0) continue;
           const int lf = r / NGL, n = r % NGL;
           const double sg = s_side[lf] == 0 ? -1.0 : 1.0;
-          const double *fq = s_fq + lf * NQ * 4;
+          const double *fq = s_fq + lf * NQ;
           double c[NQ], fw[NQ], ps[NQ];
 #pragma unroll
           for (int iq = 0; iq < NQ; iq++) {
-            fw[iq] = fq[iq * 4];
+            fw[iq] = fq[iq];
             ps[iq] = s_psiq[n * NQ + iq];
-            c[iq] = fq[iq * 4 + 1 + v];
+            c[iq] = fq[(1 + v) * FQS + iq];
           }
           asm volatile("" ::: "memory");
 #pragma unroll
@@ -1585,13 +1592,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
             if (r < 0) continue;
             const int lf = r / NGL, n = r % NGL;
             const double sg = s_side[lf] == 0 ? -1.0 : 1.0;
-            const double *fq = s_fq + lf * NQ * 4;
+            const double *fq = s_fq + lf * NQ;
             double c[NQ], fw[NQ], ps[NQ];
 #pragma unroll
             for (int iq = 0; iq < NQ; iq++) {
-              fw[iq] = fq[iq * 4];
+              fw[iq] = fq[iq];
               ps[iq] = s_psiq[n * NQ + iq];
-              c[iq] = fq[iq * 4 + 1 + v];
+              c[iq] = fq[(1 + v) * FQS + iq];
             }
             asm volatile("" ::: "memory");
 #pragma unroll
@@ -1618,7 +1625,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       const int WT = (k < NCH) ? ((k == NCH - 1) ? (Q - k * QC) : QC) * NGL : 0;  // term tasks
       if constexpr (VSUM) {
         // first node halves on [0, WT), second halves on [WTMAX, WTMAX + WT)
-        if (tid < WT || (tid >= WTMAX && tid < WTMAX + WT)) term_task(k, tid);
+        if ((tid < WT || (tid >= WTMAX && tid < WTMAX + WT)) && !(a.dbg & 64)) term_task(k, tid);
         if (k >= 1 && tid >= C::OVS && !(a.dbg & 4)) vsum_chunk(k - 1);
       } else {
       for_tasks<BS>(tid, 0, WT, [&](int t, bool) { term_task(k, t); });

@@ -48,9 +48,11 @@ for e in list(range(8)) + [256, 257, 512, 513]:
         print(f"    blk {e:4d}: xcc {xcc[e]} se {se[e, 0]} cu {cu[e, 0]:2d} simd {simd[e].tolist()}")
 key = xcc * 1000 + se[:, 0] * 100 + cu[:, 0]
 u, c = np.unique(key, return_counts=True)
-print(f"  distinct CUs used {len(u)}, blocks per CU: {np.bincount(c).tolist()}")
+hist = {int(k): int(n) for k, n in zip(*np.unique(c, return_counts=True))}
+print(f"  distinct CUs used {len(u)}, blocks per CU over the launch -> number of CUs: {hist}")
 
-if pr[:, 26].max() > 0:
+# (slots 24-29: the persistent sub-cycle only; a per-stage launch leaves them unwritten)
+if getattr(eng, "stage_path", "") == "persistent" and (pr[:, 26] > 0).all():
     nst = pr[:, 26].astype(float)
     aw, wk, wt = pr[:, 24] / nst, pr[:, 25] / nst, pr[:, 27] / nst
     print(f"  trace wait per stage (longest thread): mean {wt.mean():.0f} clk, p10 {np.percentile(wt, 10):.0f}, "
