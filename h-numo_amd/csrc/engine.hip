@@ -85,6 +85,7 @@ struct hnumo_engine {
   // events recorded inside the captured step around the corrector sub-cycle's stage kernels
   hipEvent_t evk0 = nullptr, evk1 = nullptr;
   bool capturing = false, kernel_events = false, no_graph = false;
+  bool no_fuse = false;                      // HNUMO_FUSE=0: face kernels and extract launches (A/B)
   int summation = HNUMO_SUM_REFERENCE;        // hnumo_set_summation
   unsigned long long *stage_prof = nullptr;  // HNUMO_STAGE_PROF=1: per-element phase clocks
   int stage_dbg = 0;                         // HNUMO_STAGE_DBG: diagnostic phase switches (timing only)
@@ -159,6 +160,17 @@ static void face_exchange_gdpp(hnumo_engine *e);
 static void face_exchange_cdef(hnumo_engine *e);
 
 // ------------------------------------------------------------------ kernel dispatch
+// On a single rank every face's elements are in the element kernels' launches, so
+// fused_extract(e): the face traces qf of qprime are written by the kernels that write qprime
+// (mom_elem, cons_elem) instead of by extract launches after them (the face traces of a qprime
+// uploaded by the host are extracted at the upload, upload_state);
+// fused_faces(e): the layer mass and consistency fluxes of a face are formed by the element
+// kernels of both its elements instead of by the face kernels before them (HNUMO_FUSE=0: off).
+static bool fused_extract(const hnumo_engine *e) {
+  return e->comm_mode == 0 && e->nranks == 1 && !e->face_halo && !e->no_fuse;
+}
+static bool fused_faces(const hnumo_engine *e) { return fused_extract(e); }
+
 template <int NGL, int NQ>
 struct Launch {
   static constexpr int BSE = ((NQ * NQ + 63) / 64) * 64;
@@ -278,15 +290,22 @@ struct Launch {
   }
   // layer mass update (owned elements); produces dp' (e->dpp) for the consistency step
   // (q_in: the layer thicknesses entering the update; q: where they are written)
+  // (single rank: the element kernels form their faces' fluxes themselves, fused_faces)
   static void mass(hnumo_engine *e, const double *qp, const double *qf, const double *q_in, double *q) {
-    hipLaunchKernelGGL((mass_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
-                       e->fmass, e->slmf_face);
+    const bool fz = fused_faces(e);
+    if (!fz)
+      hipLaunchKernelGGL((mass_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
+                         e->fmass, e->slmf_face);
     hipLaunchKernelGGL((mass_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(Blk<NGL, NQ>::BSW), 0, e->stream, e->m, qp,
-                       e->qacc, e->fmass, q_in, q, e->slmf, e->dpp, e->neg_flag);
+                       e->qacc, e->fmass, q_in, q, e->slmf, e->dpp, e->neg_flag, fz ? qf : nullptr, e->facc,
+                       e->slmf_face);
   }
-  static void cons(hnumo_engine *e, double *q, double *qp_out, int finalize_dp) {
-    hipLaunchKernelGGL((cons_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, e->dpp,
-                       e->facc, e->slmf_face, e->fcons, e->face_halo ? e->cdef : nullptr);
+  // (qf: the face traces of qp_out's thickness written by cons_elem itself -- fused extract)
+  static void cons(hnumo_engine *e, double *q, double *qp_out, int finalize_dp, double *qf = nullptr) {
+    const bool fz = fused_faces(e);
+    if (!fz)
+      hipLaunchKernelGGL((cons_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, e->dpp,
+                         e->facc, e->slmf_face, e->fcons, e->face_halo ? e->cdef : nullptr);
     if (e->face_halo) {  // mass_deficit_mass_face halo (mod_layer_terms.F90:135)
       face_exchange_cdef(e);
       if (e->NS)
@@ -294,20 +313,21 @@ struct Launch {
                          e->cdef, e->d_sface, e->NS, e->fcons);
     }
     hipLaunchKernelGGL((cons_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(Blk<NGL, NQ>::BSW), 0, e->stream, e->m, e->dpp,
-                       e->qacc, e->slmf, e->fcons, q, qp_out, finalize_dp);
+                       e->qacc, e->slmf, e->fcons, q, qp_out, finalize_dp, qf, fz ? e->facc : nullptr,
+                       e->slmf_face);
   }
   // (q_in: the momenta entering the update; mode 1 writes the final qprime, see mom_elem_kernel)
   // (qp_avg0, qf_avg0: the corrector's thickness averages of ti_rk_bcl.F90:78-80, formed by the two
   // kernels on load instead of by a launch before them; the final qprime(1) is then qp_in's own)
   static void momentum(hnumo_engine *e, const double *qf, const double *qp_in, const double *qb, const double *q_in,
                        double *q, double *qp_out, int mode, const double *qp_avg0 = nullptr,
-                       const double *qf_avg0 = nullptr) {
+                       const double *qf_avg0 = nullptr, double *qf_out = nullptr) {
     if (e->lapq_on) lapq_bcl(e, qp_in);
     hipLaunchKernelGGL((mom_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
                        e->gdpp_face, e->gfacc, e->momL, e->momR, e->lapf, qf_avg0);
     hipLaunchKernelGGL((mom_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(MomCfg<NGL, NQ>::BS), 0, e->stream, e->m, qp_in, e->qacc,
                        e->nacc, e->dpp_graduv, e->dpprime_visc, e->momL, e->momR, e->lapf, qb, q_in, q, qp_out, mode,
-                       e->lapq_on ? e->lapq : nullptr, e->dpp2, e->neg_flag, qp_avg0);
+                       e->lapq_on ? e->lapq : nullptr, e->dpp2, e->neg_flag, qp_avg0, qf_out);
   }
 };
 
@@ -618,7 +638,7 @@ static void subcycle_prologue(hnumo_engine *e, const double *qb_state, unsigned 
 }
 
 static void launch_bcl_coeffs(hnumo_engine *e, double *qp, double *qf) {
-  DISPATCH(e, extract(e, qp, qf, 0));
+  if (!fused_extract(e)) DISPATCH(e, extract(e, qp, qf, 0));
   DISPATCH(e, bcl_coeffs(e, qp, qf));
 }
 
@@ -777,7 +797,8 @@ static void launch_predict(hnumo_engine *e) {
   DISPATCH(e, mass(e, e->qp, e->qf, e->q, e->q2));
   exchange_dpp(e);
   DISPATCH(e, cons(e, e->q2, nullptr, 0));
-  DISPATCH(e, momentum(e, e->qf, e->qp, e->qbp, e->q, e->q2, e->qp2, 0));
+  DISPATCH(e, momentum(e, e->qf, e->qp, e->qbp, e->q, e->q2, e->qp2, 0, nullptr, nullptr,
+                       fused_extract(e) ? e->qf2 : nullptr));
   exchange_qp(e, e->qp2);
 }
 
@@ -785,16 +806,17 @@ static void launch_predict(hnumo_engine *e) {
 static void launch_step(hnumo_engine *e) {
   const size_t n3 = 3 * (size_t)e->npoin * e->L, nf = 6 * e->FN * e->L, nl = (size_t)e->npoin * e->L;
   int blocks = (int)std::min<size_t>((nl + 255) / 256, 4096);
+  const bool fx = fused_extract(e);
   launch_predict(e);
-  DISPATCH(e, extract(e, e->qp2, e->qf2, 0));
+  if (!fx) DISPATCH(e, extract(e, e->qp2, e->qf2, 0));
   // correction (ti_rk_bcl.F90:62-85)
   DISPATCH(e, bcl_coeffs(e, e->qp2, e->qf2, e->qp, e->qf));
   launch_subcycle(e, e->qb, e->qp2, true);
   DISPATCH(e, mass(e, e->qp2, e->qf2, e->q, e->q));
   exchange_dpp(e);
-  DISPATCH(e, cons(e, e->q, e->qp2, 1));
+  DISPATCH(e, cons(e, e->q, e->qp2, 1, fx ? e->qf2 : nullptr));
   exchange_qp(e, e->qp2);
-  DISPATCH(e, extract(e, e->qp2, e->qf2, 1));
+  if (!fx) DISPATCH(e, extract(e, e->qp2, e->qf2, 1));
   // (the corrector's momentum update writes the final qprime_df -- thickness dpp2, momenta of
   // evaluate_bcl_v1 -- and checks the barotropic state, ti_rk_bcl.F90:81-84; the thickness averages
   // of :78-80 are formed by its kernels on load, except with the quad-point LDG Laplacian, which
@@ -802,9 +824,9 @@ static void launch_step(hnumo_engine *e) {
   if (e->lapq_on) {
     hipLaunchKernelGGL(dp_average_face_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp2, e->qp, e->dpp2, nl,
                        e->qf2, e->qf, nf / 3);
-    DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qb, e->q, e->q, e->qp, 1));
+    DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qb, e->q, e->q, e->qp, 1, nullptr, nullptr, fx ? e->qf : nullptr));
   } else {
-    DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qb, e->q, e->q, e->qp, 1, e->qp, e->qf));
+    DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qb, e->q, e->q, e->qp, 1, e->qp, e->qf, fx ? e->qf : nullptr));
   }
   exchange_qp(e, e->qp);
   // ad_mlswe > 0 with the reference's corrector input leaves NaN layer momenta (hnumo_params)
@@ -1215,6 +1237,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   if (const char *sm = getenv("HNUMO_SUMMATION"))
     eng->summation = (sm[0] == 'r' || sm[0] == '0') ? HNUMO_SUM_REFERENCE : HNUMO_SUM_FACTORED;
   if (const char *sd = getenv("HNUMO_STAGE_DBG")) eng->stage_dbg = atoi(sd);
+  if (const char *fz = getenv("HNUMO_FUSE")) eng->no_fuse = fz[0] == '0';
   // per-stage kernel arena: on meshes that take several residency rounds per stage, the arena
   // sized for 4 workgroups per CU (1-row term chunks) -- 1.566 -> 1.517 ms per stage at C4
   // (tools/ab_env.py, round 2); small meshes keep the 3-per-CU arena
@@ -1404,6 +1427,7 @@ static int upload_state(hnumo_engine *eng, const double *q, const double *qb, co
   if (q) HIPCHK(hipMemcpyAsync(eng->q, q, n3 * 8, hipMemcpyHostToDevice, eng->stream));
   if (qb) HIPCHK(hipMemcpyAsync(eng->qb, qb, 4 * (size_t)eng->npoin * 8, hipMemcpyHostToDevice, eng->stream));
   if (qp) HIPCHK(hipMemcpyAsync(eng->qp, qp, n3 * 8, hipMemcpyHostToDevice, eng->stream));
+  if (qp && fused_extract(eng)) DISPATCH(eng, extract(eng, eng->qp, eng->qf, 0));
   return 0;
 }
 

@@ -293,6 +293,53 @@ __global__ void extract_face_kernel(DevMesh m, const double *qp, double *qf, int
   }
 }
 
+// extract_qprime_df_face fused into the kernel that writes the nodal qprime (single rank, every
+// face's elements in the launch): the thread of node p writes, for each face point r = lf*NGL + n
+// at p (node_faces), its element's side of face lf and, on a physical boundary (er < 0), the
+// ghost side -- the values extract_face_kernel would read back from qprime, the same arithmetic.
+// v[k][c] = qprime(c, p, k) of the node; only_dp: component 0 alone (extract_dprime_df_face).
+template <int NGL>
+__device__ __forceinline__ void extract_node_faces(const DevMesh &m, double *qf, const int *s_face, const int *s_side,
+                                                   const int *s_bc, int r0, int r1, const double (*v)[3], int only_dp) {
+  const int F = m.nface, L = m.L;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int r = h ? r1 : r0;
+    if (r < 0) continue;
+    const int lf = r / NGL, n = r - lf * NGL, f = s_face[lf], s = s_side[lf], er = s_bc[lf];
+    const size_t gid = (size_t)f * NGL + n;
+    double nx = 0.0, ny = 0.0;
+    if (!only_dp && er == -4) {
+      nx = m.fnstat[FN_NX * (size_t)F * NGL + gid];
+      ny = m.fnstat[FN_NY * (size_t)F * NGL + gid];
+    }
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      if (k >= L) break;
+      const double l0 = v[k][0];
+      QF(0, s, n, f, k) = l0;
+      if (er <= 0) QF(0, 1, n, f, k) = l0;
+      if (only_dp) continue;
+      const double l1 = v[k][1], l2 = v[k][2];
+      QF(1, s, n, f, k) = l1;
+      QF(2, s, n, f, k) = l2;
+      if (er <= 0) {
+        double r1_ = l1, r2_ = l2;
+        if (er == -4) {
+          double un = l1 * nx + l2 * ny;
+          r1_ = l1 - 2.0 * un * nx;
+          r2_ = l2 - 2.0 * un * ny;
+        } else if (er == -2) {
+          r1_ = -l1;
+          r2_ = -l2;
+        }
+        QF(1, 1, n, f, k) = r1_;
+        QF(2, 1, n, f, k) = r2_;
+      }
+    }
+  }
+}
+
 // ======================================================= btp_bcl_coeffs_qdf: element
 // Q_uu_dp, Q_uv_dp, Q_vv_dp, H_bcl at quad points (mod_barotropic_terms.F90:265-283);
 // dpp_graduv, btp_dpp_graduv, pbprime_visc at nodes (:287-304).  dpprime_visc =
@@ -522,6 +569,45 @@ __global__ void __launch_bounds__(64)
 // create_layer_mass_flux (mod_create_rhs_mlswe.F90:922-1034): upwind mass flux per face,
 // layer and face quad point: fmass[k][f*NQ+iq] = nx*flux_edge_u + ny*flux_edge_v; the
 // element kernels apply -/+ (wq*hi)*flux in the reference's order.
+// create_layer_mass_flux at (face f, quad point iq) from the face's qf block staged as s_qf
+// [MAXL][6*NGL] (stage_qf): fm[k] = nx*flux_edge_u + ny*flux_edge_v per layer and the layer sums
+// (su, sv) -- one restatement for mass_flux_face_kernel and mass_elem_kernel's fused faces
+template <int NGL, int NQ>
+__device__ __forceinline__ void mass_flux_at(const DevMesh &m, const double (*s_qf)[6 * NGL], const double *s_psiq,
+                                              const double *facc, int f, int iq, double fm[MAXL], double &su,
+                                              double &sv) {
+  const int F = m.nface, L = m.L;
+  const size_t FQ = (size_t)F * NQ, fq = (size_t)f * NQ + iq;
+  double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
+  const int sa = m.fslotA[f];
+  double qbl0 = facc[FACC_I(FA_OPEL, sa, iq)], qbr0 = facc[FACC_I(FA_OPER, sa, iq)];
+  double qbl1 = facc[FACC_I(FA_UL, sa, iq)], qbr1 = facc[FACC_I(FA_UR, sa, iq)];
+  double qbl2 = facc[FACC_I(FA_VL, sa, iq)], qbr2 = facc[FACC_I(FA_VR, sa, iq)];
+  su = 0.0;
+  sv = 0.0;
+#pragma unroll
+  for (int k = 0; k < MAXL; k++) {
+    if (k >= L) break;
+    double ql[3] = {0, 0, 0}, qr[3] = {0, 0, 0};
+#pragma unroll
+    for (int n = 0; n < NGL; n++) {
+      double hi = s_psiq[n * NQ + iq];
+      for (int v = 0; v < 3; v++) {
+        ql[v] = ql[v] + hi * SQF(v, 0, n, k);
+        qr[v] = qr[v] + hi * SQF(v, 1, n, k);
+      }
+    }
+    double uu = 0.5 * ((ql[1] + qbl1) + (qr[1] + qbr1));
+    double vv = 0.5 * ((ql[2] + qbl2) + (qr[2] + qbr2));
+    double dpl = qbl0 * ql[0], dpr = qbr0 * qr[0];
+    double feu = (uu * nxl > 0.0) ? uu * dpl : uu * dpr;
+    double fev = (vv * nyl > 0.0) ? vv * dpl : vv * dpr;
+    su = su + feu;
+    sv = sv + fev;
+    fm[k] = nxl * feu + nyl * fev;
+  }
+}
+
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(64)
     mass_flux_face_kernel(DevMesh m, const double *qf, const double *facc, double *fmass, double *slmf_face) {
@@ -533,34 +619,10 @@ __global__ void __launch_bounds__(64)
   __syncthreads();
   const size_t FQ = (size_t)F * NQ;
   if (tid < NQ) {
-    const int iq = tid;
-    const size_t fq = (size_t)f * NQ + iq;
-    double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
-    double qbl0 = facc[FACC_I(FA_OPEL, m.fslotA[f], iq)], qbr0 = facc[FACC_I(FA_OPER, m.fslotA[f], iq)];
-    double qbl1 = facc[FACC_I(FA_UL, m.fslotA[f], iq)], qbr1 = facc[FACC_I(FA_UR, m.fslotA[f], iq)];
-    double qbl2 = facc[FACC_I(FA_VL, m.fslotA[f], iq)], qbr2 = facc[FACC_I(FA_VR, m.fslotA[f], iq)];
-    double su = 0.0, sv = 0.0;
-#pragma unroll
-    for (int k = 0; k < MAXL; k++) {
-      if (k >= L) break;
-      double ql[3] = {0, 0, 0}, qr[3] = {0, 0, 0};
-#pragma unroll
-      for (int n = 0; n < NGL; n++) {
-        double hi = s_psiq[n * NQ + iq];
-        for (int v = 0; v < 3; v++) {
-          ql[v] = ql[v] + hi * SQF(v, 0, n, k);
-          qr[v] = qr[v] + hi * SQF(v, 1, n, k);
-        }
-      }
-      double uu = 0.5 * ((ql[1] + qbl1) + (qr[1] + qbr1));
-      double vv = 0.5 * ((ql[2] + qbl2) + (qr[2] + qbr2));
-      double dpl = qbl0 * ql[0], dpr = qbr0 * qr[0];
-      double feu = (uu * nxl > 0.0) ? uu * dpl : uu * dpr;
-      double fev = (vv * nyl > 0.0) ? vv * dpl : vv * dpr;
-      su = su + feu;
-      sv = sv + fev;
-      fmass[(size_t)k * FQ + fq] = nxl * feu + nyl * fev;
-    }
+    const size_t fq = (size_t)f * NQ + tid;
+    double fm[MAXL], su, sv;
+    mass_flux_at<NGL, NQ>(m, s_qf, s_psiq, facc, f, tid, fm, su, sv);
+    for (int k = 0; k < L; k++) fmass[(size_t)k * FQ + fq] = fm[k];
     slmf_face[0 * FQ + fq] = su;
     slmf_face[1 * FQ + fq] = sv;
   }
@@ -573,6 +635,31 @@ __global__ void __launch_bounds__(64)
 // cdef [L][side][2][F*NQ]; a processor face's side 2 is its neighbour's side 1, which only
 // arrives with the exchange (bcl_create_communicator at mod_layer_terms.F90:135), so its flux
 // is formed afterwards by cons_flux_proc_kernel.
+// evaluate_consistency_face + the upwind selection at face quad point iq of one layer, from the
+// face nodes' dp' of the left (dnl) and right (dnr) side: the side-1 deficits m11, m21 and the flux
+// -- one restatement for cons_flux_face_kernel and cons_elem_kernel's fused faces
+template <int NGL, int NQ>
+__device__ __forceinline__ void cons_face_layer(const double *s_psiq, const double *dnl, const double *dnr, int er,
+                                                int iq, double pbl, double pbr, double d1, double d2, double nxl,
+                                                double nyl, double &m11, double &m21, double &flux) {
+  double ql = 0.0, qr = 0.0;
+#pragma unroll
+  for (int n = 0; n < NGL; n++) ql = ql + s_psiq[n * NQ + iq] * dnl[n];
+  if (er > 0) {
+#pragma unroll
+    for (int n = 0; n < NGL; n++) qr = qr + s_psiq[n * NQ + iq] * dnr[n];
+  } else {
+    qr = ql;
+  }
+  double wl = ql / pbl, wr = qr / pbr;
+  m11 = wl * d1;
+  m21 = wl * d2;
+  double m12 = wr * d1, m22 = wr * d2;
+  double feu = (m11 * nxl > 0.0) ? m11 : m12;
+  double fev = (m21 * nyl > 0.0) ? m21 : m22;
+  flux = nxl * feu + nyl * fev;
+}
+
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(64)
     cons_flux_face_kernel(DevMesh m, const double *dpp, const double *facc, const double *slmf_face, double *fcons,
@@ -599,25 +686,14 @@ __global__ void __launch_bounds__(64)
 #pragma unroll
     for (int k = 0; k < MAXL; k++) {
       if (k >= L) break;
-      double ql = 0.0, qr = 0.0;
-#pragma unroll
-      for (int n = 0; n < NGL; n++) ql = ql + s_psiq[n * NQ + iq] * s_dn[k][0][n];
-      if (er > 0) {
-#pragma unroll
-        for (int n = 0; n < NGL; n++) qr = qr + s_psiq[n * NQ + iq] * s_dn[k][1][n];
-      } else {
-        qr = ql;
-      }
-      double wl = ql / pbl, wr = qr / pbr;
-      double m11 = wl * d1, m21 = wl * d2, m12 = wr * d1, m22 = wr * d2;
+      double m11, m21, fl;
+      cons_face_layer<NGL, NQ>(s_psiq, s_dn[k][0], s_dn[k][1], er, iq, pbl, pbr, d1, d2, nxl, nyl, m11, m21, fl);
       if (cdef) {
         cdef[((size_t)k * 4 + 0) * FQ + fq] = m11;
         cdef[((size_t)k * 4 + 1) * FQ + fq] = m21;
         if (er == 0) continue;  // processor face: cons_flux_proc_kernel after the exchange
       }
-      double feu = (m11 * nxl > 0.0) ? m11 : m12;
-      double fev = (m21 * nyl > 0.0) ? m21 : m22;
-      fcons[(size_t)k * FQ + fq] = nxl * feu + nyl * fev;
+      fcons[(size_t)k * FQ + fq] = fl;
     }
   }
 }
@@ -697,7 +773,11 @@ __global__ void face_unpack_kernel(double *base, const double *buf, const int *s
 template <int NGL, int NQ>
 __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     mass_elem_kernel(DevMesh m, const double *qp, const double *qacc, const double *fmass, const double *q_in,
-                     double *q, double *slmf, double *dpp, int *neg_flag) {
+                     double *q, double *slmf, double *dpp, int *neg_flag, const double *qf, const double *facc,
+                     double *slmf_face) {
+  // qf != NULL (single rank): the layer mass fluxes of the element's four faces are formed here
+  // (mass_flux_at, in place of mass_flux_face_kernel; each face by both its elements, the same
+  // bits), the left element of a face writing its layer sums slmf_face for the consistency step
   constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BSW;
   using QS = typename Blk<NGL, NQ>::QS;
   static_assert(MAXL * P <= BS, "one quad-point sum per thread");
@@ -710,6 +790,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   __shared__ double s_adv[MAXL][P];
   __shared__ double s_fw[4 * NQ], s_fx[MAXL][4 * NQ];  // face weights, layer mass fluxes of the 4 faces
   __shared__ double s_tb[QS::SIZE];                    // quad-sum term buffers
+  __shared__ double s_qfF[4][MAXL][6 * NGL];           // (qf) the four faces' qf blocks
   __shared__ int s_map[4 * NGL], s_face[4], s_side[4];
   load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
   if (tid < 4) {
@@ -717,7 +798,14 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     s_side[tid] = m.eside[e * 4 + tid];
   }
   stage_face_quads<NQ>(s_fw, m.fstat + FS_W * (size_t)F * NQ, 0, 1, m.efaces + e * 4, tid, BS);
-  stage_face_quads<NQ>(&s_fx[0][0], fmass, (size_t)F * NQ, L, m.efaces + e * 4, tid, BS);
+  if (qf) {
+    for (int t = tid; t < 4 * L * 6 * NGL; t += BS) {
+      const int lf = t / (L * 6 * NGL), r = t % (L * 6 * NGL), k = r / (6 * NGL), rr = r % (6 * NGL);
+      s_qfF[lf][k][rr] = qf[((size_t)k * F + m.efaces[e * 4 + lf]) * NGL * 6 + rr];
+    }
+  } else {
+    stage_face_quads<NQ>(&s_fx[0][0], fmass, (size_t)F * NQ, L, m.efaces + e * 4, tid, BS);
+  }
   for (int t = tid; t < 4 * NGL; t += BS) s_map[t] = m.efmap[e * 4 * NGL + t];
   for (int t = tid; t < L * 3 * P; t += BS) {
     int k = t / (3 * P), r = t % (3 * P);
@@ -730,7 +818,25 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   __syncthreads();
   if (*m.runflag & RUN_ABORT) return;  // (a persistent sub-cycle of this run did no work: DevMesh)
   BCL_MARK(0, 1)
-  for (int q = tid; q < Q; q += BS) {
+  // quad points [0, Q); with qf, the four faces' flux tasks from the next whole wave on
+  constexpr int FT0 = ((Q + 63) / 64) * 64;
+  for (int w = tid; w < (qf ? FT0 + 4 * NQ : Q); w += BS) {
+    if (w >= Q) {
+      if (w < FT0) continue;
+      const int lf = (w - FT0) / NQ, iq = (w - FT0) % NQ, f = s_face[lf];
+      double fm[MAXL], su, sv;
+      mass_flux_at<NGL, NQ>(m, s_qfF[lf], s_psiq, facc, f, iq, fm, su, sv);
+#pragma unroll
+      for (int k = 0; k < MAXL; k++)
+        if (k < L) s_fx[k][lf * NQ + iq] = fm[k];
+      if (s_side[lf] == 0) {
+        const size_t FQ = (size_t)F * NQ, fq = (size_t)f * NQ + iq;
+        slmf_face[0 * FQ + fq] = su;
+        slmf_face[1 * FQ + fq] = sv;
+      }
+      continue;
+    }
+    const int q = w;
     const int iq = q % NQ, jq = q / NQ;
     const size_t Iq = (size_t)e * Q + q;
     double qb0 = qacc[QACC_I(QA_OPE, e, q)], qb1 = qacc[QACC_I(QA_UB, e, q)],
@@ -804,7 +910,12 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
 template <int NGL, int NQ>
 __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     cons_elem_kernel(DevMesh m, const double *dpp, const double *qacc, const double *slmf, const double *fcons,
-                     double *q, double *qp_out, int finalize_dp) {
+                     double *q, double *qp_out, int finalize_dp, double *qf, const double *facc,
+                     const double *slmf_face) {
+  // facc != NULL (single rank): the consistency fluxes of the element's four faces are formed here
+  // (cons_face_layer, in place of cons_flux_face_kernel; each face by both its elements, the same bits)
+  // qf (finalize_dp, single rank): extract_dprime_df_face of the new thickness fused into the
+  // finalize (extract_node_faces), in place of the extract launch after this kernel
   constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BSW;
   using QS = typename Blk<NGL, NQ>::QS;
   static_assert(MAXL * P <= BS, "one quad-point sum per thread");
@@ -817,14 +928,25 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   __shared__ double s_new[MAXL][P];
   __shared__ double s_fw[4 * NQ], s_fx[MAXL][4 * NQ];  // face weights, consistency fluxes of the 4 faces
   __shared__ double s_tb[QS::SIZE];                    // quad-sum term buffers
-  __shared__ int s_map[4 * NGL], s_face[4], s_side[4];
+  __shared__ double s_dnF[4][MAXL][2][NGL];            // (facc) dp' at the four faces' left | right nodes
+  __shared__ int s_map[4 * NGL], s_face[4], s_side[4], s_bc[4];
   load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
   if (tid < 4) {
     s_face[tid] = m.efaces[e * 4 + tid];
     s_side[tid] = m.eside[e * 4 + tid];
+    s_bc[tid] = m.ebc[e * 4 + tid];
   }
   stage_face_quads<NQ>(s_fw, m.fstat + FS_W * (size_t)F * NQ, 0, 1, m.efaces + e * 4, tid, BS);
-  stage_face_quads<NQ>(&s_fx[0][0], fcons, (size_t)F * NQ, L, m.efaces + e * 4, tid, BS);
+  if (facc) {
+    for (int t = tid; t < 4 * L * 2 * NGL; t += BS) {
+      const int lf = t / (L * 2 * NGL), r = t % (L * 2 * NGL), k = r / (2 * NGL), sd = (r / NGL) % 2, n = r % NGL;
+      const int f = m.efaces[e * 4 + lf];
+      if (sd == 1 && m.fer[f] <= 0) continue;
+      s_dnF[lf][k][sd][n] = dpp[(size_t)k * npoin + (sd ? m.fnodeR : m.fnodeL)[(size_t)f * NGL + n]];
+    }
+  } else {
+    stage_face_quads<NQ>(&s_fx[0][0], fcons, (size_t)F * NQ, L, m.efaces + e * 4, tid, BS);
+  }
   for (int t = tid; t < 4 * NGL; t += BS) s_map[t] = m.efmap[e * 4 * NGL + t];
   for (int t = tid; t < L * P; t += BS) s_d[t / P][t % P] = dpp[(size_t)(t / P) * npoin + (size_t)e * P + t % P];
   for (int t = tid; t < 5 * Q; t += BS) {
@@ -834,7 +956,28 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   __syncthreads();
   if (*m.runflag & RUN_ABORT) return;  // (a persistent sub-cycle of this run did no work: DevMesh)
   BCL_MARK(1, 1)
-  for (int q = tid; q < Q; q += BS) {
+  // quad points [0, Q); with facc, the four faces' flux tasks from the next whole wave on
+  constexpr int FT0 = ((Q + 63) / 64) * 64;
+  for (int w = tid; w < (facc ? FT0 + 4 * NQ : Q); w += BS) {
+    if (w >= Q) {
+      if (w < FT0) continue;
+      const int lf = (w - FT0) / NQ, iq = (w - FT0) % NQ, f = s_face[lf], er = s_bc[lf];
+      const size_t FQ = (size_t)F * NQ, fq = (size_t)f * NQ + iq;
+      const double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
+      const double d1 = facc[FACC_I(FA_MFX, m.fslotA[f], iq)] - slmf_face[0 * FQ + fq];
+      const double d2 = facc[FACC_I(FA_MFY, m.fslotA[f], iq)] - slmf_face[1 * FQ + fq];
+      const double pbl = m.fstat[FS_PBL * FQ + fq], pbr = m.fstat[FS_PBR * FQ + fq];
+#pragma unroll
+      for (int k = 0; k < MAXL; k++) {
+        if (k >= L) break;
+        double m11, m21, fl;
+        cons_face_layer<NGL, NQ>(s_psiq, s_dnF[lf][k][0], s_dnF[lf][k][1], er, iq, pbl, pbr, d1, d2, nxl, nyl, m11,
+                                 m21, fl);
+        s_fx[k][lf * NQ + iq] = fl;
+      }
+      continue;
+    }
+    const int q = w;
     const int iq = q % NQ, jq = q / NQ;
     const size_t Iq = (size_t)e * Q + q;
     double pb = m.qstat[QS_PB * (size_t)npq + Iq];
@@ -889,7 +1032,16 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     double sum = 0.0;
     for (int k = 0; k < L; k++) sum = sum + s_new[k][p];
     double ope = sum / m.nstat[NS_PB * (size_t)npoin + I];
-    for (int k = 0; k < L; k++) qp_out[((size_t)k * npoin + I) * 3] = s_new[k][p] / ope;
+    double v[MAXL][3];
+    for (int k = 0; k < L; k++) {
+      v[k][0] = s_new[k][p] / ope;
+      qp_out[((size_t)k * npoin + I) * 3] = v[k][0];
+    }
+    if (qf) {
+      int r0, r1;
+      node_faces<NGL>(s_map, p, r0, r1);
+      extract_node_faces<NGL>(m, qf, s_face, s_side, s_bc, r0, r1, v, 1);
+    }
   }
   BCL_MARK(1, 5) BCL_WALL(1, 7)
 }
@@ -1200,7 +1352,9 @@ __global__ void __launch_bounds__(256, 3)
     mom_elem_kernel(DevMesh m, const double *qp_in, const double *qacc, const double *nacc, const double *dpp_graduv,
                     const double *dpprime_visc, const double *momL, const double *momR, const double *lapf,
                     const double *qb, const double *q_in, double *q, double *qp_out, int mode, const double *lapx,
-                    const double *dpp2, int *flag, const double *qp_avg0) {
+                    const double *dpp2, int *flag, const double *qp_avg0, double *qf) {
+  // qf (single rank): extract_qprime_df_face of the new qprime fused into the tail
+  // (extract_node_faces), in place of the extract launch after this kernel
   // qp_avg0 (the corrector, non-NULL: dpp2 is then not read): the layer thicknesses qprime(1)
   // enter as 0.5*(qp_avg0 + qp_in) (ti_rk_bcl.F90:78-79, formed on load) and the final qprime(1)
   // is qp_in's own (dpp2 of :78, read back from qp_in).  The engine passes qp_avg0 == qp_out (both
@@ -1837,6 +1991,7 @@ __global__ void __launch_bounds__(256, 3)
         if (k < L) ope = ope + h[k];
       ope = ope / m.nstat[NS_PB * (size_t)npoin + I];
     }
+    double ov[MAXL][3];
 #pragma unroll
     for (int k = 0; k < MAXL; k++) {
       if (k >= L) break;
@@ -1844,9 +1999,17 @@ __global__ void __launch_bounds__(256, 3)
       qq[1] = nw[k][1];
       qq[2] = nw[k][2];
       double *o = qp_out + ((size_t)k * npoin + I) * 3;
-      o[0] = mode == 0 ? h[k] / ope : (qp_avg0 ? qp_in[((size_t)k * npoin + I) * 3] : dpp2[(size_t)k * npoin + I]);
-      o[1] = uv[k][0] - b3 / b1;
-      o[2] = uv[k][1] - b4 / b1;
+      ov[k][0] = mode == 0 ? h[k] / ope : (qp_avg0 ? qp_in[((size_t)k * npoin + I) * 3] : dpp2[(size_t)k * npoin + I]);
+      ov[k][1] = uv[k][0] - b3 / b1;
+      ov[k][2] = uv[k][1] - b4 / b1;
+      o[0] = ov[k][0];
+      o[1] = ov[k][1];
+      o[2] = ov[k][2];
+    }
+    if (qf) {
+      int r0, r1;
+      node_faces<NGL>(s_map, p, r0, r1);
+      extract_node_faces<NGL>(m, qf, s_face, s_side, s_bc, r0, r1, ov, 0);
     }
     if (mode == 1) {
       const double b2 = qb[I * 4 + 1];
