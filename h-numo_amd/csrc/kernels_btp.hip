@@ -60,6 +60,33 @@
 #ifndef HNUMO_LEAN
 #define HNUMO_LEAN 1
 #endif
+// Wave priorities by role (stage_body, s_setprio; 0: off).  On a CU holding three elements the
+// elements' waves compete for the SIMDs; the waves whose chains a phase waits for -- the volume
+// sums, the last D phase, E -- issue ahead of the ones with slack (the term tasks, which finish
+// behind the sums anyway): PRIO_S for the summing waves in D, PRIO_E for the last D phase and E,
+// 0 for the term tasks, 1 elsewhere
+#ifndef HNUMO_PRIO
+#define HNUMO_PRIO 1
+#endif
+#ifndef HNUMO_PRIO_S
+#define HNUMO_PRIO_S 2
+#endif
+#ifndef HNUMO_PRIO_E
+#define HNUMO_PRIO_E 3
+#endif
+#ifndef HNUMO_PRIO_L
+#define HNUMO_PRIO_L HNUMO_PRIO_E
+#endif
+#ifndef HNUMO_PRIO_B
+#define HNUMO_PRIO_B 1
+#endif
+#define SETPRIO_IF(cond, hi, lo)        \
+  do {                                  \
+    if (cond)                           \
+      __builtin_amdgcn_s_setprio(hi);   \
+    else                                \
+      __builtin_amdgcn_s_setprio(lo);   \
+  } while (0)
 namespace hnumo {
 
 // A trace value with the tag of the stage it is for: one 16-byte write-through store makes
@@ -440,6 +467,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     if (tid == 0) s_prof[20] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
   }
   STAGE_MARK(0);
+  if (HNUMO_PRIO) __builtin_amdgcn_s_setprio(HNUMO_PRIO_B);
   if (a.prof && tid == 0) s_prof[22] = 0;
   const bool use_q0 = !a.rhs_only && a.a1 != 0.0, use_q2 = !a.rhs_only && a.a3 != 0.0;
   const int qpm = (SF || !m.botfr || !a.qpq) ? 0 : a.qpq_mode;  // see StageArgs::qpq
@@ -1335,6 +1363,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       // fluxes and the Laplacian (it alone writes and reads qq and the face fluxes: a wave-local
       // LDS wait, no barrier)
       double acc_r = 0.0, acc_r2 = 0.0;  // SLATE: this thread's volume sum(s), lifted after the barrier
+      if (HNUMO_PRIO) SETPRIO_IF(tid < C::EW * 64, HNUMO_PRIO_S, HNUMO_PRIO_B);  // the volume sums ahead
       if (tid < C::EW * 64) {
         if constexpr (C::OPAIR && !PERSIST) {
           if (tid < P)
@@ -1406,6 +1435,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       }
       LDS_BARRIER();
       STAGE_MARK(C::SLATE ? 7 : 6);
+      if (HNUMO_PRIO) SETPRIO_IF(tid >= C::EW * 64, HNUMO_PRIO_E, HNUMO_PRIO_B);  // E1 runs on the last wave
     } else {
       for_tasks<BS>(tid, 0, 3 * P, otf_task);
       for_tasks<BS>(tid, 3 * P, P, [&](int t, bool) { qq_task(t); });
@@ -1619,9 +1649,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         }
       }
     }
+    // the term-task waves behind everything else, the summing waves ahead
+    if (HNUMO_PRIO)
+      SETPRIO_IF(VSUM ? tid >= C::OVS - (C::OVS & 63) : (OSUM == BS - 64 && tid >= OSUM), HNUMO_PRIO_S, 0);
 #pragma unroll
     for (int k = 0; k <= NCH; k++) {
       asm volatile("" ::: "memory");  // keep LDS reads inside their phase (no hoisting)
+      if (HNUMO_PRIO && k == NCH) __builtin_amdgcn_s_setprio(HNUMO_PRIO_L);
       const int WT = (k < NCH) ? ((k == NCH - 1) ? (Q - k * QC) : QC) * NGL : 0;  // term tasks
       if constexpr (VSUM) {
         // first node halves on [0, WT), second halves on [WTMAX, WTMAX + WT)
@@ -1661,6 +1695,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   }
 
   // ------------------------------------------------------------- E1: update + wall fix
+  if (HNUMO_PRIO && !C::OTF && HNUMO_PRIO_L != HNUMO_PRIO_E) __builtin_amdgcn_s_setprio(HNUMO_PRIO_E);
   // (SLIM: on the last wave, with its registers; otherwise wave 0)
   constexpr int EW0 = (C::SLIM || C::LEAN) ? C::EW * 64 : 0;
   static_assert(P <= 64, "E1 and the nodal gradients run on one wave");
@@ -1749,6 +1784,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         a.trace_out[slot] = val;
     }
   }
+  if (HNUMO_PRIO) __builtin_amdgcn_s_setprio(HNUMO_PRIO_B);
   if constexpr (REGACC) {
     // the sub-cycle's last stage: each accumulating thread writes its time averages once, scaled
     // as btp_finalize_kernel scales the atomically summed ones (mod_rk_mlswe.F90:124-149); the
