@@ -1076,7 +1076,9 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   HIPCHK(hipMemcpy(eng->iconn, conn.data(), conn.size() * sizeof(int), hipMemcpyHostToDevice));
 
   // ---- statics
-  std::vector<double> hb(2 * ngl * nq + 2 * ngl * ngl);
+  // (+ the stage kernel's interleaved copy, basis_pd: 16-byte aligned, the counts above are even)
+  const size_t nb0 = 2 * (size_t)ngl * nq + 2 * (size_t)ngl * ngl;
+  std::vector<double> hb(nb0 + 2 * ngl * nq + ngl * ngl);
   for (int n = 0; n < ngl; n++)
     for (int iq = 0; iq < nq; iq++) {
       hb[n * nq + iq] = mesh->psiq[n + ngl * iq];
@@ -1087,6 +1089,11 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
       hb[2 * ngl * nq + n * ngl + k] = mesh->dpsi[n + ngl * k];
       hb[2 * ngl * nq + ngl * ngl + n * ngl + k] = mesh->psi[n + ngl * k];
     }
+  for (int x = 0; x < ngl * nq; x++) {
+    hb[nb0 + 2 * x] = hb[x];
+    hb[nb0 + 2 * x + 1] = hb[ngl * nq + x];
+  }
+  for (int x = 0; x < ngl * ngl; x++) hb[nb0 + 2 * ngl * nq + x] = hb[2 * ngl * nq + x];
   // the stage kernels drop the zero terms of the nodal derivative sums: psi must be the
   // identity at the LGL nodes (it is, exactly, for the reference's nodal basis)
   for (int n = 0; n < ngl; n++)
@@ -1362,7 +1369,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   m.fslotL = eng->iconn + o_sl; m.fslotR = eng->iconn + o_sr; m.fslotA = eng->iconn + o_sa;
   m.erec = eng->iconn + o_er;
   m.qstatE = eng->qstatE; m.nstatE = eng->nstatE; m.efstat = eng->efstat;
-  m.basis = eng->basis; m.qstat = eng->qstat; m.nstat = eng->nstat; m.fstat = eng->fstat; m.fnstat = eng->fnstat;
+  m.basis = eng->basis; m.basis_pd = eng->basis + nb0; m.qstat = eng->qstat; m.nstat = eng->nstat; m.fstat = eng->fstat; m.fnstat = eng->fnstat;
   m.alpha = eng->alpha;
   m.gravity = par->gravity; m.cd = par->cd_mlswe; m.visc = par->visc_mlswe; m.dt = par->dt; m.dt_btp = par->dt_btp;
   m.botfr = par->botfr;

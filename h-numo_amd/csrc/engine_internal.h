@@ -118,6 +118,7 @@ struct DevMesh {
   const int *erec;                // [E][EREC_SIZE]
   const double *qstatE, *nstatE, *efstat;
   const double *basis;            // psiq[NGL*NQ] dpsiq[NGL*NQ] dpsi[NGL*NGL]
+  const double *basis_pd;         // the stage kernel's copy: (psiq, dpsiq)[NGL*NQ] interleaved, dpsi[NGL*NGL]
   const double *qstat;            // [QS_N][npoin_q]
   const double *nstat;            // [NS_N][npoin]
   const double *fstat;            // [FS_N][F*NQ]

@@ -48,6 +48,14 @@
 #ifndef HNUMO_OTF_PAIR
 #define HNUMO_OTF_PAIR 1
 #endif
+// Interleaved basis in LDS (PDI): psiq(n, iq) and dpsiq(n, iq) adjacent, read together with one
+// ds_read_b128 where the pair is needed (the volume terms) instead of two rows NGL*NQ apart
+#ifndef HNUMO_PDI
+#define HNUMO_PDI 1
+#endif
+#ifndef HNUMO_OPAIR_PERSIST
+#define HNUMO_OPAIR_PERSIST 1
+#endif
 #ifndef HNUMO_OTF_UNROLL
 #define HNUMO_OTF_UNROLL 5
 #endif
@@ -79,6 +87,19 @@
 #endif
 #ifndef HNUMO_PRIO_B
 #define HNUMO_PRIO_B 1
+#endif
+// experiments: B-phase levels of the face wave / quad waves, A2 level of the last wave (-1: base)
+#ifndef HNUMO_PRIO_XF
+#define HNUMO_PRIO_XF -1
+#endif
+#ifndef HNUMO_PRIO_XQ
+#define HNUMO_PRIO_XQ -1
+#endif
+#ifndef HNUMO_PRIO_XA
+#define HNUMO_PRIO_XA -1
+#endif
+#ifndef HNUMO_PRIO_XP
+#define HNUMO_PRIO_XP -1
 #endif
 #define SETPRIO_IF(cond, hi, lo)        \
   do {                                  \
@@ -426,7 +447,21 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   const auto &m = a.m;
   const int npoin = m.npoin;
   double *const S = s_arena;
+  // basis: psiq [NGL][NQ], dpsiq [NGL][NQ] (PDI: interleaved [NGL][NQ][2]), dpsi [NGL][NGL] + a zero slot
   const double *s_psiq = S + C::O_BASIS, *s_dpsiq = s_psiq + NGL * NQ, *s_dpsi = s_dpsiq + NGL * NQ;
+  constexpr bool PDI = HNUMO_PDI;
+  auto PSQ = [&](int x) -> double { return PDI ? s_psiq[2 * x] : s_psiq[x]; };
+  auto DPSQ = [&](int x) -> double { return PDI ? s_psiq[2 * x + 1] : s_dpsiq[x]; };
+  auto PDQ = [&](int x, double &pv, double &dv) {
+    if constexpr (PDI) {
+      const double2 w = reinterpret_cast<const double2 *>(s_psiq)[x];
+      pv = w.x;
+      dv = w.y;
+    } else {
+      pv = s_psiq[x];
+      dv = s_dpsiq[x];
+    }
+  };
   const int *s_er = reinterpret_cast<const int *>(S + C::O_EREC);
   const int *s_side = s_er + EREC_SIDE, *s_bc = s_er + EREC_BC;
   const int *s_nbe = s_er + EREC_NBE, *s_nblf = s_er + EREC_NBLF, *s_map = s_er + EREC_MAP, *s_pf = s_er + EREC_PF(NGL);
@@ -474,7 +509,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   {
     int rot = 0;
     if (!PERSIST || first) {
-      glds_copy<BS, C::G16>(m.basis, S + C::O_BASIS, 2 * C::NB, tid, rot);
+      glds_copy<BS, C::G16>(PDI ? m.basis_pd : m.basis, S + C::O_BASIS, 2 * C::NB, tid, rot);
       glds_copy<BS, C::G16>(m.erec + (size_t)e * C::ERS, S + C::O_EREC, C::ERS, tid, rot);
       glds_copy<BS, C::G16>(m.qstatE + (size_t)e * qe_stride(Q), s_qk, 2 * QE_KEEP * Q, tid, rot);
       if constexpr (!C::SLIM) glds_copy<BS, C::G16>(a.ecoef + (size_t)e * C::ECO + 4 * Q, s_nc, 2 * 5 * P, tid, rot);
@@ -571,6 +606,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   if (tid == 0) S[C::O_BASIS + C::NB] = 0.0;  // zero slot of the dpsi table (nz_coef)
 
   // ------------------------------------------------------------- A2
+  if (HNUMO_PRIO && HNUMO_PRIO_XA >= 0 && PERSIST && C::WIDE && (tid >> 6) == BS / 64 - 1) __builtin_amdgcn_s_setprio(HNUMO_PRIO_XA < 0 ? 0 : HNUMO_PRIO_XA);
   // u_bar, v_bar of the stage-input state once per node (Uk of mod_laplacian_quad.F90:48-49);
   // the face-node wall normals; and the nodal -> quad interpolations of mod_rhs_btp.F90:
   // 141-152, split over threads by variable group: (dp, dpp) | (udp, vdp) | bottom-layer
@@ -684,7 +720,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           const int mm = r / NQ, iq = r % NQ;
           double pa[NGL];
 #pragma unroll
-          for (int n = 0; n < NGL; n++) pa[n] = s_psiq[n * NQ + iq];
+          for (int n = 0; n < NGL; n++) pa[n] = PSQ(n * NQ + iq);
           if (g < 2) {
             double x0 = 0.0, x1 = 0.0;
 #pragma unroll
@@ -713,8 +749,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           double pa[NGL], pb[NGL];
 #pragma unroll
           for (int n = 0; n < NGL; n++) {
-            pa[n] = s_psiq[n * NQ + iq];
-            pb[n] = s_psiq[n * NQ + jq];
+            pa[n] = PSQ(n * NQ + iq);
+            pb[n] = PSQ(n * NQ + jq);
           }
           if (g < 2) {
             // broadcast LDS reads (every lane of the group reads the same node)
@@ -765,7 +801,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           double x[4][NGL], hv[NGL];
 #pragma unroll
           for (int n = 0; n < NGL; n++) {
-            hv[n] = s_psiq[n * NQ + iq];
+            hv[n] = PSQ(n * NQ + iq);
             const int p = s_map[lf * NGL + n];
 #pragma unroll
             for (int c = 0; c < 4; c++) x[c][n] = s_qb[p * 4 + c];
@@ -840,7 +876,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         double tv[4][NGL], hv[NGL];
 #pragma unroll
         for (int n = 0; n < NGL; n++) {
-          hv[n] = s_psiq[n * NQ + iq];
+          hv[n] = PSQ(n * NQ + iq);
 #pragma unroll
           for (int c = 0; c < 4; c++) tv[c][n] = tr[c * NGL + n];
         }
@@ -863,7 +899,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     } else {
 #pragma unroll
     for (int n = 0; n < NGL; n++) {
-      const double hi = s_psiq[n * NQ + iq];
+      const double hi = PSQ(n * NQ + iq);
       const int p = s_map[lf * NGL + n];
       double own[4] = {s_qb[p * 4], s_qb[p * 4 + 1], s_qb[p * 4 + 2], s_qb[p * 4 + 3]};
       double oth[4];
@@ -938,6 +974,11 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   };
 
   // ------------------------------------------------------------- B
+  if (HNUMO_PRIO && C::WIDE && !C::SLATE) {
+    if (PERSIST && HNUMO_PRIO_XA >= 0) __builtin_amdgcn_s_setprio(HNUMO_PRIO_B);
+    if (HNUMO_PRIO_XF >= 0 && tid >= C::OF && tid < C::OF + 64) __builtin_amdgcn_s_setprio(HNUMO_PRIO_XF < 0 ? 0 : HNUMO_PRIO_XF);
+    if (HNUMO_PRIO_XQ >= 0 && tid < C::OF) __builtin_amdgcn_s_setprio(HNUMO_PRIO_XQ < 0 ? 0 : HNUMO_PRIO_XQ);
+  }
   for (int w = tid; w < C::BEND; w += BS) {
     asm volatile("" ::: "memory");
     if (w < Q) {
@@ -948,7 +989,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         // second interpolation pass: sum_mm psiq(mm, jq) Y(var, mm, iq)
 #pragma unroll
         for (int mm = 0; mm < NGL; mm++) {
-          const double pb = s_psiq[mm * NQ + jq];
+          const double pb = PSQ(mm * NQ + jq);
           const double *y = s_y + mm * NQ + iq;
           dp = dp + pb * y[0 * NGL * NQ];
           dpp = dpp + pb * y[1 * NGL * NQ];
@@ -958,7 +999,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         if (m.botfr) {
 #pragma unroll
           for (int mm = 0; mm < NGL; mm++) {
-            const double pb = s_psiq[mm * NQ + jq];
+            const double pb = PSQ(mm * NQ + jq);
             const double *y = s_y + mm * NQ + iq;
             pp = pp + pb * y[4 * NGL * NQ];
             up = up + pb * y[5 * NGL * NQ];
@@ -1096,7 +1137,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       const double sg = s_side[lf] == 0 ? -1.0 : 1.0;  // acc - c == acc + (-c)
       const double *fq = s_fq + lf * NQ;
 #pragma unroll
-      for (int iq = 0; iq < NQ; iq++) acc = acc + sg * (fq[iq] * s_psiq[n * NQ + iq] * fq[(1 + v) * FQS + iq]);
+      for (int iq = 0; iq < NQ; iq++) acc = acc + sg * (fq[iq] * PSQ(n * NQ + iq) * fq[(1 + v) * FQS + iq]);
     }
     return acc;
   };
@@ -1234,7 +1275,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         double u = 0.0, wv = 0.0;
 #pragma unroll
         for (int iq = 0; iq < NQ; iq++) {
-          const double pi = s_psiq[i * NQ + iq], dpi = s_dpsiq[i * NQ + iq];
+          double pi, dpi;
+          PDQ(i * NQ + iq, pi, dpi);
           if (v > 0) u = u + pi * F[iq];
           u = u + dpi * G[iq];
           wv = wv + pi * H[iq];
@@ -1256,7 +1298,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         const double *U = s_uw + ((2 * v) * NGL + i) * NQ, *W = s_uw + ((2 * v + 1) * NGL + i) * NQ;
         double acc = 0.0;
 #pragma unroll
-        for (int jq = 0; jq < NQ; jq++) acc = acc + (s_psiq[j * NQ + jq] * U[jq] + s_dpsiq[j * NQ + jq] * W[jq]);
+        for (int jq = 0; jq < NQ; jq++) acc = acc + (PSQ(j * NQ + jq) * U[jq] + DPSQ(j * NQ + jq) * W[jq]);
         s_rhs[v * P + p] = face_proj(v, p, acc);
       } else {
         const int t = w - 3 * P;
@@ -1283,16 +1325,18 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       // (qstatE: W rows, then e_x/n_x and e_y/n_y interleaved, qe_pos -- stride 2 for the metrics)
       const double *Wq = s_qk + qe_pos(QE_W, 0, Q), *Ex = s_qk + qe_pos(QE_EX, 0, Q), *Ey = s_qk + qe_pos(QE_EY, 0, Q);
       const double *Nx = s_qk + qe_pos(QE_NX, 0, Q), *Ny = s_qk + qe_pos(QE_NY, 0, Q);
-      const double *Pi = s_psiq + i * NQ, *DPi = s_dpsiq + i * NQ, *Pj = s_psiq + j * NQ, *DPj = s_dpsiq + j * NQ;
+      const int bi = i * NQ, bj = j * NQ;
       double acc = 0.0;
 #pragma unroll 1
       for (int jq = 0; jq < NQ; jq++) {
-        const double pj = Pj[jq], dpj = DPj[jq];
+        double pj, dpj;
+        PDQ(bj + jq, pj, dpj);
         const int q0 = jq * NQ;
 #pragma unroll HNUMO_OTF_UNROLL
         for (int iq = 0; iq < NQ; iq++) {
           const int q = q0 + iq;
-          const double pi = Pi[iq], dpi = DPi[iq];
+          double pi, dpi;
+          PDQ(bi + iq, pi, dpi);
           const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
           const double dhdx = h_e * Ex[2 * q] + h_n * Nx[2 * q];
           const double dhdy = h_e * Ey[2 * q] + h_n * Ny[2 * q];
@@ -1313,16 +1357,18 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       // (qstatE: W rows, then e_x/n_x and e_y/n_y interleaved, qe_pos -- stride 2 for the metrics)
       const double *Wq = s_qk + qe_pos(QE_W, 0, Q), *Ex = s_qk + qe_pos(QE_EX, 0, Q), *Ey = s_qk + qe_pos(QE_EY, 0, Q);
       const double *Nx = s_qk + qe_pos(QE_NX, 0, Q), *Ny = s_qk + qe_pos(QE_NY, 0, Q);
-      const double *Pi = s_psiq + i * NQ, *DPi = s_dpsiq + i * NQ, *Pj = s_psiq + j * NQ, *DPj = s_dpsiq + j * NQ;
+      const int bi = i * NQ, bj = j * NQ;
       double acc = 0.0;
 #pragma unroll 1
       for (int jq = 0; jq < NQ; jq++) {
-        const double pj = Pj[jq], dpj = DPj[jq];
+        double pj, dpj;
+        PDQ(bj + jq, pj, dpj);
         const int q0 = jq * NQ;
 #pragma unroll HNUMO_OTF_UNROLL
         for (int iq = 0; iq < NQ; iq++) {
           const int q = q0 + iq;
-          const double pi = Pi[iq], dpi = DPi[iq];
+          double pi, dpi;
+          PDQ(bi + iq, pi, dpi);
           const double h_e = dpi * pj, h_n = pi * dpj;
           const double dhdx = h_e * Ex[2 * q] + h_n * Nx[2 * q];
           const double dhdy = h_e * Ey[2 * q] + h_n * Ny[2 * q];
@@ -1337,16 +1383,18 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       // (qstatE: W rows, then e_x/n_x and e_y/n_y interleaved, qe_pos -- stride 2 for the metrics)
       const double *Wq = s_qk + qe_pos(QE_W, 0, Q), *Ex = s_qk + qe_pos(QE_EX, 0, Q), *Ey = s_qk + qe_pos(QE_EY, 0, Q);
       const double *Nx = s_qk + qe_pos(QE_NX, 0, Q), *Ny = s_qk + qe_pos(QE_NY, 0, Q);
-      const double *Pi = s_psiq + i * NQ, *DPi = s_dpsiq + i * NQ, *Pj = s_psiq + j * NQ, *DPj = s_dpsiq + j * NQ;
+      const int bi = i * NQ, bj = j * NQ;
       double a1 = 0.0, a2 = 0.0;
 #pragma unroll 1
       for (int jq = 0; jq < NQ; jq++) {
-        const double pj = Pj[jq], dpj = DPj[jq];
+        double pj, dpj;
+        PDQ(bj + jq, pj, dpj);
         const int q0 = jq * NQ;
 #pragma unroll HNUMO_OTF_UNROLL
         for (int iq = 0; iq < NQ; iq++) {
           const int q = q0 + iq;
-          const double pi = Pi[iq], dpi = DPi[iq];
+          double pi, dpi;
+          PDQ(bi + iq, pi, dpi);
           const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
           const double dhdx = h_e * Ex[2 * q] + h_n * Nx[2 * q];
           const double dhdy = h_e * Ey[2 * q] + h_n * Ny[2 * q];
@@ -1364,8 +1412,10 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       // LDS wait, no barrier)
       double acc_r = 0.0, acc_r2 = 0.0;  // SLATE: this thread's volume sum(s), lifted after the barrier
       if (HNUMO_PRIO) SETPRIO_IF(tid < C::EW * 64, HNUMO_PRIO_S, HNUMO_PRIO_B);  // the volume sums ahead
+      if (HNUMO_PRIO && HNUMO_PRIO_XP >= 0 && C::OPAIR && (!PERSIST || HNUMO_OPAIR_PERSIST) && (tid >> 6) == 1)
+        __builtin_amdgcn_s_setprio(HNUMO_PRIO_XP < 0 ? 0 : HNUMO_PRIO_XP);  // (the pair wave)
       if (tid < C::EW * 64) {
-        if constexpr (C::OPAIR && !PERSIST) {
+        if constexpr (C::OPAIR && (!PERSIST || HNUMO_OPAIR_PERSIST)) {
           if (tid < P)
             acc_r = otf_sum0(tid);
           else if (tid >= 64 && tid < 64 + P)
@@ -1422,7 +1472,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       if constexpr (C::SLATE) {
         LDS_BARRIER();  // the face fluxes are in
         STAGE_MARK(6);
-        if constexpr (C::OPAIR && !PERSIST) {
+        if constexpr (C::OPAIR && (!PERSIST || HNUMO_OPAIR_PERSIST)) {
           if (tid < P) {
             s_rhs[tid] = face_proj(0, tid, acc_r);
           } else if (tid >= 64 && tid < 64 + P) {
@@ -1470,12 +1520,14 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       const double nx = s_qk[qe_pos(QE_NX, q, Q)], ny = s_qk[qe_pos(QE_NY, q, Q)];
       const double udp = s_qv[0 * Q + q], vdp = s_qv[1 * Q + q], scx = s_qv[2 * Q + q], A = s_qv[3 * Q + q];
       const double quv = s_qv[4 * Q + q], scy = s_qv[5 * Q + q], B = s_qv[6 * Q + q];
-      const double pi = s_psiq[i * NQ + iq], dpi = s_dpsiq[i * NQ + iq];
+      double pi, dpi;
+      PDQ(i * NQ + iq, pi, dpi);
 #pragma unroll
       for (int jj = 0; jj < JH; jj++) {
         const int j = h * JH + jj;
         if (j >= NGL) break;
-        const double pj = s_psiq[j * NQ + jq], dpj = s_dpsiq[j * NQ + jq];
+        double pj, dpj;
+        PDQ(j * NQ + jq, pj, dpj);
         const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
         const double dhdx = h_e * ex + h_n * nx;
         const double dhdy = h_e * ey + h_n * ny;
@@ -1530,7 +1582,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
 #pragma unroll
             for (int iq = i0; iq < i0 + FB && iq < NQ; iq++) {
               fw[iq - i0] = fq[iq];
-              ps[iq - i0] = s_psiq[n * NQ + iq];
+              ps[iq - i0] = PSQ(n * NQ + iq);
 #pragma unroll
               for (int v = 0; v < 3; v++) c[v][iq - i0] = fq[(1 + v) * FQS + iq];
             }
@@ -1578,7 +1630,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
 #pragma unroll
           for (int iq = 0; iq < NQ; iq++) {
             fw[iq] = fq[iq];
-            ps[iq] = s_psiq[n * NQ + iq];
+            ps[iq] = PSQ(n * NQ + iq);
             c[iq] = fq[(1 + v) * FQS + iq];
           }
           asm volatile("" ::: "memory");
@@ -1627,7 +1679,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
 #pragma unroll
             for (int iq = 0; iq < NQ; iq++) {
               fw[iq] = fq[iq];
-              ps[iq] = s_psiq[n * NQ + iq];
+              ps[iq] = PSQ(n * NQ + iq);
               c[iq] = fq[(1 + v) * FQS + iq];
             }
             asm volatile("" ::: "memory");
@@ -1835,7 +1887,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
 template <int NGL, int NQ, bool SF, int NB = 0>
 __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF, NB>::BS), (StageCfg<NGL, NQ, SF, NB>::MINW))
     btp_stage_kernel(StageArgs a) {
-  __shared__ double s_arena[StageCfg<NGL, NQ, SF, NB>::ARENA];
+  __shared__ __attribute__((aligned(16))) double s_arena[StageCfg<NGL, NQ, SF, NB>::ARENA];
   __shared__ unsigned long long s_prof[32];
   stage_body<NGL, NQ, SF, false, StageArgs, NB>(a, s_arena, s_prof, true,
                                                 a.elist ? a.elist[blockIdx.x] : (int)blockIdx.x, threadIdx.x);
@@ -1897,7 +1949,7 @@ template <int NGL, int NQ, bool SF>
 __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ, SF>::MINW))
     btp_subcycle_kernel(SubArgs sa) {
   using C = StageCfg<NGL, NQ, SF>;
-  __shared__ double s_arena[C::ARENA];
+  __shared__ __attribute__((aligned(16))) double s_arena[C::ARENA];
   __shared__ unsigned long long s_prof[32];
   const int e = blockIdx.x, tid = threadIdx.x;
   const unsigned long long ep = *sa.epoch;
