@@ -53,11 +53,19 @@
 #ifndef HNUMO_PDI
 #define HNUMO_PDI 1
 #endif
+// N=7 volume sums of the persistent kernel: all three components of a node on one thread (TRIPLE,
+// sharing hi, dhdx, dhdy), their face lifts on three waves after the barrier
+#ifndef HNUMO_I4
+#define HNUMO_I4 1
+#endif
+#ifndef HNUMO_OTF_TRIPLE
+#define HNUMO_OTF_TRIPLE 1
+#endif
 #ifndef HNUMO_OPAIR_PERSIST
 #define HNUMO_OPAIR_PERSIST 1
 #endif
 #ifndef HNUMO_OTF_UNROLL
-#define HNUMO_OTF_UNROLL 5
+#define HNUMO_OTF_UNROLL 3
 #endif
 // Chunked D phases (StageCfg::VSUM): term tasks split in two node halves, and one summing thread
 // per (component, node) for the whole volume integral (its partial sum in a register)
@@ -87,19 +95,6 @@
 #endif
 #ifndef HNUMO_PRIO_B
 #define HNUMO_PRIO_B 1
-#endif
-// experiments: B-phase levels of the face wave / quad waves, A2 level of the last wave (-1: base)
-#ifndef HNUMO_PRIO_XF
-#define HNUMO_PRIO_XF -1
-#endif
-#ifndef HNUMO_PRIO_XQ
-#define HNUMO_PRIO_XQ -1
-#endif
-#ifndef HNUMO_PRIO_XA
-#define HNUMO_PRIO_XA -1
-#endif
-#ifndef HNUMO_PRIO_XP
-#define HNUMO_PRIO_XP -1
 #endif
 #define SETPRIO_IF(cond, hi, lo)        \
   do {                                  \
@@ -606,7 +601,6 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   if (tid == 0) S[C::O_BASIS + C::NB] = 0.0;  // zero slot of the dpsi table (nz_coef)
 
   // ------------------------------------------------------------- A2
-  if (HNUMO_PRIO && HNUMO_PRIO_XA >= 0 && PERSIST && C::WIDE && (tid >> 6) == BS / 64 - 1) __builtin_amdgcn_s_setprio(HNUMO_PRIO_XA < 0 ? 0 : HNUMO_PRIO_XA);
   // u_bar, v_bar of the stage-input state once per node (Uk of mod_laplacian_quad.F90:48-49);
   // the face-node wall normals; and the nodal -> quad interpolations of mod_rhs_btp.F90:
   // 141-152, split over threads by variable group: (dp, dpp) | (udp, vdp) | bottom-layer
@@ -707,9 +701,12 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     // persistent, after the first stage: the wall normals and u_bar, v_bar of this state are in
     // LDS already (E1 formed u_bar, v_bar of the new state); qpm == 2: pp, up, vp are loaded
     const bool full = !PERSIST || first;
+    // I4 (more quad points than half the block): one task per quad point forms all four of
+    // (dp, dpp, udp, vdp) -- one pass instead of two -- and the bottom layer's three another
+    constexpr bool I4 = !SF && HNUMO_I4 && 2 * Q > BS;
     const int ng = (m.botfr && qpm != 2) ? 3 : 2;
     constexpr int TPG = SF ? NQ * NGL : Q;  // tasks per group
-    const int nint = ng * TPG;
+    const int nint = (I4 ? ng - 1 : ng) * TPG;
     const int T_WN = nint + (full ? 8 * NGL : 0), T_UV = T_WN + (full ? P : 0);
     constexpr int NFP = C::FPRE ? 8 * NQ : 0;  // face-quad pre-interpolation tasks (own | ghost side)
     for (int w = tid; w < T_UV + NFP; w += BS) {
@@ -744,6 +741,29 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
             s_y[(5 * NGL + mm) * NQ + iq] = x1;
             s_y[(6 * NGL + mm) * NQ + iq] = x2;
           }
+        } else if (I4 && g == 0) {
+          const int q = r, iq = q % NQ, jq = q / NQ;
+          double pa[NGL];
+#pragma unroll
+          for (int n = 0; n < NGL; n++) pa[n] = PSQ(n * NQ + iq);
+          double x0 = 0.0, x1 = 0.0, x2 = 0.0, x3 = 0.0;
+#pragma unroll 1
+          for (int mm = 0; mm < NGL; mm++) {
+            const double pbm = PSQ(mm * NQ + jq);
+#pragma unroll
+            for (int n = 0; n < NGL; n++) {
+              const int ip = mm * NGL + n;
+              const double hi = pa[n] * pbm;  // PSIH(n,mm,iq,jq)
+              x0 = x0 + hi * s_qb[ip * 4 + 0];
+              x1 = x1 + hi * s_qb[ip * 4 + 1];
+              x2 = x2 + hi * s_qb[ip * 4 + 2];
+              x3 = x3 + hi * s_qb[ip * 4 + 3];
+            }
+          }
+          s_qv[0 * Q + q] = x0;
+          s_qv[1 * Q + q] = x1;
+          s_qv[2 * Q + q] = x2;
+          s_qv[3 * Q + q] = x3;
         } else {
           const int q = r, iq = q % NQ, jq = q / NQ;
           double pa[NGL], pb[NGL];
@@ -752,7 +772,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
             pa[n] = PSQ(n * NQ + iq);
             pb[n] = PSQ(n * NQ + jq);
           }
-          if (g < 2) {
+          if (!I4 && g < 2) {
             // broadcast LDS reads (every lane of the group reads the same node)
             double x0 = 0.0, x1 = 0.0;
 #pragma unroll 1
@@ -974,11 +994,6 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   };
 
   // ------------------------------------------------------------- B
-  if (HNUMO_PRIO && C::WIDE && !C::SLATE) {
-    if (PERSIST && HNUMO_PRIO_XA >= 0) __builtin_amdgcn_s_setprio(HNUMO_PRIO_B);
-    if (HNUMO_PRIO_XF >= 0 && tid >= C::OF && tid < C::OF + 64) __builtin_amdgcn_s_setprio(HNUMO_PRIO_XF < 0 ? 0 : HNUMO_PRIO_XF);
-    if (HNUMO_PRIO_XQ >= 0 && tid < C::OF) __builtin_amdgcn_s_setprio(HNUMO_PRIO_XQ < 0 ? 0 : HNUMO_PRIO_XQ);
-  }
   for (int w = tid; w < C::BEND; w += BS) {
     asm volatile("" ::: "memory");
     if (w < Q) {
@@ -1406,16 +1421,55 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       acc1 = a1;
       acc2 = a2;
     };
+    // TRIPLE: the three sums of node p on one thread, sharing hi, dhdx, dhdy (otf_sum0's and
+    // otf_sum12's terms, the same order)
+    auto otf_sum012 = [&](int p, double &acc0, double &acc1, double &acc2) {
+      const int i = p % NGL, j = p / NGL;
+      const double *U = s_qv + 0 * Q, *V = s_qv + 1 * Q;
+      const double *SX = s_qv + 2 * Q, *A_ = s_qv + 3 * Q, *UV = s_qv + 4 * Q, *SY = s_qv + 5 * Q, *B_ = s_qv + 6 * Q;
+      const double *Wq = s_qk + qe_pos(QE_W, 0, Q), *Ex = s_qk + qe_pos(QE_EX, 0, Q), *Ey = s_qk + qe_pos(QE_EY, 0, Q);
+      const double *Nx = s_qk + qe_pos(QE_NX, 0, Q), *Ny = s_qk + qe_pos(QE_NY, 0, Q);
+      const int bi = i * NQ, bj = j * NQ;
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll 1
+      for (int jq = 0; jq < NQ; jq++) {
+        double pj, dpj;
+        PDQ(bj + jq, pj, dpj);
+        const int q0 = jq * NQ;
+#pragma unroll HNUMO_OTF_UNROLL
+        for (int iq = 0; iq < NQ; iq++) {
+          const int q = q0 + iq;
+          double pi, dpi;
+          PDQ(bi + iq, pi, dpi);
+          const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
+          const double dhdx = h_e * Ex[2 * q] + h_n * Nx[2 * q];
+          const double dhdy = h_e * Ey[2 * q] + h_n * Ny[2 * q];
+          const double w = Wq[q], uv = UV[q];
+          a0 = a0 + w * (dhdx * U[q] + V[q] * dhdy);
+          a1 = a1 + w * ((hi * SX[q] + dhdx * A_[q]) + uv * dhdy);
+          a2 = a2 + w * ((hi * SY[q] + dhdx * uv) + B_[q] * dhdy);
+        }
+      }
+      acc0 = a0;
+      acc1 = a1;
+      acc2 = a2;
+    };
     if constexpr (C::SLIM) {
       // waves 0..EW-1: the volume sums; the last wave: its register loads, qq, the LDG face
       // fluxes and the Laplacian (it alone writes and reads qq and the face fluxes: a wave-local
       // LDS wait, no barrier)
       double acc_r = 0.0, acc_r2 = 0.0;  // SLATE: this thread's volume sum(s), lifted after the barrier
       if (HNUMO_PRIO) SETPRIO_IF(tid < C::EW * 64, HNUMO_PRIO_S, HNUMO_PRIO_B);  // the volume sums ahead
-      if (HNUMO_PRIO && HNUMO_PRIO_XP >= 0 && C::OPAIR && (!PERSIST || HNUMO_OPAIR_PERSIST) && (tid >> 6) == 1)
-        __builtin_amdgcn_s_setprio(HNUMO_PRIO_XP < 0 ? 0 : HNUMO_PRIO_XP);  // (the pair wave)
       if (tid < C::EW * 64) {
-        if constexpr (C::OPAIR && (!PERSIST || HNUMO_OPAIR_PERSIST)) {
+        if constexpr (HNUMO_OTF_TRIPLE && PERSIST && C::SLATE) {
+          if (tid < P) {
+            double a1_, a2_;
+            otf_sum012(tid, acc_r, a1_, a2_);
+            s_rhs[P + tid] = a1_;  // (lifted after the barrier by waves 1 and 2)
+            s_rhs[2 * P + tid] = a2_;
+          }
+          if (a.prof && tid == 0) s_prof[28] = clock64();
+        } else if constexpr (C::OPAIR && (!PERSIST || HNUMO_OPAIR_PERSIST)) {
           if (tid < P)
             acc_r = otf_sum0(tid);
           else if (tid >= 64 && tid < 64 + P)
@@ -1472,7 +1526,14 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       if constexpr (C::SLATE) {
         LDS_BARRIER();  // the face fluxes are in
         STAGE_MARK(6);
-        if constexpr (C::OPAIR && (!PERSIST || HNUMO_OPAIR_PERSIST)) {
+        if constexpr (HNUMO_OTF_TRIPLE && PERSIST && C::SLATE) {
+          if (tid < P) {
+            s_rhs[tid] = face_proj(0, tid, acc_r);
+          } else if ((tid & 63) < P && tid < 3 * 64) {
+            const int v = tid >> 6, p = tid & 63;
+            s_rhs[v * P + p] = face_proj(v, p, s_rhs[v * P + p]);
+          }
+        } else if constexpr (C::OPAIR && (!PERSIST || HNUMO_OPAIR_PERSIST)) {
           if (tid < P) {
             s_rhs[tid] = face_proj(0, tid, acc_r);
           } else if (tid >= 64 && tid < 64 + P) {
