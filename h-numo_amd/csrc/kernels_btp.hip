@@ -58,6 +58,9 @@
 #ifndef HNUMO_I4
 #define HNUMO_I4 1
 #endif
+#ifndef HNUMO_QPM
+#define HNUMO_QPM 1
+#endif
 #ifndef HNUMO_OTF_TRIPLE
 #define HNUMO_OTF_TRIPLE 1
 #endif
@@ -262,17 +265,25 @@ struct StageCfg {
   // (the regions LDS-DMA writes start on 16 bytes: ev; not the slim arena, which keeps the dword
   // copies -- see G16)
   static constexpr int ev(int x) { return SLIM ? x : (x + 1) & ~1; }
+  // QPM (SLIM): the quad-point values quad-point-major, s_qv [Q][8] = (w, the 7 integrand factors) --
+  // A2's interpolations in slots 0..3 and the bottom layer's in 4..6 until B overwrites them -- so the
+  // on-the-fly sums read a quad point's 8 values as four ds_read_b128 from one address; w moves out of
+  // s_qk, which keeps the metric pairs alone (16-byte aligned)
+  static constexpr bool QPM = SLIM && HNUMO_QPM;
+  static constexpr int QKR = QPM ? 4 : QE_KEEP;  // s_qk rows
+  static constexpr int al2(int x) { return (x + 1) & ~1; }
   static constexpr int O_BASIS = 0, O_EREC = ev(O_BASIS + NB + 1), O_QB = ev(O_EREC + ERSD), O_Q0 = O_QB + 4 * P,
-                       O_Q2 = O_Q0 + ((SLIM || LEAN) ? 0 : 4 * P), O_QK = O_Q2 + ((SLIM || LEAN) ? 0 : 4 * P),
-                       O_NS = ev(O_QK + QE_KEEP * Q),
+                       O_Q2 = O_Q0 + ((SLIM || LEAN) ? 0 : 4 * P),
+                       O_QK = QPM ? al2(O_Q2) : O_Q2 + ((SLIM || LEAN) ? 0 : 4 * P),
+                       O_NS = ev(O_QK + QKR * Q),
                        O_NC = ev(O_NS + (SLIM ? NE_LDS : NE_N) * P), O_UV = O_NC + (SLIM ? 0 : 5 * P), O_WN = O_UV + 2 * P;
   // working arrays: quad-point values (exact: the 7 integrand factors; SF: the 8 weighted
   // integrands F1,F2,G0..G2,H0..H2), B outputs, then a region written only after B that the
   // SF variant also uses for the interpolation partials Y [NYV][NGL][NQ] (A2 -> B)
-  static constexpr int NQV = SF ? 8 : 7, NYV = 7;
+  static constexpr int NQV = (SF || QPM) ? 8 : 7, NYV = 7;
   // (SLIM: no Laplacian / new-state buffers; the face-quad traces of FPRE, A2 -> B, share the W
   // region with qq and rhs, D -> E)
-  static constexpr int O_QV = O_WN + 8 * NGL, O_GR = ev(O_QV + NQV * Q), O_FQ = O_GR + 4 * P, O_FL = O_FQ + 16 * NQ,
+  static constexpr int O_QV = QPM ? al2(O_WN + 8 * NGL) : O_WN + 8 * NGL, O_GR = ev(O_QV + NQV * Q), O_FQ = O_GR + 4 * P, O_FL = O_FQ + 16 * NQ,
                        O_W = O_FL + 8 * NGL, O_QQ = O_W, O_RHS = O_QQ + 4 * P, O_LAP = O_RHS + (LEAN ? 0 : 3 * P),
                        O_QN = O_LAP + ((SLIM || LEAN) ? 0 : 2 * P), O_Y = O_W,
                        W_END0 = O_QN + ((SLIM || LEAN) ? 0 : 4 * P),
@@ -469,6 +480,15 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   double *s_wn = S + C::O_WN;      // [4][2][NGL] face-node normals (wall fix)
   double *s_qv = S + C::O_QV;      // [NQV][Q] (see StageCfg)
   double *s_pq = s_qv + 4 * Q;     // [3][Q] bottom-layer pp, up, vp (exact, A2 -> B)
+  // the quad-point values by role (StageCfg::QPM: quad-point-major): A2's interpolations c = 0..3
+  // (dp, dpp, udp, vdp), the bottom layer's c = 0..2, B's outputs k = 0..6, the weight w, and the
+  // metric pairs (QE_EX, QE_NX, QE_EY, QE_NY)
+  constexpr bool QPM = C::QPM;
+  auto QI = [&](int c, int q) -> double & { return QPM ? s_qv[q * 8 + c] : s_qv[c * Q + q]; };
+  auto QP = [&](int c, int q) -> double & { return QPM ? s_qv[q * 8 + 4 + c] : s_pq[c * Q + q]; };
+  auto QO = [&](int k, int q) -> double & { return QPM ? s_qv[q * 8 + 1 + k] : s_qv[k * Q + q]; };
+  auto QW = [&](int q) -> double { return QPM ? s_qv[q * 8] : s_qk[qe_pos(QE_W, q, Q)]; };
+  auto QK = [&](int c, int q) -> double { return s_qk[qe_pos(c, q, Q) - (QPM ? Q : 0)]; };
   double *s_y = S + C::O_Y;        // SF: [NYV][NGL][NQ] interpolation partials
   double *s_grad = S + C::O_GR, *s_qq = S + C::O_QQ;  // [4][P]
   // [4][4*NQ]: wq, flux, H_kx+flux_x, H_ky+flux_y at (face lf, quad iq) = lf*NQ + iq, component-major
@@ -506,7 +526,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     if (!PERSIST || first) {
       glds_copy<BS, C::G16>(PDI ? m.basis_pd : m.basis, S + C::O_BASIS, 2 * C::NB, tid, rot);
       glds_copy<BS, C::G16>(m.erec + (size_t)e * C::ERS, S + C::O_EREC, C::ERS, tid, rot);
-      glds_copy<BS, C::G16>(m.qstatE + (size_t)e * qe_stride(Q), s_qk, 2 * QE_KEEP * Q, tid, rot);
+      glds_copy<BS, C::G16>(m.qstatE + (size_t)e * qe_stride(Q) + (QPM ? Q : 0), s_qk, 2 * C::QKR * Q, tid, rot);
       if constexpr (!C::SLIM) glds_copy<BS, C::G16>(a.ecoef + (size_t)e * C::ECO + 4 * Q, s_nc, 2 * 5 * P, tid, rot);
       glds_copy<BS, C::G16>(m.nstatE + (size_t)e * NE_N * P, s_ns, 2 * (C::SLIM ? NE_LDS : NE_N) * P, tid, rot);
     }
@@ -557,9 +577,11 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   // keeps the reference's summation order.)
   constexpr int NST = QE_N - QE_KEEP, NPRE = NST + 7;
   double pre[NPRE];
+  double r_wq = 0.0;  // (QPM: the quad task's weight, into s_qv slot 0 in B)
   auto load_pre = [&]() {
     if (tid < Q) {
       const double *qse = m.qstatE + (size_t)e * qe_stride(Q) + tid;
+      if (QPM) r_wq = qse[0];  // (qe_pos(QE_W, q) = q)
 #pragma unroll
       for (int k = 0; k < NST; k++) pre[k] = qse[(QE_KEEP + k) * Q];
       const double *eco = a.ecoef + (size_t)e * C::ECO + tid;
@@ -760,10 +782,10 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
               x3 = x3 + hi * s_qb[ip * 4 + 3];
             }
           }
-          s_qv[0 * Q + q] = x0;
-          s_qv[1 * Q + q] = x1;
-          s_qv[2 * Q + q] = x2;
-          s_qv[3 * Q + q] = x3;
+          QI(0, q) = x0;
+          QI(1, q) = x1;
+          QI(2, q) = x2;
+          QI(3, q) = x3;
         } else {
           const int q = r, iq = q % NQ, jq = q / NQ;
           double pa[NGL], pb[NGL];
@@ -784,8 +806,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
                 x0 = x0 + hi * s_qb[ip * 4 + 2 * g];
                 x1 = x1 + hi * s_qb[ip * 4 + 2 * g + 1];
               }
-            s_qv[(2 * g) * Q + q] = x0;
-            s_qv[(2 * g + 1) * Q + q] = x1;
+            QI(2 * g, q) = x0;
+            QI(2 * g + 1, q) = x1;
           } else {
             double x0 = 0.0, x1 = 0.0, x2 = 0.0;
 #pragma unroll 1
@@ -798,9 +820,9 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
                 x1 = x1 + hi * s_qp[ip * 3 + 1];
                 x2 = x2 + hi * s_qp[ip * 3 + 2];
               }
-            s_pq[0 * Q + q] = x0;
-            s_pq[1 * Q + q] = x1;
-            s_pq[2 * Q + q] = x2;
+            QP(0, q) = x0;
+            QP(1, q) = x1;
+            QP(2, q) = x2;
           }
         }
       } else if (w < T_WN) {
@@ -1022,18 +1044,18 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           }
         }
       } else {
-        dp = s_qv[0 * Q + q];
-        dpp = s_qv[1 * Q + q];
-        udp = s_qv[2 * Q + q];
-        vdp = s_qv[3 * Q + q];
+        dp = QI(0, q);
+        dpp = QI(1, q);
+        udp = QI(2, q);
+        vdp = QI(3, q);
         if (qpm == 2) {
           pp = pre[NST + 4];
           up = pre[NST + 5];
           vp = pre[NST + 6];
         } else if (m.botfr) {
-          pp = s_pq[0 * Q + q];
-          up = s_pq[1 * Q + q];
-          vp = s_pq[2 * Q + q];
+          pp = QP(0, q);
+          up = QP(1, q);
+          vp = QP(2, q);
           if (qpm == 1) {
             double *qq = a.qpq + (size_t)e * 3 * Q + q;
             qq[0] = pp;
@@ -1096,13 +1118,14 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         s_qv[6 * Q + q] = wq * (nx * A + ny * quv);
         s_qv[7 * Q + q] = wq * (nx * quv + ny * B);
       } else {
-        s_qv[0 * Q + q] = udp;
-        s_qv[1 * Q + q] = vdp;
-        s_qv[2 * Q + q] = sc_x;
-        s_qv[3 * Q + q] = Hq + qu;
-        s_qv[4 * Q + q] = quv;
-        s_qv[5 * Q + q] = sc_y;
-        s_qv[6 * Q + q] = Hq + qv;
+        if (QPM) s_qv[q * 8] = r_wq;
+        QO(0, q) = udp;
+        QO(1, q) = vdp;
+        QO(2, q) = sc_x;
+        QO(3, q) = Hq + qu;
+        QO(4, q) = quv;
+        QO(5, q) = sc_y;
+        QO(6, q) = Hq + qv;
       }
     } else if (!C::SLATE && w >= C::OF && w < C::OF + 4 * NQ) {
       face_task(w - C::OF);
@@ -1332,14 +1355,11 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     // zero term can only differ in the sign of zero -- added to a sum that starts at +0 it
     // changes nothing (round-to-nearest never produces -0 from +0 + x).  Then the face
     // projections; qq and the LDG face fluxes run beside; the Laplacian after the barrier.
+    // (quad-point values by role: QO(k, q), k = 0..6 = udp, vdp, scx, A, quv, scy, B; QW, QK -- see QPM)
     auto otf_sum = [&](int t) {
       const int v = t / P, p = t % P, i = p % NGL, j = p / NGL;
       const int r1 = v == 2 ? 5 : 2, r2 = v == 0 ? 0 : (v == 1 ? 3 : 4), r3 = v == 0 ? 1 : (v == 1 ? 4 : 6);
       const bool z1 = v == 0;
-      const double *Q1 = s_qv + r1 * Q, *Q2 = s_qv + r2 * Q, *Q3 = s_qv + r3 * Q;
-      // (qstatE: W rows, then e_x/n_x and e_y/n_y interleaved, qe_pos -- stride 2 for the metrics)
-      const double *Wq = s_qk + qe_pos(QE_W, 0, Q), *Ex = s_qk + qe_pos(QE_EX, 0, Q), *Ey = s_qk + qe_pos(QE_EY, 0, Q);
-      const double *Nx = s_qk + qe_pos(QE_NX, 0, Q), *Ny = s_qk + qe_pos(QE_NY, 0, Q);
       const int bi = i * NQ, bj = j * NQ;
       double acc = 0.0;
 #pragma unroll 1
@@ -1353,10 +1373,10 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           double pi, dpi;
           PDQ(bi + iq, pi, dpi);
           const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
-          const double dhdx = h_e * Ex[2 * q] + h_n * Nx[2 * q];
-          const double dhdy = h_e * Ey[2 * q] + h_n * Ny[2 * q];
-          const double s1 = z1 ? 0.0 : Q1[q];
-          acc = acc + Wq[q] * ((hi * s1 + dhdx * Q2[q]) + Q3[q] * dhdy);
+          const double dhdx = h_e * QK(QE_EX, q) + h_n * QK(QE_NX, q);
+          const double dhdy = h_e * QK(QE_EY, q) + h_n * QK(QE_NY, q);
+          const double s1 = z1 ? 0.0 : QO(r1, q);
+          acc = acc + QW(q) * ((hi * s1 + dhdx * QO(r2, q)) + QO(r3, q) * dhdy);
         }
       }
       return acc;
@@ -1368,10 +1388,6 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     // terms in the same order
     auto otf_sum0 = [&](int p) {
       const int i = p % NGL, j = p / NGL;
-      const double *U = s_qv + 0 * Q, *V = s_qv + 1 * Q;
-      // (qstatE: W rows, then e_x/n_x and e_y/n_y interleaved, qe_pos -- stride 2 for the metrics)
-      const double *Wq = s_qk + qe_pos(QE_W, 0, Q), *Ex = s_qk + qe_pos(QE_EX, 0, Q), *Ey = s_qk + qe_pos(QE_EY, 0, Q);
-      const double *Nx = s_qk + qe_pos(QE_NX, 0, Q), *Ny = s_qk + qe_pos(QE_NY, 0, Q);
       const int bi = i * NQ, bj = j * NQ;
       double acc = 0.0;
 #pragma unroll 1
@@ -1385,19 +1401,15 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           double pi, dpi;
           PDQ(bi + iq, pi, dpi);
           const double h_e = dpi * pj, h_n = pi * dpj;
-          const double dhdx = h_e * Ex[2 * q] + h_n * Nx[2 * q];
-          const double dhdy = h_e * Ey[2 * q] + h_n * Ny[2 * q];
-          acc = acc + Wq[q] * (dhdx * U[q] + V[q] * dhdy);
+          const double dhdx = h_e * QK(QE_EX, q) + h_n * QK(QE_NX, q);
+          const double dhdy = h_e * QK(QE_EY, q) + h_n * QK(QE_NY, q);
+          acc = acc + QW(q) * (dhdx * QO(0, q) + QO(1, q) * dhdy);
         }
       }
       return acc;
     };
     auto otf_sum12 = [&](int p, double &acc1, double &acc2) {
       const int i = p % NGL, j = p / NGL;
-      const double *SX = s_qv + 2 * Q, *A_ = s_qv + 3 * Q, *UV = s_qv + 4 * Q, *SY = s_qv + 5 * Q, *B_ = s_qv + 6 * Q;
-      // (qstatE: W rows, then e_x/n_x and e_y/n_y interleaved, qe_pos -- stride 2 for the metrics)
-      const double *Wq = s_qk + qe_pos(QE_W, 0, Q), *Ex = s_qk + qe_pos(QE_EX, 0, Q), *Ey = s_qk + qe_pos(QE_EY, 0, Q);
-      const double *Nx = s_qk + qe_pos(QE_NX, 0, Q), *Ny = s_qk + qe_pos(QE_NY, 0, Q);
       const int bi = i * NQ, bj = j * NQ;
       double a1 = 0.0, a2 = 0.0;
 #pragma unroll 1
@@ -1411,11 +1423,11 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           double pi, dpi;
           PDQ(bi + iq, pi, dpi);
           const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
-          const double dhdx = h_e * Ex[2 * q] + h_n * Nx[2 * q];
-          const double dhdy = h_e * Ey[2 * q] + h_n * Ny[2 * q];
-          const double w = Wq[q], uv = UV[q];
-          a1 = a1 + w * ((hi * SX[q] + dhdx * A_[q]) + uv * dhdy);
-          a2 = a2 + w * ((hi * SY[q] + dhdx * uv) + B_[q] * dhdy);
+          const double dhdx = h_e * QK(QE_EX, q) + h_n * QK(QE_NX, q);
+          const double dhdy = h_e * QK(QE_EY, q) + h_n * QK(QE_NY, q);
+          const double w = QW(q), uv = QO(4, q);
+          a1 = a1 + w * ((hi * QO(2, q) + dhdx * QO(3, q)) + uv * dhdy);
+          a2 = a2 + w * ((hi * QO(5, q) + dhdx * uv) + QO(6, q) * dhdy);
         }
       }
       acc1 = a1;
@@ -1425,10 +1437,6 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     // otf_sum12's terms, the same order)
     auto otf_sum012 = [&](int p, double &acc0, double &acc1, double &acc2) {
       const int i = p % NGL, j = p / NGL;
-      const double *U = s_qv + 0 * Q, *V = s_qv + 1 * Q;
-      const double *SX = s_qv + 2 * Q, *A_ = s_qv + 3 * Q, *UV = s_qv + 4 * Q, *SY = s_qv + 5 * Q, *B_ = s_qv + 6 * Q;
-      const double *Wq = s_qk + qe_pos(QE_W, 0, Q), *Ex = s_qk + qe_pos(QE_EX, 0, Q), *Ey = s_qk + qe_pos(QE_EY, 0, Q);
-      const double *Nx = s_qk + qe_pos(QE_NX, 0, Q), *Ny = s_qk + qe_pos(QE_NY, 0, Q);
       const int bi = i * NQ, bj = j * NQ;
       double a0 = 0.0, a1 = 0.0, a2 = 0.0;
 #pragma unroll 1
@@ -1442,12 +1450,12 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           double pi, dpi;
           PDQ(bi + iq, pi, dpi);
           const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
-          const double dhdx = h_e * Ex[2 * q] + h_n * Nx[2 * q];
-          const double dhdy = h_e * Ey[2 * q] + h_n * Ny[2 * q];
-          const double w = Wq[q], uv = UV[q];
-          a0 = a0 + w * (dhdx * U[q] + V[q] * dhdy);
-          a1 = a1 + w * ((hi * SX[q] + dhdx * A_[q]) + uv * dhdy);
-          a2 = a2 + w * ((hi * SY[q] + dhdx * uv) + B_[q] * dhdy);
+          const double dhdx = h_e * QK(QE_EX, q) + h_n * QK(QE_NX, q);
+          const double dhdy = h_e * QK(QE_EY, q) + h_n * QK(QE_NY, q);
+          const double w = QW(q), uv = QO(4, q);
+          a0 = a0 + w * (dhdx * QO(0, q) + QO(1, q) * dhdy);
+          a1 = a1 + w * ((hi * QO(2, q) + dhdx * QO(3, q)) + uv * dhdy);
+          a2 = a2 + w * ((hi * QO(5, q) + dhdx * uv) + QO(6, q) * dhdy);
         }
       }
       acc0 = a0;
@@ -1522,6 +1530,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           r_lap[1] = lap_val(1, p);
         }
         if constexpr (C::SLATE) load_e1();
+        if (a.prof && p == 0) s_prof[23] = clock64();  // (the last wave's D work done)
       }
       if constexpr (C::SLATE) {
         LDS_BARRIER();  // the face fluxes are in

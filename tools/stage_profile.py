@@ -50,6 +50,15 @@ key = xcc * 1000 + se[:, 0] * 100 + cu[:, 0]
 u, c = np.unique(key, return_counts=True)
 hist = {int(k): int(n) for k, n in zip(*np.unique(c, return_counts=True))}
 print(f"  distinct CUs used {len(u)}, blocks per CU over the launch -> number of CUs: {hist}")
+# SIMD sharing of the blocks' role waves on each CU (persistent: all blocks resident together):
+# for wave w, the CUs on which two or more blocks run their wave w on the same SIMD
+if getattr(eng, "stage_path", "") == "persistent":
+    for w in range(4):
+        coll = 0
+        for k in u:
+            sims = simd[key == k, w]
+            coll += int(len(sims) != len(set(sims.tolist())))
+        print(f"    wave {w}: CUs with two blocks' wave {w} on one SIMD: {coll} of {len(u)}")
 
 # (slots 24-29: the persistent sub-cycle only; a per-stage launch leaves them unwritten)
 if getattr(eng, "stage_path", "") == "persistent" and (pr[:, 26] > 0).all():
@@ -65,6 +74,9 @@ if getattr(eng, "stage_path", "") == "persistent" and (pr[:, 26] > 0).all():
     ph = [pr[:, k] / nst for k in (8, 9, 10, 11, 29)]
     print("  persistent per-stage phase means: A2 %.0f | B %.0f | D %.0f (wave-0 volume sums %.0f) | E %.0f clk"
           % (ph[0].mean(), ph[1].mean(), ph[2].mean(), ph[4].mean(), ph[3].mean()))
+    if (pr[:, 23] > 0).all() and (pr[:, 28] > 0).all():  # SLATE (N=7): the last stage's D split
+        print("  last stage, from D's start: volume sums done %.0f clk, the last wave's D work done %.0f clk"
+              % ((pr[:, 28] - pr[:, 2]).mean(), (pr[:, 23] - pr[:, 2]).mean()))
     for k in sorted(set(bpc.tolist())):
         sel = bpc == k
         print(f"    CUs with {k} blocks: {sel.sum()} blocks, A(+waits) {aw[sel].mean():.0f}, work {wk[sel].mean():.0f} "
