@@ -65,7 +65,7 @@ struct hnumo_engine {
   int *iconn;
   std::vector<double> ssprk_a, ssprk_beta;  // host copies (kstages x 3), (kstages)
   // state and step temporaries
-  double *q, *qb, *qp, *q2, *qp2, *qbp, *qf, *qf2, *dpp2;
+  double *q, *qb, *qp, *q2, *qp2, *qbp, *qf, *qf2, *qfa, *dpp2;  // (qfa: fused faces, bcl_coeffs)
   double *qbuf[4], *gtrace[2];  // gtrace: [E][4][8][NGL] face traces (qb, grad u_bar) in the reader's slot
   // per-sub-cycle coefficients
   double *qcoef, *ncoef, *fcoef, *fncoef, *dpp_graduv, *dpprime_visc, *gdpp_face;
@@ -253,12 +253,17 @@ struct Launch {
   }
   // (qp_avg, qf_avg: the corrector's averages qp = 0.5*(qp + qp_avg), qf = 0.5*(qf_avg + qf) formed
   // and written back by the two kernels, ti_rk_bcl.F90:64-65)
+  // (single rank, fused_faces: the element kernel forms the face part as well; the corrector's
+  // averaged face traces then go to qf_out = e->qfa, which the rest of the corrector reads)
   static void bcl_coeffs(hnumo_engine *e, double *qp, double *qf, const double *qp_avg = nullptr,
-                         const double *qf_avg = nullptr) {
+                         const double *qf_avg = nullptr, double *qf_out = nullptr) {
+    const bool fz = fused_faces(e);
     hipLaunchKernelGGL((bcl_coeffs_elem_kernel<NGL, NQ>), dim3(e->nelem), dim3(Blk<NGL, NQ>::BSW), 0, e->stream, e->m, qp,
-                       qp_avg, e->qcoef, e->ncoef, e->dpp_graduv, e->dpprime_visc, e->ecoef);
-    hipLaunchKernelGGL((bcl_coeffs_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, qf_avg,
-                       e->dpp_graduv, e->dpprime_visc, e->fcoef, e->fncoef, e->gdpp_face, e->efcoef);
+                       qp_avg, e->qcoef, e->ncoef, e->dpp_graduv, e->dpprime_visc, e->ecoef, fz ? qf : nullptr,
+                       qf_avg, qf_out, e->fcoef, e->fncoef, e->gdpp_face, e->efcoef);
+    if (!fz)
+      hipLaunchKernelGGL((bcl_coeffs_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, qf_avg,
+                         e->dpp_graduv, e->dpprime_visc, e->fcoef, e->fncoef, e->gdpp_face, e->efcoef);
     if (e->face_halo) {  // graduv_dpp_face halo (mod_barotropic_terms.F90:393) and its layer sums
       face_exchange_gdpp(e);
       if (e->NS)
@@ -809,24 +814,25 @@ static void launch_step(hnumo_engine *e) {
   const bool fx = fused_extract(e);
   launch_predict(e);
   if (!fx) DISPATCH(e, extract(e, e->qp2, e->qf2, 0));
-  // correction (ti_rk_bcl.F90:62-85)
-  DISPATCH(e, bcl_coeffs(e, e->qp2, e->qf2, e->qp, e->qf));
+  // correction (ti_rk_bcl.F90:62-85); qfc = the averaged qprime_face2 (fused faces: e->qfa)
+  double *qfc = fused_faces(e) ? e->qfa : e->qf2;
+  DISPATCH(e, bcl_coeffs(e, e->qp2, e->qf2, e->qp, e->qf, qfc == e->qf2 ? nullptr : qfc));
   launch_subcycle(e, e->qb, e->qp2, true);
-  DISPATCH(e, mass(e, e->qp2, e->qf2, e->q, e->q));
+  DISPATCH(e, mass(e, e->qp2, qfc, e->q, e->q));
   exchange_dpp(e);
-  DISPATCH(e, cons(e, e->q, e->qp2, 1, fx ? e->qf2 : nullptr));
+  DISPATCH(e, cons(e, e->q, e->qp2, 1, fx ? qfc : nullptr));
   exchange_qp(e, e->qp2);
-  if (!fx) DISPATCH(e, extract(e, e->qp2, e->qf2, 1));
+  if (!fx) DISPATCH(e, extract(e, e->qp2, qfc, 1));
   // (the corrector's momentum update writes the final qprime_df -- thickness dpp2, momenta of
   // evaluate_bcl_v1 -- and checks the barotropic state, ti_rk_bcl.F90:81-84; the thickness averages
   // of :78-80 are formed by its kernels on load, except with the quad-point LDG Laplacian, which
   // reads the averaged qprime before them)
   if (e->lapq_on) {
     hipLaunchKernelGGL(dp_average_face_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qp2, e->qp, e->dpp2, nl,
-                       e->qf2, e->qf, nf / 3);
-    DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qb, e->q, e->q, e->qp, 1, nullptr, nullptr, fx ? e->qf : nullptr));
+                       qfc, e->qf, nf / 3);
+    DISPATCH(e, momentum(e, qfc, e->qp2, e->qb, e->q, e->q, e->qp, 1, nullptr, nullptr, fx ? e->qf : nullptr));
   } else {
-    DISPATCH(e, momentum(e, e->qf2, e->qp2, e->qb, e->q, e->q, e->qp, 1, e->qp, e->qf, fx ? e->qf : nullptr));
+    DISPATCH(e, momentum(e, qfc, e->qp2, e->qb, e->q, e->q, e->qp, 1, e->qp, e->qf, fx ? e->qf : nullptr));
   }
   exchange_qp(e, e->qp);
   // ad_mlswe > 0 with the reference's corrector input leaves NaN layer momenta (hnumo_params)
@@ -1204,6 +1210,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   eng->q = dalloc<double>(eng, n3); eng->qp = dalloc<double>(eng, n3); eng->qb = dalloc<double>(eng, 4 * npoin);
   eng->q2 = dalloc<double>(eng, n3); eng->qp2 = dalloc<double>(eng, n3); eng->qbp = dalloc<double>(eng, 4 * npoin);
   eng->qf = dalloc<double>(eng, 6 * FN * L); eng->qf2 = dalloc<double>(eng, 6 * FN * L);
+  eng->qfa = dalloc<double>(eng, 6 * FN * L);
   eng->dpp2 = dalloc<double>(eng, npoin * L);
   for (int i = 0; i < 4; i++) eng->qbuf[i] = dalloc<double>(eng, 4 * npoin);
   // trace buffers: element slots [4E], then (processor-face halo) NS send + NS receive slots

@@ -340,6 +340,57 @@ __device__ __forceinline__ void extract_node_faces(const DevMesh &m, double *qf,
   }
 }
 
+// btp_bcl_coeffs_qdf at face quad point iq (mod_barotropic_terms.F90:306-337) from the face's qf
+// block s_qf [MAXL][6*NGL]: Q_*_dp_edge and H_bcl_edge, the average of the two sides -- one
+// restatement for bcl_coeffs_face_kernel and bcl_coeffs_elem_kernel's fused faces
+template <int NGL, int NQ>
+__device__ __forceinline__ void bcl_face_quad(const DevMesh &m, const double (*s_qf)[6 * NGL], const double *s_psiq,
+                                              int iq, double &quu, double &quv, double &qvv, double &hb) {
+  const int L = m.L;
+  double pl = 0, pr = 0;
+  quu = 0;
+  quv = 0;
+  qvv = 0;
+  hb = 0;
+#pragma unroll
+  for (int k = 0; k < MAXL; k++) {
+    if (k >= L) break;
+    double ql[3] = {0, 0, 0}, qr[3] = {0, 0, 0};
+#pragma unroll
+    for (int n = 0; n < NGL; n++) {
+      double hi = s_psiq[n * NQ + iq];
+      for (int v = 0; v < 3; v++) {
+        ql[v] = ql[v] + hi * SQF(v, 0, n, k);
+        qr[v] = qr[v] + hi * SQF(v, 1, n, k);
+      }
+    }
+    quu = quu + 0.5 * ((ql[1] * ql[1] * ql[0]) + (qr[1] * qr[1] * qr[0]));
+    quv = quv + 0.5 * ((ql[2] * ql[1] * ql[0]) + (qr[2] * qr[1] * qr[0]));
+    qvv = qvv + 0.5 * ((ql[2] * ql[2] * ql[0]) + (qr[2] * qr[2] * qr[0]));
+    double pl1 = pl + ql[0];
+    double left_dp = 0.5 * m.alpha[k] * (pl1 * pl1 - pl * pl);
+    double pr1 = pr + qr[0];
+    double right_dp = 0.5 * m.alpha[k] * (pr1 * pr1 - pr * pr);
+    hb = hb + 0.5 * (left_dp + right_dp);
+    pl = pl1;
+    pr = pr1;
+  }
+}
+
+// the ghost side of graduv_dpp_face on a physical boundary (mod_barotropic_terms.F90:360-390):
+// a copy, the two gradient pairs reflected at a free-slip wall (er == -4)
+__device__ __forceinline__ void bcl_face_ghost(const double l[5], double r[5], int er, double nx, double ny) {
+  for (int c = 0; c < 5; c++) r[c] = l[c];
+  if (er == -4) {
+    double un = l[0] * nx + l[1] * ny;
+    r[0] = l[0] - 2.0 * un * nx;
+    r[1] = l[1] - 2.0 * un * ny;
+    un = l[2] * nx + l[3] * ny;
+    r[2] = l[2] - 2.0 * un * nx;
+    r[3] = l[3] - 2.0 * un * ny;
+  }
+}
+
 // ======================================================= btp_bcl_coeffs_qdf: element
 // Q_uu_dp, Q_uv_dp, Q_vv_dp, H_bcl at quad points (mod_barotropic_terms.F90:265-283);
 // dpp_graduv, btp_dpp_graduv, pbprime_visc at nodes (:287-304).  dpprime_visc =
@@ -347,16 +398,46 @@ __device__ __forceinline__ void extract_node_faces(const DevMesh &m, double *qf,
 template <int NGL, int NQ>
 __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     bcl_coeffs_elem_kernel(DevMesh m, double *qp, const double *qp_avg, double *qcoef, double *ncoef,
-                           double *dpp_graduv, double *dpprime_visc, double *ecoef) {
+                           double *dpp_graduv, double *dpprime_visc, double *ecoef, const double *qf,
+                           const double *qf_avg, double *qf_out, double *fcoef, double *fncoef, double *gdpp_face,
+                           double *efcoef) {
   // qp_avg (the corrector): qprime_df2 = 0.5*(qprime_df2 + qprime_df) of the element's nodes first
   // (ti_rk_bcl.F90:64), written back
+  // qf != NULL (single rank): the face part of btp_bcl_coeffs_qdf is formed here too, in place of
+  // bcl_coeffs_face_kernel -- the element's four faces' quad-point coefficients into its own efcoef
+  // slots (both elements of a face compute them, the same bits; the left one writes fcoef), and its
+  // side's face-node dpp_graduv / dpprime_visc traces with their layer sums into gdpp_face, fncoef
+  // and both elements' efcoef slots (a physical boundary: both sides, the ghost side reflected).
+  // qf_avg (the corrector): the averaged qprime_face2 = 0.5*(qprime_face + qprime_face2) goes to
+  // qf_out (not in place: the neighbour reads the face block too), each element writing its side
   constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BSW;
-  const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q;
+  static_assert(BS >= 192 && 4 * NQ <= 64 && 4 * NGL <= 64, "face tasks on waves 1 and 2");
+  const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
   __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
   __shared__ double s_q[MAXL][3][P];
   __shared__ double s_nm[4][P];
   __shared__ double s_g[MAXL][4][P];
+  __shared__ double s_qfF[4][MAXL][6 * NGL];  // (qf) the four faces' qf blocks (averaged)
+  __shared__ int s_map[4 * NGL], s_face[4], s_side[4], s_bc[4];
   load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
+  if (qf) {
+    if (tid < 4) {
+      s_face[tid] = m.efaces[e * 4 + tid];
+      s_side[tid] = m.eside[e * 4 + tid];
+      s_bc[tid] = m.ebc[e * 4 + tid];
+    }
+    for (int t = tid; t < 4 * NGL; t += BS) s_map[t] = m.efmap[e * 4 * NGL + t];
+    for (int t = tid; t < 4 * L * 6 * NGL; t += BS) {
+      const int lf = t / (L * 6 * NGL), r = t % (L * 6 * NGL), k = r / (6 * NGL), rr = r % (6 * NGL);
+      const size_t i = ((size_t)k * F + m.efaces[e * 4 + lf]) * NGL * 6 + rr;
+      double v = qf[i];
+      if (qf_avg) {
+        v = 0.5 * (qf_avg[i] + v);
+        if ((rr / 3) % 2 == m.eside[e * 4 + lf] || m.ebc[e * 4 + lf] <= 0) qf_out[i] = v;
+      }
+      s_qfF[lf][k][rr] = v;
+    }
+  }
   for (int t = tid; t < L * 3 * P; t += BS) {
     int k = t / (3 * P), r = t % (3 * P);
     const size_t i = (size_t)k * 3 * npoin + (size_t)e * 3 * P + r;
@@ -448,6 +529,70 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     ec[NC_PV * P + p] = pv;
     for (int c = 0; c < 4; c++) ec[(NC_D1 + c) * P + p] = sum[c];
   }
+  if (!qf) return;
+  constexpr int EFC = 4 * NQ + 10 * NGL;
+  const size_t FQ = (size_t)F * NQ, FN = (size_t)F * NGL;
+  if (tid >= 64 && tid < 64 + 4 * NQ) {  // face quad points (bcl_coeffs_face_kernel's arithmetic)
+    const int lf = (tid - 64) / NQ, iq = (tid - 64) % NQ;
+    double quu, quv, qvv, hb;
+    bcl_face_quad<NGL, NQ>(m, s_qfF[lf], s_psiq, iq, quu, quv, qvv, hb);
+    const double vals[4] = {quu, quv, qvv, hb};
+    for (int c = 0; c < 4; c++) efcoef[(size_t)(e * 4 + lf) * EFC + c * NQ + iq] = vals[c];
+    if (s_side[lf] == 0) {
+      const size_t fq = (size_t)s_face[lf] * NQ + iq;
+      for (int c = 0; c < 4; c++) fcoef[(FC_QUU + c) * FQ + fq] = vals[c];
+    }
+  } else if (tid >= 128 && tid < 128 + 4 * NGL) {  // face nodes: this element's side
+    const int lf = (tid - 128) / NGL, n = (tid - 128) % NGL, p = s_map[lf * NGL + n];
+    const int s = s_side[lf], er = s_bc[lf];
+    const size_t fn = (size_t)s_face[lf] * NGL + n;
+    double *eo = efcoef + (size_t)(e * 4 + lf) * EFC + 4 * NQ;
+    if (er > 0) {
+      double hs[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < MAXL; k++) {
+        if (k >= L) break;
+        const double d = s_q[k][0][p];
+        double h[5];
+        for (int c = 0; c < 4; c++) h[c] = d * s_g[k][c][p];
+        h[4] = d;
+        for (int c = 0; c < 5; c++) {
+          gdpp_face[((size_t)k * 10 + 5 * s + c) * FN + fn] = h[c];
+          hs[c] = hs[c] + h[c];
+        }
+      }
+      double *en = efcoef + (size_t)(m.enbr_e[e * 4 + lf] * 4 + m.enbr_lf[e * 4 + lf]) * EFC + 4 * NQ;
+      for (int c = 0; c < 5; c++) {
+        fncoef[(size_t)(5 * s + c) * FN + fn] = hs[c];
+        eo[(5 * s + c) * NGL + n] = hs[c];
+        en[(5 * s + c) * NGL + n] = hs[c];
+      }
+    } else {
+      const double nx = m.fnstat[FN_NX * FN + fn], ny = m.fnstat[FN_NY * FN + fn];
+      double bsum[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < MAXL; k++) {
+        if (k >= L) break;
+        const double d = s_q[k][0][p];
+        double l[5], r[5];
+        for (int c = 0; c < 4; c++) l[c] = d * s_g[k][c][p];
+        l[4] = d;
+        bcl_face_ghost(l, r, er, nx, ny);
+        for (int c = 0; c < 5; c++) {
+          gdpp_face[((size_t)k * 10 + c) * FN + fn] = l[c];
+          gdpp_face[((size_t)k * 10 + 5 + c) * FN + fn] = r[c];
+        }
+        for (int c = 0; c < 5; c++) {
+          bsum[c] = bsum[c] + l[c];
+          bsum[5 + c] = bsum[5 + c] + r[c];
+        }
+      }
+      for (int c = 0; c < 10; c++) {
+        fncoef[(size_t)c * FN + fn] = bsum[c];
+        eo[c * NGL + n] = bsum[c];
+      }
+    }
+  }
 }
 
 // ========================================================= btp_bcl_coeffs_qdf: faces
@@ -486,30 +631,8 @@ __global__ void __launch_bounds__(64)
   __syncthreads();
   if (tid < NQ) {
     const int iq = tid;
-    double quu = 0, quv = 0, qvv = 0, hb = 0, pl = 0, pr = 0;
-#pragma unroll
-    for (int k = 0; k < MAXL; k++) {
-      if (k >= L) break;
-      double ql[3] = {0, 0, 0}, qr[3] = {0, 0, 0};
-#pragma unroll
-      for (int n = 0; n < NGL; n++) {
-        double hi = s_psiq[n * NQ + iq];
-        for (int v = 0; v < 3; v++) {
-          ql[v] = ql[v] + hi * SQF(v, 0, n, k);
-          qr[v] = qr[v] + hi * SQF(v, 1, n, k);
-        }
-      }
-      quu = quu + 0.5 * ((ql[1] * ql[1] * ql[0]) + (qr[1] * qr[1] * qr[0]));
-      quv = quv + 0.5 * ((ql[2] * ql[1] * ql[0]) + (qr[2] * qr[1] * qr[0]));
-      qvv = qvv + 0.5 * ((ql[2] * ql[2] * ql[0]) + (qr[2] * qr[2] * qr[0]));
-      double pl1 = pl + ql[0];
-      double left_dp = 0.5 * m.alpha[k] * (pl1 * pl1 - pl * pl);
-      double pr1 = pr + qr[0];
-      double right_dp = 0.5 * m.alpha[k] * (pr1 * pr1 - pr * pr);
-      hb = hb + 0.5 * (left_dp + right_dp);
-      pl = pl1;
-      pr = pr1;
-    }
+    double quu, quv, qvv, hb;
+    bcl_face_quad<NGL, NQ>(m, s_qf, s_psiq, iq, quu, quv, qvv, hb);
     const size_t fq = (size_t)f * NQ + iq;
     fcoef[FC_QUU * FQ + fq] = quu;
     fcoef[FC_QUV * FQ + fq] = quv;
@@ -536,15 +659,7 @@ __global__ void __launch_bounds__(64)
       if (er > 0) {
         for (int c = 0; c < 5; c++) r[c] = s_lr[k][1][c][n];
       } else {
-        for (int c = 0; c < 5; c++) r[c] = l[c];
-        if (er == -4) {
-          double un = l[0] * nx + l[1] * ny;
-          r[0] = l[0] - 2.0 * un * nx;
-          r[1] = l[1] - 2.0 * un * ny;
-          un = l[2] * nx + l[3] * ny;
-          r[2] = l[2] - 2.0 * un * nx;
-          r[3] = l[3] - 2.0 * un * ny;
-        }
+        bcl_face_ghost(l, r, er, nx, ny);
       }
       for (int c = 0; c < 5; c++) {
         gdpp_face[((size_t)k * 10 + c) * FN + fn] = l[c];
@@ -2022,7 +2137,9 @@ __global__ void __launch_bounds__(256, 3)
 #define HNUMO_INSTANTIATE_BCL(NGL, NQ)                                                                              \
   template __global__ void extract_face_kernel<NGL>(DevMesh, const double *, double *, int);                      \
   template __global__ void bcl_coeffs_elem_kernel<NGL, NQ>(DevMesh, double *, const double *, double *, double *,    \
-                                                           double *, double *, double *);                          \
+                                                           double *, double *, double *, const double *,           \
+                                                           const double *, double *, double *, double *, double *, \
+                                                           double *);                                              \
   template __global__ void bcl_coeffs_face_kernel<NGL, NQ>(DevMesh, double *, const double *, const double *,        \
                                                            const double *, double *, double *, double *, double *);
 
