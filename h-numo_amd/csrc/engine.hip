@@ -1225,8 +1225,9 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   eng->slmf = dalloc<double>(eng, 2 * npq); eng->slmf_face = dalloc<double>(eng, 2 * FQ);
   eng->dpp = dalloc<double>(eng, npoin * L);
   eng->fmass = dalloc<double>(eng, FQ * L); eng->fcons = dalloc<double>(eng, FQ * L);
-  eng->momL = dalloc<double>(eng, 2 * FQ * L); eng->momR = dalloc<double>(eng, 2 * FQ * L);
-  eng->lapf = dalloc<double>(eng, 2 * FN * L);
+  eng->momL = dalloc<double>(eng, 4 * (size_t)E * 2 * nq * L);  // [slot][L][2][NQ] (MSLOT)
+  eng->momR = nullptr;
+  eng->lapf = dalloc<double>(eng, 4 * (size_t)E * 2 * ngl * L);  // [slot][L][2][NGL]
   if (par->method_visc == 1) {  // quad-point LDG (kernels_lapq.hip)
     eng->lapq_on = true;
     eng->dpq = dalloc<double>(eng, npq * L);

@@ -107,6 +107,11 @@ __host__ __device__ constexpr int eco_stride(int Q, int P) { return (4 * Q + 5 *
 #define NACC_I(k, e, p) ((((size_t)(e)) * NA_N + (k)) * P + (p))
 #define FACC_I(k, slot, iq) ((((size_t)(slot)) * FA_N + (k)) * NQ + (iq))
 #define GFACC_I(c, slot, n) ((((size_t)(slot)) * 8 + (c)) * NGL + (n))
+// layer momentum face terms / LDG face fluxes per element-side slot: [slot][L][2][N] (N = NQ or
+// NGL; needs L in scope)
+#define MSLOT(slot, k, o, i, N) (((((size_t)(slot)) * L + (k)) * 2 + (o)) * (N) + (i))
+// the efstat block of one element side (StageCfg::FBLK)
+#define EFBLK(NGL, NQ) (EF_N * (NQ) + EFN_N * (NGL))
 
 struct DevMesh {
   int nelem, npoin, npoin_q, nface, ngl, nq, L;

@@ -453,6 +453,26 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   __syncthreads();
   // GSPLIT: quad-point tasks on threads [0, Q), the nodal gradient tasks on the threads past them
   constexpr bool GSPLIT = BS - Q >= 128;
+  constexpr int EFC = 4 * NQ + 10 * NGL;
+  const size_t FQ = (size_t)F * NQ, FN = (size_t)F * NGL;
+  // (qf) the faces' quad-point coefficients (bcl_coeffs_face_kernel's arithmetic), task t < 4*NQ
+  auto face_quad = [&](int t) {
+    const int lf = t / NQ, iq = t % NQ;
+    double quu, quv, qvv, hb;
+    bcl_face_quad<NGL, NQ>(m, s_qfF[lf], s_psiq, iq, quu, quv, qvv, hb);
+    const double vals[4] = {quu, quv, qvv, hb};
+    for (int c = 0; c < 4; c++) efcoef[(size_t)(e * 4 + lf) * EFC + c * NQ + iq] = vals[c];
+    if (s_side[lf] == 0) {
+      const size_t fq = (size_t)s_face[lf] * NQ + iq;
+      for (int c = 0; c < 4; c++) fcoef[(FC_QUU + c) * FQ + fq] = vals[c];
+    }
+  };
+  // FQ1: room beside the quad-point tasks -- the face quad tasks on the last wave in this phase
+  // (they need only the staged face blocks), the gradient tasks on the lanes between and after
+  constexpr int FQL = BS - 64;
+  constexpr bool FQ1 = GSPLIT && Q <= FQL && 4 * NQ <= 64 && Q + 4 * NQ + 64 <= BS;
+  const bool fq1 = FQ1 && qf;
+  if (fq1 && tid >= FQL && tid < FQL + 4 * NQ) face_quad(tid - FQL);
   for (int q = tid; q < Q; q += BS) {
     const int iq = q % NQ, jq = q / NQ;
     double quu = 0.0, quv = 0.0, qvv = 0.0, hb = 0.0, pk = 0.0;
@@ -486,7 +506,9 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     ec[QC_HBCL * Q + q] = hb;
   }
   // compute_gradient_uv of (u'_k, v'_k), reference order, one thread per (layer, comp, node)
-  for (int t = GSPLIT ? tid - Q : tid; t >= 0 && t < L * 4 * P; t += GSPLIT ? BS - Q : BS) {
+  const int g0 = !GSPLIT ? tid : (!fq1 ? tid - Q : (tid < FQL ? tid - Q : (tid >= FQL + 4 * NQ ? tid - Q - 4 * NQ : -1)));
+  const int gstride = !GSPLIT ? BS : (fq1 ? BS - Q - 4 * NQ : BS - Q);
+  for (int t = g0; t >= 0 && t < L * 4 * P; t += gstride) {
     const int k = t / (4 * P), c = (t / P) % 4, p = t % P, i = p % NGL, j = p / NGL;
     const double *u = s_q[k][1 + (c >> 1)];
     const double ex = s_nm[(c & 1) ? 1 : 0][p], nx = s_nm[(c & 1) ? 3 : 2][p];
@@ -530,18 +552,8 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     for (int c = 0; c < 4; c++) ec[(NC_D1 + c) * P + p] = sum[c];
   }
   if (!qf) return;
-  constexpr int EFC = 4 * NQ + 10 * NGL;
-  const size_t FQ = (size_t)F * NQ, FN = (size_t)F * NGL;
-  if (tid >= 64 && tid < 64 + 4 * NQ) {  // face quad points (bcl_coeffs_face_kernel's arithmetic)
-    const int lf = (tid - 64) / NQ, iq = (tid - 64) % NQ;
-    double quu, quv, qvv, hb;
-    bcl_face_quad<NGL, NQ>(m, s_qfF[lf], s_psiq, iq, quu, quv, qvv, hb);
-    const double vals[4] = {quu, quv, qvv, hb};
-    for (int c = 0; c < 4; c++) efcoef[(size_t)(e * 4 + lf) * EFC + c * NQ + iq] = vals[c];
-    if (s_side[lf] == 0) {
-      const size_t fq = (size_t)s_face[lf] * NQ + iq;
-      for (int c = 0; c < 4; c++) fcoef[(FC_QUU + c) * FQ + fq] = vals[c];
-    }
+  if (!fq1 && tid >= 64 && tid < 64 + 4 * NQ) {  // face quad points (not in the phase above)
+    face_quad(tid - 64);
   } else if (tid >= 128 && tid < 128 + 4 * NGL) {  // face nodes: this element's side
     const int lf = (tid - 128) / NGL, n = (tid - 128) % NGL, p = s_map[lf * NGL + n];
     const int s = s_side[lf], er = s_bc[lf];
@@ -1164,9 +1176,11 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
 // ========================================== layer momentum: face kernel
 // Apply_layers_fluxes (mod_create_rhs_mlswe.F90:458-820) and the layer LDG flux
 // bcl_create_rhs_laplacian_flux (mod_laplacian_quad.F90:521-611).  Outputs per face
-// face quad point: momL/momR[k][2][F*NQ] = (nx*H_face + flux_x, ny*H_face + flux_y) of the
-// left / right side (the element kernels apply -/+ (wq*hi)*value in reference order), and
-// per face node lap[k][2][F*NGL] = wq*psi(n,n)*flux (LDG; + for left, - for right).
+// face quad point: (nx*H_face + flux_x, ny*H_face + flux_y) of the left / right side into the
+// element-side slot (fslotL / fslotR) of that side, momL[slot][L][2][NQ] (MSLOT; the element
+// kernel applies -/+ (wq*hi)*value in reference order and loads its four slots without first
+// reading its face ids), and per face node wq*psi(n,n)*flux (LDG; + for left, - for right) into
+// both sides' slots, lap[slot][L][2][NGL].  (momR is unused.)
 template <int NGL, int NQ>
 __global__ void __launch_bounds__(64)
     mom_flux_face_kernel(DevMesh m, const double *qf, const double *facc, const double *gdpp_face,
@@ -1176,7 +1190,7 @@ __global__ void __launch_bounds__(64)
   const int f = blockIdx.x, tid = threadIdx.x, F = m.nface, L = m.L;
   const size_t FQ = (size_t)F * NQ, FN = (size_t)F * NGL;
   BCL_MARK(3, 0) BCL_WALL(3, 6)
-  const int slot = m.fslotA[f];
+  const int slot = m.fslotA[f], slotL = m.fslotL[f], slotR = m.fslotR[f];
   // every input of the face in one round of independent loads (the face's qf block per layer,
   // its 16 averages, the LDG face averages and coefficients, the face statics), then the
   // arithmetic from LDS: one memory round trip instead of one per dependent step
@@ -1416,10 +1430,12 @@ __global__ void __launch_bounds__(64)
       double hlx = nxl * Hf[0][k], hrx = nxl * Hf[1][k], hly = nyl * Hf[0][k], hry = nyl * Hf[1][k];
       double flux_x = nxl * udpf[0][k] + nyl * udpf[1][k];
       double flux_y = nxl * vdpf[0][k] + nyl * vdpf[1][k];
-      momL[((size_t)k * 2 + 0) * FQ + fq] = hlx + flux_x;
-      momL[((size_t)k * 2 + 1) * FQ + fq] = hly + flux_y;
-      momR[((size_t)k * 2 + 0) * FQ + fq] = hrx + flux_x;
-      momR[((size_t)k * 2 + 1) * FQ + fq] = hry + flux_y;
+      momL[MSLOT(slotL, k, 0, iq, NQ)] = hlx + flux_x;
+      momL[MSLOT(slotL, k, 1, iq, NQ)] = hly + flux_y;
+      if (slotR >= 0) {
+        momL[MSLOT(slotR, k, 0, iq, NQ)] = hrx + flux_x;
+        momL[MSLOT(slotR, k, 1, iq, NQ)] = hry + flux_y;
+      }
     }
     BCL_MARK(3, 2)
   } else if (tid >= 32 && tid < 32 + NGL) {
@@ -1441,8 +1457,13 @@ __global__ void __launch_bounds__(64)
       double flux_qu = (qum0 - fl[0] * nx) + (qum1 - fl[1] * ny);
       double flux_qv = (qvm0 - fl[2] * nx) + (qvm1 - fl[3] * ny);
       double h1 = s_psi[n * NGL + n];
-      lap[((size_t)k * 2 + 0) * FN + fn] = wq * h1 * flux_qu;
-      lap[((size_t)k * 2 + 1) * FN + fn] = wq * h1 * flux_qv;
+      const double l0 = wq * h1 * flux_qu, l1 = wq * h1 * flux_qv;
+      lap[MSLOT(slotL, k, 0, n, NGL)] = l0;
+      lap[MSLOT(slotL, k, 1, n, NGL)] = l1;
+      if (slotR >= 0) {
+        lap[MSLOT(slotR, k, 0, n, NGL)] = l0;
+        lap[MSLOT(slotR, k, 1, n, NGL)] = l1;
+      }
     }
   }
   BCL_MARK(3, 5) BCL_WALL(3, 7)
@@ -1523,16 +1544,16 @@ __global__ void __launch_bounds__(256, 3)
   for (int t = tid; t < 4 * NGL; t += BS) s_map[t] = m.efmap[e * 4 * NGL + t];
   // the element's face data (Apply_layers_fluxes' lifts, the LDG face fluxes), staged with the
   // other loads: momL or momR by the element's side of each face
-  stage_face_quads<NQ>(s_fw, m.fstat + FS_W * (size_t)F * NQ, 0, 1, m.efaces + e * 4, tid, BS);
+  // (element-major sources only: no load here waits for another)
+  for (int t = tid; t < 4 * NQ; t += BS)
+    s_fw[t] = m.efstat[((size_t)e * 4 + t / NQ) * EFBLK(NGL, NQ) + EF_W * NQ + t % NQ];
   for (int t = tid; t < L * 2 * 4 * NQ; t += BS) {
     const int ko = t / (4 * NQ), lf = (t / NQ) % 4, iq = t % NQ;
-    const int f = m.efaces[e * 4 + lf];
-    const double *src = m.eside[e * 4 + lf] == 0 ? momL : momR;
-    (&s_fm[0][0][0])[t] = src[(size_t)ko * F * NQ + (size_t)f * NQ + iq];
+    (&s_fm[0][0][0])[t] = momL[MSLOT(e * 4 + lf, ko >> 1, ko & 1, iq, NQ)];
   }
   for (int t = tid; t < L * 2 * 4 * NGL; t += BS) {
     const int ko = t / (4 * NGL), lf = (t / NGL) % 4, n = t % NGL;
-    (&s_fl[0][0][0])[t] = lapf[(size_t)ko * F * NGL + (size_t)m.efaces[e * 4 + lf] * NGL + n];
+    (&s_fl[0][0][0])[t] = lapf[MSLOT(e * 4 + lf, ko >> 1, ko & 1, n, NGL)];
   }
   for (int t = tid; t < L * 3 * P; t += BS) {
     int k = t / (3 * P), r = t % (3 * P);
