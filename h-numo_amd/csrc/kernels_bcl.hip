@@ -467,12 +467,6 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
       for (int c = 0; c < 4; c++) fcoef[(FC_QUU + c) * FQ + fq] = vals[c];
     }
   };
-  // FQ1: room beside the quad-point tasks -- the face quad tasks on the last wave in this phase
-  // (they need only the staged face blocks), the gradient tasks on the lanes between and after
-  constexpr int FQL = BS - 64;
-  constexpr bool FQ1 = GSPLIT && Q <= FQL && 4 * NQ <= 64 && Q + 4 * NQ + 64 <= BS;
-  const bool fq1 = FQ1 && qf;
-  if (fq1 && tid >= FQL && tid < FQL + 4 * NQ) face_quad(tid - FQL);
   for (int q = tid; q < Q; q += BS) {
     const int iq = q % NQ, jq = q / NQ;
     double quu = 0.0, quv = 0.0, qvv = 0.0, hb = 0.0, pk = 0.0;
@@ -506,9 +500,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     ec[QC_HBCL * Q + q] = hb;
   }
   // compute_gradient_uv of (u'_k, v'_k), reference order, one thread per (layer, comp, node)
-  const int g0 = !GSPLIT ? tid : (!fq1 ? tid - Q : (tid < FQL ? tid - Q : (tid >= FQL + 4 * NQ ? tid - Q - 4 * NQ : -1)));
-  const int gstride = !GSPLIT ? BS : (fq1 ? BS - Q - 4 * NQ : BS - Q);
-  for (int t = g0; t >= 0 && t < L * 4 * P; t += gstride) {
+  for (int t = GSPLIT ? tid - Q : tid; t >= 0 && t < L * 4 * P; t += GSPLIT ? BS - Q : BS) {
     const int k = t / (4 * P), c = (t / P) % 4, p = t % P, i = p % NGL, j = p / NGL;
     const double *u = s_q[k][1 + (c >> 1)];
     const double ex = s_nm[(c & 1) ? 1 : 0][p], nx = s_nm[(c & 1) ? 3 : 2][p];
@@ -552,7 +544,9 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     for (int c = 0; c < 4; c++) ec[(NC_D1 + c) * P + p] = sum[c];
   }
   if (!qf) return;
-  if (!fq1 && tid >= 64 && tid < 64 + 4 * NQ) {  // face quad points (not in the phase above)
+  // (the face quad tasks here, not beside the quad-point tasks: there they took lanes from the
+  // gradient tasks, 2 -> 3 rounds, 14.8 -> 16.2 us per launch at dg25L3)
+  if (tid >= 64 && tid < 64 + 4 * NQ) {  // face quad points
     face_quad(tid - 64);
   } else if (tid >= 128 && tid < 128 + 4 * NGL) {  // face nodes: this element's side
     const int lf = (tid - 128) / NGL, n = (tid - 128) % NGL, p = s_map[lf * NGL + n];
