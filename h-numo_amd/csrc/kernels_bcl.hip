@@ -1516,6 +1516,10 @@ __global__ void __launch_bounds__(256, 3)
   __shared__ double s_fm[MAXL][2][4 * NQ]; // momentum face terms of this element's side, per face
   __shared__ double s_fl[MAXL][2][4 * NGL];// layer LDG face fluxes at the face nodes
   __shared__ int s_map[4 * NGL], s_face[4], s_side[4], s_bc[4];
+  // the nodal inputs of phase 4 (massinv, f2, A, B, qb(4), pbprime, the layer thicknesses of q
+  // and, mode 1, of the final qprime), fetched with the other loads instead of in that phase
+  enum { P4_MI = 0, P4_F2, P4_A, P4_B, P4_QB, P4_PB = P4_QB + 4, P4_H, P4_D = P4_H + MAXL, P4_N = P4_D + MAXL };
+  __shared__ double s_p4[P4_N][P];
 
   // quad-point scalars for the layer-coupling task of quad point tid, in flight during
   // the loads and the interpolation
@@ -1562,6 +1566,25 @@ __global__ void __launch_bounds__(256, 3)
   for (int t = tid; t < 5 * P; t += BS) {
     const int c = t / P;
     s_nm[c][t % P] = m.nstat[(c < 4 ? NS_EX + c : NS_W) * (size_t)npoin + (size_t)e * P + t % P];
+  }
+  for (int t = tid; t < P4_N * P; t += BS) {
+    const int c = t / P, p = t - c * P;
+    const size_t I = (size_t)e * P + p;
+    double v = 0.0;
+    if (c < P4_QB) {
+      const int ns[4] = {NS_MINV, NS_F2, NS_A, NS_B};
+      v = m.nstat[ns[c] * (size_t)npoin + I];
+    } else if (c < P4_PB) {
+      v = qb[I * 4 + (c - P4_QB)];
+    } else if (c == P4_PB) {
+      v = m.nstat[NS_PB * (size_t)npoin + I];
+    } else if (c < P4_D) {
+      if (c - P4_H < L) v = q[((size_t)(c - P4_H) * npoin + I) * 3];
+    } else if (mode == 1 && c - P4_D < L) {
+      const int k = c - P4_D;
+      v = qp_avg0 ? qp_in[((size_t)k * npoin + I) * 3] : dpp2[(size_t)k * npoin + I];
+    }
+    s_p4[c][p] = v;
   }
   __syncthreads();
   if (*m.runflag & RUN_ABORT) return;  // (a persistent sub-cycle of this run did no work: DevMesh)
@@ -1877,7 +1900,7 @@ __global__ void __launch_bounds__(256, 3)
   const bool shear = m.ad > 0.0, shear_zero = mode == 1 && m.shear_corr != 1;
   for (int p = tid; p < P; p += BS) {
     const size_t I = (size_t)e * P + p;
-    const double mi = m.nstat[NS_MINV * (size_t)npoin + I];
+    const double mi = s_p4[P4_MI][p];
 #pragma unroll
     for (int k = 0; k < MAXL; k++) {
       if (k >= L) break;
@@ -2040,9 +2063,8 @@ __global__ void __launch_bounds__(256, 3)
   //      evaluate_bcl / evaluate_bcl_v1 with extract_velocity (:198-320)
   for (int p = tid; p < P; p += BS) {
     const size_t I = (size_t)e * P + p;
-    const double f2 = m.nstat[NS_F2 * (size_t)npoin + I], ab = m.nstat[NS_A * (size_t)npoin + I],
-                 bb = m.nstat[NS_B * (size_t)npoin + I];
-    const double b1 = qb[I * 4], b3 = qb[I * 4 + 2], b4 = qb[I * 4 + 3];
+    const double f2 = s_p4[P4_F2][p], ab = s_p4[P4_A][p], bb = s_p4[P4_B][p];
+    const double b1 = s_p4[P4_QB][p], b3 = s_p4[P4_QB + 2][p], b4 = s_p4[P4_QB + 3][p];
     double nw[MAXL][3];
 #pragma unroll
     for (int k = 0; k < MAXL; k++) {
@@ -2051,7 +2073,7 @@ __global__ void __launch_bounds__(256, 3)
       const double tu = s_r[k][0][p] + f2 * q3, tv = s_r[k][1][p] - f2 * q2;
       nw[k][1] = ab * tu + bb * tv;
       nw[k][2] = -bb * tu + ab * tv;
-      nw[k][0] = q[((size_t)k * npoin + I) * 3];
+      nw[k][0] = s_p4[P4_H + k][p];
     }
     for (int lf = 0; lf < 4; lf++) {
       const int er = s_bc[lf];
@@ -2119,7 +2141,7 @@ __global__ void __launch_bounds__(256, 3)
 #pragma unroll
       for (int k = 0; k < MAXL; k++)
         if (k < L) ope = ope + h[k];
-      ope = ope / m.nstat[NS_PB * (size_t)npoin + I];
+      ope = ope / s_p4[P4_PB][p];
     }
     double ov[MAXL][3];
 #pragma unroll
@@ -2129,7 +2151,7 @@ __global__ void __launch_bounds__(256, 3)
       qq[1] = nw[k][1];
       qq[2] = nw[k][2];
       double *o = qp_out + ((size_t)k * npoin + I) * 3;
-      ov[k][0] = mode == 0 ? h[k] / ope : (qp_avg0 ? qp_in[((size_t)k * npoin + I) * 3] : dpp2[(size_t)k * npoin + I]);
+      ov[k][0] = mode == 0 ? h[k] / ope : s_p4[P4_D + k][p];
       ov[k][1] = uv[k][0] - b3 / b1;
       ov[k][2] = uv[k][1] - b4 / b1;
       o[0] = ov[k][0];
@@ -2142,7 +2164,7 @@ __global__ void __launch_bounds__(256, 3)
       extract_node_faces<NGL>(m, qf, s_face, s_side, s_bc, r0, r1, ov, 0);
     }
     if (mode == 1) {
-      const double b2 = qb[I * 4 + 1];
+      const double b2 = s_p4[P4_QB + 1][p];
       if (!(isfinite(b1) && isfinite(b2) && isfinite(b3) && isfinite(b4))) atomicOr(flag, 2);
     }
   }
