@@ -180,6 +180,18 @@ def face_partition(case: Case, nranks: int, rank: int, order: str = "block") -> 
                         elems=elems, faces=faces, flipped=np.flatnonzero(flip), fneighbours=fneighbours)
 
 
+def add_dense_tables(pc: FaceRankCase) -> FaceRankCase:
+    """The reference's dense per-quad-point tables (psih, dpsidx, ... Tensor_product.F90:50-126)
+    for this rank's elements only, built from its own element metrics.  Equal to slicing the
+    global tables (face_partition of a dense case): every column depends on its own element
+    alone, and the index tables are the same local base + node.  For meshes whose global dense
+    tables do not fit (C4: ~6 GB), the reference harness reads these per rank."""
+    from types import SimpleNamespace
+    from .case import _dense_tables
+    _dense_tables(pc.arrays, pc.basis, SimpleNamespace(nelem=int(pc.scalars["nelem"])))
+    return pc
+
+
 def halo_lists(pc: FaceRankCase):
     """mod_parallel's arrays for this rank: num_nbh, nbh_proc (1-based ranks), num_send_recv,
     nbh_send_recv (1-based local face ids), nbh_send_recv_multi (1: conforming)."""

@@ -19,9 +19,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(REPO, "h-numo_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
+sys.path.insert(0, os.path.dirname(HERE))
 import oracle as O  # noqa: E402
 from hnumo import bundle as B  # noqa: E402
 from hnumo.case import build_case, make_config  # noqa: E402
+from util import partition_inputs_sha256  # noqa: E402
 
 # (fixture name, config, mode, nsteps, node stride for the stored state)
 GOLDEN = [
@@ -35,6 +37,8 @@ GOLDEN = [
     ("dg8L3q_step1", "dg8L3q", "step", 1, 1),
     # C3 at N=7 (8x8 elements: the 25x25 bundle's dense tables are ~0.5 GB)
     ("dg8N7L3_step1", "dg25N7L3", "step", 1, 1, dict(nelx=8, nely=8)),
+    # C3 at its stated size (25x25, N=7), strided like dg25_step1
+    ("dg25N7L3_step1", "dg25N7L3", "step", 1, 7),
     # branches the shipped namelists do not exercise: quadratic drag + no-slip
     # walls, linear drag + beta plane + mixed walls, 3-layer lake, quad-point LDG + no-slip
     ("bump10_b2ns_step1", "bump10", "step", 1, 1,
@@ -59,6 +63,11 @@ FIELDS_KEPT = ["ope_ave", "H_ave", "Qu_ave", "btp_mass_flux_ave", "uvb_face_ave"
                "graduvb_ave", "Q_uu_dp", "H_bcl_edge", "btp_graduv_dpp_face"]
 
 
+def state_sha256(a) -> str:
+    """sha256 of a state array's float64 values in C order (the tests hash the engine's the same way)."""
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=np.float64).tobytes()).hexdigest()
+
+
 def bundle_hash(case, mode, nsteps):
     with tempfile.TemporaryDirectory() as d:
         p = os.path.join(d, "b.bin")
@@ -79,24 +88,58 @@ GOLDEN_MPI = [
     ("dg8L3q_mpi4m_step2", "dg8L3q", {}, 4, "morton", 2),
     # C5 (lake at rest) on 4 ranks
     ("lake10_mpi4m_step2", "lake10", {}, 4, "morton", 2),
+    # the BASELINE configs at their stated sizes (VERDICT r03 "next" 1), each rank's state stored
+    # at a node stride (the dense tables are built per rank: add_dense_tables):
+    # C5: lake at rest 200x200 on 4 Morton ranks (dt scaled with the element size, test_lake_gpu.py)
+    ("lake200_mpi4m_step1", "lake10", dict(nelx=200, nely=200, dt=5.0, dt_btp=0.09), 4, "morton", 1, 61),
+    # C4: double gyre 316x316 on the 4x2 block partition of the 8-GPU metric
+    ("dg316L3_mpi8b_step1", "dg316L3", {}, 8, "block", 1, 97),
 ]
 
 
 def make_mpi(only=None):
-    from hnumo.facepart import face_partition
-    for name, cfg, ov, R, order, nsteps in GOLDEN_MPI:
+    from hnumo.facepart import add_dense_tables, face_partition
+    for entry in GOLDEN_MPI:
+        name, cfg, ov, R, order, nsteps = entry[:6]
+        stride = entry[6] if len(entry) > 6 else 1
         if only and name not in only:
             continue
-        case = build_case(make_config(cfg, **ov))
-        parts = [face_partition(case, R, r, order) for r in range(R)]
+        if stride == 1:
+            case = build_case(make_config(cfg, **ov))
+            parts = [face_partition(case, R, r, order) for r in range(R)]
+        else:
+            case = build_case(make_config(cfg, **ov), dense=False)
+            parts = [add_dense_tables(face_partition(case, R, r, order)) for r in range(R)]
+            del case
         outs = O.run_reference_mpi(parts, "step", nsteps)
         keep = {"config": np.array(cfg), "overrides": np.array(json.dumps(ov)), "nranks": np.array(R),
-                "order": np.array(order), "nsteps": np.array(nsteps), "mode": np.array("step")}
+                "order": np.array(order), "nsteps": np.array(nsteps), "mode": np.array("step"),
+                "stride": np.array(stride)}
         for r, (pc, o) in enumerate(zip(parts, outs)):
             keep[f"bundle_sha256_r{r}"] = np.array(bundle_hash(pc, "step", nsteps))
+            keep[f"nelem_r{r}"] = np.array(pc.scalars["nelem"])
+            keep[f"inputs_sha256_r{r}"] = np.array(partition_inputs_sha256(pc))
             for k in ("q_df", "qb_df", "qprime_df"):
-                keep[f"{k}_r{r}"] = o[k]
+                keep[f"{k}_r{r}"] = o[k][:, ::stride, ...]
+                # the whole array, bit for bit, in 32 bytes (state_sha256)
+                keep[f"{k}_sha256_r{r}"] = np.array(state_sha256(o[k]))
         path = os.path.join(HERE, name + ".npz")
+        np.savez_compressed(path, **keep)
+        print(name, os.path.getsize(path))
+
+
+def add_mpi_inputs_hash(only):
+    """Adds inputs_sha256_r* to existing strided multi-rank fixtures (no reference run)."""
+    from hnumo.facepart import face_partition
+    for entry in GOLDEN_MPI:
+        name, cfg, ov, R, order = entry[:5]
+        if name not in only:
+            continue
+        path = os.path.join(HERE, name + ".npz")
+        keep = dict(np.load(path, allow_pickle=False))
+        case = build_case(make_config(cfg, **ov), dense=False)
+        for r in range(R):
+            keep[f"inputs_sha256_r{r}"] = np.array(partition_inputs_sha256(face_partition(case, R, r, order)))
         np.savez_compressed(path, **keep)
         print(name, os.path.getsize(path))
 
@@ -175,6 +218,10 @@ def main(only=None):
         if mode in ("step", "predict"):
             keep["q_df"] = out["q_df"][:, ::stride, :]
             keep["qprime_df"] = out["qprime_df"][:, ::stride, :]
+        if stride > 1:
+            for k in ("q_df", "qb_df", "qprime_df"):
+                if k in keep:
+                    keep[k + "_sha256"] = np.array(state_sha256(out[k]))
         for f in FIELDS_KEPT:
             a = out[f]
             keep["field_" + f] = a.reshape(-1, order="F")[::stride]
@@ -189,6 +236,8 @@ if __name__ == "__main__":
     args = sys.argv[1:]
     if args and args[0] == "mpi":
         make_mpi(args[1:] or None)
+    elif args and args[0] == "mpi_inputs":
+        add_mpi_inputs_hash(args[1:])
     elif args and args[0] == "setup":
         make_setup(args[1:] or None)
     elif args and args[0] == "geom":

@@ -14,7 +14,7 @@ import os
 import numpy as np
 import pytest
 
-from util import layer_mass, rel
+from util import layer_mass, rel, state_sha256
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-10
@@ -159,7 +159,9 @@ def test_shear_stress_reference_corrector_is_nonfinite(case_factory):
 
 GOLDEN_STEPS = ["bump10_step2", "lake10_step1", "dg25_step1", "dg25L3_step1", "bump10q_step1", "dg8L3q_step1",
                 "dg8N7L3_step1", "bump10_b2ns_step1", "bump10_mixed_step1", "lake10L3_step1", "bump10q_ns_step1",
-                "dg8L3q_mixed_step1", "qmbump8_step2", "qmdg8L3_step1", "bump16_step1"]
+                "dg8L3q_mixed_step1", "qmbump8_step2", "qmdg8L3_step1", "bump16_step1",
+                # C3 at its stated size (25x25, N=7): strided sample + sha256 of the whole state
+                "dg25N7L3_step1"]
 
 
 @pytest.mark.parametrize("name", GOLDEN_STEPS)
@@ -181,6 +183,9 @@ def test_engine_matches_reference_golden(name, case_factory, engines):
     # the engine reproduces the reference arithmetic: the state is bit-identical
     assert np.array_equal(q[:, ::s, :], g["q_df"]) and np.array_equal(qb[:, ::s], g["qb_df"])
     assert np.array_equal(qp[:, ::s, :], g["qprime_df"])
+    for k, a in (("q_df", q), ("qb_df", qb), ("qprime_df", qp)):
+        if k + "_sha256" in g:        # strided fixtures: the whole state, bit for bit
+            assert state_sha256(a) == str(g[k + "_sha256"]), k
 
 
 @pytest.mark.parametrize("name", ["bump10s_predict", "dg8L3s_predict"])

@@ -112,6 +112,24 @@ def _mpi_parts(g):
     return case, [face_partition(case, R, r, str(g["order"])) for r in range(R)]
 
 
+# the BASELINE configs at their stated sizes (C5 lake 200x200 on 4 ranks, C4 316x316 on 8): the
+# reference bundles (dense tables included) are GBs, so the fixtures carry a hash of every rank's
+# non-dense inputs and halo lists instead (tests/util.py partition_inputs_sha256)
+MPI_FIXTURES_FULLSIZE = ["lake200_mpi4m_step1", "dg316L3_mpi8b_step1"]
+
+
+@pytest.mark.parametrize("name", MPI_FIXTURES_FULLSIZE)
+def test_fullsize_mpi_fixture_inputs_current(name):
+    from util import overrides_of, partition_inputs_sha256
+    g = dict(np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False))
+    case = build_case(make_config(str(g["config"]), **overrides_of(g)), dense=False)
+    R = int(g["nranks"])
+    for r in range(R):
+        pc = face_partition(case, R, r, str(g["order"]))
+        assert pc.scalars["nelem"] == int(g[f"nelem_r{r}"])
+        assert partition_inputs_sha256(pc) == str(g[f"inputs_sha256_r{r}"]), (name, r)
+
+
 @pytest.mark.parametrize("name", MPI_FIXTURES)
 def test_mpi_fixture_inputs_current(name):
     import tempfile, hashlib

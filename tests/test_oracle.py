@@ -13,7 +13,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = os.path.join(HERE, "golden")
 GOLDEN = ["bump10_rhs", "bump10_btp", "bump10_step2", "lake10_step1", "dg25_step1", "dg25L3_step1",
           "bump10q_step1", "dg8L3q_step1", "dg8N7L3_step1", "bump10_b2ns_step1", "bump10_mixed_step1",
-          "lake10L3_step1", "bump10q_ns_step1", "dg8L3q_mixed_step1", "qmbump8_step2", "qmdg8L3_step1", "bump16_step1"]
+          "lake10L3_step1", "bump10q_ns_step1", "dg8L3q_mixed_step1", "qmbump8_step2", "qmdg8L3_step1", "bump16_step1",
+          "dg25N7L3_step1"]
 
 
 def load(name):
@@ -67,6 +68,10 @@ def test_oracle_matches_golden(name, case_factory):
         assert np.array_equal(q[:, ::stride, :], g["q_df"])
         assert np.array_equal(qp[:, ::stride, :], g["qprime_df"])
     assert np.array_equal(qb[:, ::stride], g["qb_df"])
+    from util import state_sha256
+    for k, a in (("q_df", q), ("qb_df", qb), ("qprime_df", qp)):
+        if k + "_sha256" in g:        # strided fixtures: the whole state, bit for bit
+            assert state_sha256(a) == str(g[k + "_sha256"]), k
     for k in g:
         if k.startswith("field_"):
             a = o.field(k[6:]).reshape(-1, order="F")[::stride]
