@@ -24,8 +24,8 @@ p4est.c:1686-1712): the reference's halo contract, with the stage traces exchang
 point-to-point (xGMI) on a second stream while the interior elements run (csrc/engine.hip
 `trace_exchange`, the overlap of mod_rhs_btp.F90:40-46).  --halo ghost uses the one-element
 ghost layer of hnumo/partition.py instead.  value = element-updates of all ranks / max time
-over ranks.  If the RCCL halo cannot be set up (or fails) on any rank, the ranks fall back to
-independent replicas of the per-GPU block and say so in config.parallelism.
+over ranks.  If the RCCL halo cannot be set up (or fails) on any rank, the run fails (exit
+status 1, an {"error": ...} line on stderr): it never substitutes another kind of number.
 """
 from __future__ import annotations
 
@@ -74,10 +74,11 @@ def _run_reference(parts_or_case, steps: int, nranks: int):
         return max(t) if t else None
 
 
-def cpu_baseline(case, steps: int, cores: int):
+def cpu_baseline(case, steps: int, cores: int, repeats: int = 3):
     """The reference Fortran timed on this host: `cores` MPI ranks (one per core) on a Morton
     processor-face partition of the same workload -- the reference's own multi-rank path --
-    and, beside it, one rank on one core.  Falls back to the C restatement (oracle, 1 core)."""
+    `repeats` times (value = the median; the host cores are shared, so min / max are reported
+    beside it), and one rank on one core.  Falls back to the C restatement (oracle, 1 core)."""
     from hnumo.facepart import face_partition
     from hnumo.roofline import element_updates_per_step
     eu = element_updates_per_step(case)
@@ -90,12 +91,16 @@ def cpu_baseline(case, steps: int, cores: int):
         many = None
         if cores > 1:
             parts = [face_partition(case, cores, r, "morton") for r in range(cores)]
-            many = _run_reference(parts, many_steps, cores)
+            runs = [t for t in (_run_reference(parts, many_steps, cores) for _ in range(repeats)) if t]
+            if runs:
+                many = sorted(runs)[len(runs) // 2]
         if many:
+            rates = sorted(eu * many_steps / t for t in runs)
             out = {"value": eu * many_steps / many, "unit": "element-updates/s", "cores": cores, "kind": "reference",
                    "sample": sample + f", {many_steps} baroclinic steps of the reference Fortran (amdflang -O2) under "
                                       f"mpiexec -n {cores} (Morton processor-face partition, its own MPI halo), "
-                                      f"one rank per core: {many:.2f} s"}
+                                      f"one rank per core: {many:.2f} s (median of {len(runs)} runs)",
+                   "spread": {"runs": len(runs), "min": round(rates[0], 1), "max": round(rates[-1], 1)}}
         if one:
             single = {"value": eu * steps / one, "cores": 1,
                       "sample": sample + f", {steps} baroclinic steps, 1 rank on core 0: {one:.2f} s"}
@@ -139,13 +144,49 @@ def single_gpu_line(cfg: str, workload: str, steps: int = 3):
     t = time.perf_counter() - t0
     k_ms = eng.time_stage_kernel(1)
     path = eng.stage_path
+    stats = eng.persistent_stats
     from hnumo.roofline import HBM_PEAK_GBS, stage_bytes
     eng.close()
     ach = stage_bytes(case) / (k_ms * 1e-3) / 1e9
-    return {"workload": f"{workload} on 1 GPU, {path} stage path",
-            "value": round(element_updates_per_step(case) * steps / t, 1), "unit": "element-updates/s",
-            "steps": steps, "ms_per_step": round(1e3 * t / steps, 3),
-            "stage_kernel_us": round(k_ms * 1e3, 2), "stage_kernel_frac": round(ach / HBM_PEAK_GBS, 4)}
+    out = {"workload": f"{workload} on 1 GPU, {path} stage path",
+           "value": round(element_updates_per_step(case) * steps / t, 1), "unit": "element-updates/s",
+           "steps": steps, "ms_per_step": round(1e3 * t / steps, 3),
+           "stage_kernel_us": round(k_ms * 1e3, 2), "stage_kernel_frac": round(ach / HBM_PEAK_GBS, 4),
+           "algorithmic_bytes_per_stage": int(stage_bytes(case)), "persistent_fallbacks": stats["aborts"]}
+    out.update(_profiled(cfg, "btp_subcycle_kernel" if path == "persistent" else "btp_stage_kernel", k_ms))
+    return out
+
+
+def _profiled(cfg: str, kname: str, k_ms: float) -> dict:
+    """roofline.traffic and the rocprofv3 duration of the stage kernel from the committed profile
+    summary (profiles/roofline_pmc.json, written by tools/profile_summary.py from a rocprofv3
+    --kernel-trace --stats run and the FETCH_SIZE / WRITE_SIZE passes of the same bench command;
+    the persistent kernel's stage-less trial launch excluded), and the DRAM rate those bytes
+    make over this run's measured kernel time.  Empty if no summary matches config and kernel."""
+    path = os.path.join(REPO, "profiles", "roofline_pmc.json")
+    try:
+        d = json.load(open(path)).get(cfg)
+    except Exception:
+        return {}
+    if not d or d.get("kernel") != kname or "hbm_bytes_per_stage" not in d:
+        return {}
+    from hnumo.roofline import HBM_PEAK_GBS
+    dram = d["hbm_bytes_per_stage"] / (k_ms * 1e-3) / 1e9
+    return {"traffic": d["hbm_bytes_per_stage"], "traffic_source": d["source"],
+            "rocprof_stage_us": d["stage_us"], "traffic_over_algorithmic": d["traffic_over_algorithmic"],
+            "dram_achieved": round(dram, 1), "dram_frac": round(dram / HBM_PEAK_GBS, 4)}
+
+
+def _limiter(frac: float, dram_frac: float | None, E: int) -> str:
+    """What the measurements say limits the stage kernel: the DRAM bytes it really moves (PMC)
+    against the algorithmic bytes' rate at the same kernel time."""
+    if dram_frac is None:
+        return "unmeasured (no PMC traffic summary for this config)"
+    if dram_frac >= 0.6:
+        return f"HBM: DRAM traffic at {dram_frac:.0%} of peak"
+    why = (f"{E} elements on 256 CUs ({E / 256.0:.1f} per CU), state and statics resident in LDS across the "
+           "stages" if E < 4096 else "VALU issue (SQ counters: profiles/roofline_pmc.json sq_per_element_stage)")
+    return f"not HBM: DRAM traffic at {dram_frac:.1%} of peak while the algorithmic bytes run at {frac:.1%}; {why}"
 
 
 def main():
@@ -216,18 +257,14 @@ def main():
         bad = torch.tensor([1 if err else 0], device="cuda")
         dist.all_reduce(bad, op=dist.ReduceOp.MAX)
         if bad.item():
+            # no substitute number (independent replicas would be another kind of measurement)
+            if rank == 0 or err:
+                print(json.dumps({"error": "multi-GPU halo setup failed", "rank": rank,
+                                  "detail": err or "on another rank"}), file=sys.stderr)
             if eng is not None:
                 eng.close()
-            eng = None
-            if weak:
-                case = build_case(base_cfg, dense=False)
-            else:  # replicas of one rank's block (same per-GPU work, no exchange)
-                bx, by = gcfg["nelx"] // px, gcfg["nely"] // py
-                x0, x1 = gcfg["xdims"]
-                y0, y1 = gcfg["ydims"]
-                case = build_case(make_config(cfg_name, nelx=bx, nely=by, xdims=(x0, x0 + (x1 - x0) / px),
-                                              ydims=(y0, y0 + (y1 - y0) / py)), dense=False)
-            parallelism = f"replicas{world} (RCCL halo unavailable: {err or 'on another rank'})"
+            dist.destroy_process_group()
+            sys.exit(1)
         else:
             bx, by = gcfg["nelx"] // px, gcfg["nely"] // py
             how = ("processor-face halo (reference contract) over RCCL p2p, traces on a 2nd stream overlapped with "
@@ -313,31 +350,18 @@ def main():
         achieved = sb / (k_ms * 1e-3) / 1e9
         step_ach = step_bytes(case) * steps / elapsed / 1e9
         E = case.scalars["nelem"]
-        limiter = ("latency: %d elements on 256 CUs (%.1f per CU), working set inside the 256 MiB Infinity "
-                   "Cache; profiles/ SQ counters: waves mostly waiting" % (E, E / 256.0)) if E < 4096 else \
-            "per-element latency x occupancy (3 workgroups/CU); HBM traffic below the algorithmic bytes"
-        # below ~4k elements (under 16 per CU) the stage is latency-bound, not HBM-bound: the PMC
-        # traffic is a fraction of the algorithmic bytes (the state stays in LDS / Infinity Cache)
-        roof = {"bound": "latency" if E < 4096 else "hbm", "bound_model": "hbm",
+        # the roofline the kernel is priced against is HBM (no MFMA work on this path); what the
+        # measurements say limits it is `limiter` (from the PMC traffic, below)
+        roof = {"bound": "hbm",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "limiter": limiter,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                 "kernel": kname, "kernel_avg_us": round(k_ms * 1e3, 3),
                 "algorithmic_bytes_per_launch": int(sb), "timing": k_src,
                 "step_achieved": round(step_ach, 1), "step_frac": round(step_ach / HBM_PEAK_GBS, 4),
                 "step_bytes": int(step_bytes(case)),
                 "step_model": "E*(2*N_btp*kstages*B_stage + B_bcl_step)/T_step per GPU (hnumo/roofline.py)"}
-        pmc = os.path.join(REPO, "profiles", "pmc_btp_stage.json")
-        if os.path.exists(pmc):
-            try:
-                d = json.load(open(pmc))
-                if d.get("config") == cfg_name and d.get("kernel", "btp_stage_kernel") == kname:
-                    roof["traffic"] = d["hbm_bytes_per_launch"]
-                    roof["traffic_source"] = pmc.replace(REPO + os.sep, "")
-                    # DRAM bytes actually moved (PMC, per stage) over the same kernel time
-                    roof["dram_achieved"] = round(d["hbm_bytes_per_launch"] / (k_ms * 1e-3) / 1e9, 1)
-                    roof["dram_frac"] = round(roof["dram_achieved"] / HBM_PEAK_GBS, 4)
-            except Exception:
-                pass
+        roof.update(_profiled(cfg_name, kname, k_ms) if world == 1 or weak else {})
+        roof["limiter"] = _limiter(roof["frac"], roof.get("dram_frac"), E)
     S = case.scalars
     if world > 1 and not weak:
         wl = (f"{cfg_name} (C4): double-gyre {base_cfg['nelx']}x{base_cfg['nely']} = "
@@ -360,6 +384,9 @@ def main():
     if halo_check is not None:
         out["halo_bitwise"] = halo_check["halo_bitwise"]
         out["halo_check"] = halo_check
+    # the persistent path's in-launch residency check: launches that gave up (and were redone on
+    # per-stage launches), trial re-probes, and re-probes that found the grid resident again
+    out["persistent"] = eng.persistent_stats
     eng.close()
     if rank == 0 and world == 1 and not args.no_c4 and args.config is None:
         for key, cfg, wl, n in [("c4_single_gpu", "dg316L3", "dg316L3 (C4: 316x316 elements, N=4, 3 layers)", 3),

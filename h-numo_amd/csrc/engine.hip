@@ -108,6 +108,12 @@ struct hnumo_engine {
   int persist_pad = 0;
   int persist_guard = 3;                      // bit 1: occupancy estimate, bit 2: trial launch
   int persist_aborts = 0;                     // runs that found a persistent launch not co-resident
+  // after an abort the persistent path is suspended, not dropped (maybe_reprobe): per-stage runs
+  // while persist_wait counts down, then a stage-less trial launch decides; the wait doubles with
+  // every abort or failed re-probe (up to 1024 runs) and resets after a completed persistent run
+  bool persist_suspended = false;
+  int persist_wait = 0, persist_backoff = 1, persist_reprobes = 0, persist_recovered = 0;
+  unsigned long long *dbg_abort_epoch = nullptr;  // hnumo_debug_force_abort: the launch epoch to abort
   StageArgs *d_stages[2] = {nullptr, nullptr};  // per-stage arguments: predictor (qp), corrector (qp2)
   // processor-face halo: the reference's own partition contract (face(8) = 0 faces listed per
   // neighbour rank in nbh_send_recv; p4est.c:1686-1712, mod_parallel).  NS shared-face slots in
@@ -197,7 +203,7 @@ struct Launch {
       hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, true>), dim3(n), dim3(StageCfg<NGL, NQ, true>::BS), 0, st, a);
   }
   static void subcycle(hnumo_engine *e, const StageArgs *stages, int ns) {
-    SubArgs sa{stages, ns, e->epoch, e->sub_done, e->sub_arrive, e->neg_flag};
+    SubArgs sa{stages, ns, e->epoch, e->sub_done, e->sub_arrive, e->neg_flag, e->dbg_abort_epoch};
     if (e->summation == HNUMO_SUM_REFERENCE)
       hipLaunchKernelGGL((btp_subcycle_kernel<NGL, NQ, false>), dim3(e->nelem_owned),
                          dim3(StageCfg<NGL, NQ, false>::BS), e->persist_pad, e->stream, sa);
@@ -229,7 +235,7 @@ struct Launch {
   }
   // the trial launch: the persistent grid with no stages, i.e. the residency rendezvous alone
   static void probe(hnumo_engine *e, int sum) {
-    SubArgs sa{e->d_stages[0], 0, e->epoch, e->sub_done, e->sub_arrive, e->neg_flag};
+    SubArgs sa{e->d_stages[0], 0, e->epoch, e->sub_done, e->sub_arrive, e->neg_flag, nullptr};
     if (sum == HNUMO_SUM_REFERENCE)
       hipLaunchKernelGGL((btp_subcycle_kernel<NGL, NQ, false>), dim3(e->nelem_owned),
                          dim3(StageCfg<NGL, NQ, false>::BS), e->persist_pad, e->stream, sa);
@@ -560,6 +566,7 @@ static const double *face_exchange_lapq(hnumo_engine *e, const double *flux, int
     hipLaunchKernelGGL(lapq_pack_kernel, dim3((unsigned)std::min<size_t>((tot + 255) / 256, 1024)), dim3(256), 0,
                        e->stream, e->bx_sbuf, flux, e->d_sface, e->m.fel, e->fqLR, e->NS, nb, e->nelem, nq, Q);
   face_tx(e, per);
+  if (e->group && e->group->aborted) return nullptr;  // (as face_exchange: no message arrived)
   return e->NS ? e->bx_rbuf : nullptr;
 }
 
@@ -710,7 +717,8 @@ static int stage_table(hnumo_engine *e, const double *qp, std::vector<StageArgs>
 // (method_visc == 1 needs its Laplacian kernels between the stages: per-stage launches)
 // (single rank only: its stage tables send every trace to an element slot)
 static bool use_persistent(const hnumo_engine *e) {
-  return e->comm_mode == 0 && e->nranks == 1 && !e->face_halo && !e->lapq_on && e->persistent_ok[e->summation];
+  return e->comm_mode == 0 && e->nranks == 1 && !e->face_halo && !e->lapq_on && e->persistent_ok[e->summation] &&
+         !e->persist_suspended;
 }
 
 // ti_barotropic_ssprk_mlswe (mod_rk_mlswe.F90:19-151) on device state qb_state
@@ -1393,6 +1401,8 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     eng->qsv = dalloc<double>(eng, (size_t)E * 8 * ngl * ngl);
     eng->sub_done = dalloc<unsigned>(eng, 1);
     eng->sub_arrive = dalloc<unsigned>(eng, 1);
+    eng->dbg_abort_epoch = dalloc<unsigned long long>(eng, 1);
+    if (eng->dbg_abort_epoch) HIPCHK(hipMemset(eng->dbg_abort_epoch, 0xff, sizeof(unsigned long long)));  // never
     for (int b = 0; b < 2; b++) eng->gtr[b] = dalloc<TraceGranule>(eng, (size_t)E * 32 * ngl);
     const double *qps[2] = {eng->qp, eng->qp2};
     for (int v = 0; v < 2; v++) {
@@ -1501,18 +1511,54 @@ static int flag_error(hnumo_engine *eng, int flags) {
   return 0;
 }
 
-// A persistent launch of the run was not co-resident (RUN_ABORT): it did no work, and neither
-// did anything after it that writes the step state, so the state is that of the last completed
-// step.  The engine drops the persistent path for good (the captured step holds it) and the
-// caller repeats what is left on per-stage launches.
-static void persistent_abort(hnumo_engine *eng) {
-  eng->persistent_ok[0] = eng->persistent_ok[1] = false;
-  eng->persist_aborts++;
+// the captured step holds the stage path and summation mode: capture again on the next step
+static void drop_graph(hnumo_engine *eng) {
   if (eng->graph_exec) (void)hipGraphExecDestroy(eng->graph_exec);
   if (eng->graph) (void)hipGraphDestroy(eng->graph);
   eng->graph_exec = nullptr;
   eng->graph = nullptr;
   if (eng->comm_mode != 1) eng->no_graph = false;
+}
+
+// A persistent launch of the run was not co-resident (RUN_ABORT): it did no work, and neither
+// did anything after it that writes the step state, so the state is that of the last completed
+// step.  The engine suspends the persistent path (maybe_reprobe brings it back once a trial launch
+// finds the grid resident again) and the caller repeats what is left on per-stage launches.
+static void persistent_abort(hnumo_engine *eng) {
+  eng->persist_suspended = true;
+  eng->persist_aborts++;
+  eng->persist_wait = eng->persist_backoff;
+  eng->persist_backoff = std::min(2 * eng->persist_backoff, 1024);
+  drop_graph(eng);
+}
+
+// Before a run: a suspended persistent path whose wait is over gets one stage-less trial launch
+// (Launch::probe, the residency rendezvous alone); all workgroups resident -> persistent again.
+// (A co-resident job that held CUs for a moment costs a few per-stage runs, not the engine's
+// lifetime on per-stage launches; one that stays costs a 20 ms probe every 1024 runs at most.)
+static int maybe_reprobe(hnumo_engine *eng) {
+  if (!eng->persist_suspended || !eng->persistent_ok[eng->summation]) return 0;
+  if (eng->persist_wait > 0) {
+    eng->persist_wait--;
+    return 0;
+  }
+  eng->persist_reprobes++;
+  HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
+  DISPATCH(eng, probe(eng, eng->summation));
+  HIPCHK(hipMemcpyAsync(eng->h_neg, eng->neg_flag, sizeof(int), hipMemcpyDeviceToHost, eng->stream));
+  HIPCHK(hipStreamSynchronize(eng->stream));
+  HIPCHK(hipGetLastError());
+  const bool resident = !(*eng->h_neg & RUN_ABORT);
+  HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
+  if (resident) {
+    eng->persist_suspended = false;
+    eng->persist_recovered++;
+    drop_graph(eng);
+  } else {
+    eng->persist_wait = eng->persist_backoff;
+    eng->persist_backoff = std::min(2 * eng->persist_backoff, 1024);
+  }
+  return 0;
 }
 
 static int transport_error(hnumo_engine *eng) {
@@ -1538,9 +1584,12 @@ static int launch_steps(hnumo_engine *eng, int nsteps) {
 }
 
 static int run_steps(hnumo_engine *eng, int nsteps) {
+  int rc = maybe_reprobe(eng);
+  if (rc) return rc;
+  const bool pers = use_persistent(eng);
   HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
   HIPCHK(hipMemsetAsync(eng->steps_done, 0, sizeof(unsigned), eng->stream));
-  int rc = launch_steps(eng, nsteps);
+  rc = launch_steps(eng, nsteps);
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(eng->h_neg, eng->neg_flag, sizeof(int), hipMemcpyDeviceToHost, eng->stream));
   HIPCHK(hipMemcpyAsync(eng->h_steps, eng->steps_done, sizeof(unsigned), hipMemcpyDeviceToHost, eng->stream));
@@ -1550,9 +1599,12 @@ static int run_steps(hnumo_engine *eng, int nsteps) {
   if ((*eng->h_neg & RUN_ABORT) && !use_persistent(eng)) return fail(eng, HNUMO_ERR_DEVICE, "run aborted off the persistent path");
   if (*eng->h_neg & RUN_ABORT) {
     const int done = (int)*eng->h_steps;
+    // an error of a step that completed before the abort is reported, not cleared by the retry
+    if ((rc = flag_error(eng, *eng->h_neg & ~RUN_ABORT))) return rc;
     persistent_abort(eng);
     return done < nsteps ? run_steps(eng, nsteps - done) : 0;
   }
+  if (pers) eng->persist_backoff = 1;  // a completed persistent run
   return flag_error(eng, *eng->h_neg);
 }
 
@@ -1593,12 +1645,7 @@ int hnumo_set_summation(hnumo_engine *eng, int mode) {
     return fail(eng, HNUMO_ERR_INVALID, "hnumo_set_summation: mode must be HNUMO_SUM_REFERENCE or HNUMO_SUM_FACTORED");
   if (mode != eng->summation) {
     eng->summation = mode;
-    // the captured step holds the other kernel: capture again on the next step
-    if (eng->graph_exec) (void)hipGraphExecDestroy(eng->graph_exec);
-    if (eng->graph) (void)hipGraphDestroy(eng->graph);
-    eng->graph_exec = nullptr;
-    eng->graph = nullptr;
-    if (eng->comm_mode != 1) eng->no_graph = false;
+    drop_graph(eng);  // (the captured step holds the other kernel)
   }
   return 0;
 }
@@ -1632,6 +1679,26 @@ int hnumo_persistent_info(hnumo_engine *eng, int32_t *out) {
   const int32_t v[8] = {use_persistent(eng) ? 1 : 0, eng->occ_blocks[0], eng->occ_blocks[1], eng->occ_ncu,
                         eng->probe_ok[0], eng->probe_ok[1], eng->persist_aborts, lds};
   std::memcpy(out, v, sizeof(v));
+  return 0;
+}
+
+int hnumo_persistent_stats(hnumo_engine *eng, int32_t *out4) {
+  if (!eng || !out4) return HNUMO_ERR_INVALID;
+  const int32_t v[4] = {eng->persist_aborts, eng->persist_reprobes, eng->persist_recovered,
+                        eng->persist_suspended ? eng->persist_wait : -1};
+  std::memcpy(out4, v, sizeof(v));
+  return 0;
+}
+
+int hnumo_debug_force_abort(hnumo_engine *eng, int k) {
+  if (!eng || k < 0) return HNUMO_ERR_INVALID;
+  if (!eng->dbg_abort_epoch) return fail(eng, HNUMO_ERR_INVALID, "engine has no persistent sub-cycle");
+  HIPCHK(hipSetDevice(eng->device));
+  HIPCHK(hipStreamSynchronize(eng->stream));
+  unsigned long long ep = 0;
+  HIPCHK(hipMemcpy(&ep, eng->epoch, sizeof(ep), hipMemcpyDeviceToHost));
+  ep += (unsigned long long)k;
+  HIPCHK(hipMemcpy(eng->dbg_abort_epoch, &ep, sizeof(ep), hipMemcpyHostToDevice));
   return 0;
 }
 
@@ -1669,6 +1736,7 @@ int hnumo_ti_barotropic_ssprk(hnumo_engine *eng, double *qb_df, const double *qp
   HIPCHK(hipSetDevice(eng->device));
   rc = upload_state(eng, nullptr, qb_df, qprime_df);
   if (rc) return rc;
+  if ((rc = maybe_reprobe(eng))) return rc;
   for (;;) {
     HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
     launch_subcycle(eng, eng->qbp, eng->qp);
@@ -1691,6 +1759,7 @@ int hnumo_predict(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime
   HIPCHK(hipSetDevice(eng->device));
   rc = upload_state(eng, q_df, qb_df, qprime_df);
   if (rc) return rc;
+  if ((rc = maybe_reprobe(eng))) return rc;
   for (;;) {
     HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
     launch_predict(eng);
@@ -1707,6 +1776,8 @@ int hnumo_predict(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime
   HIPCHK(hipMemcpyAsync(qb_df, eng->qbp, 4 * (size_t)eng->npoin * 8, hipMemcpyDeviceToHost, eng->stream));
   HIPCHK(hipMemcpyAsync(qprime_df, eng->qp2, n3 * 8, hipMemcpyDeviceToHost, eng->stream));
   HIPCHK(hipStreamSynchronize(eng->stream));
+  // the device state is now the caller's input: a resident engine uploads again on its next step
+  eng->uploaded = false;
   return 0;
 }
 
@@ -1875,8 +1946,9 @@ int hnumo_bench_steps(hnumo_engine *eng, int nsteps, double *ms_total, double *m
                       int64_t *kernel_launches) {
   if (!eng) return HNUMO_ERR_INVALID;
   HIPCHK(hipSetDevice(eng->device));
-  int rc = ensure_graph(eng);
+  int rc = maybe_reprobe(eng);
   if (rc) return rc;
+  if ((rc = ensure_graph(eng))) return rc;
   HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
   HIPCHK(hipEventRecord(eng->ev0, eng->stream));
   rc = launch_steps(eng, nsteps);

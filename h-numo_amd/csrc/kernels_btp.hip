@@ -75,6 +75,11 @@
 #ifndef HNUMO_VSUM
 #define HNUMO_VSUM 1
 #endif
+// VSUM's node halves in the LEAN arenas too (0: one term task forms all NGL nodes of its (i, q) --
+// fewer wave-iterations and task set-ups per phase, a longer lane)
+#ifndef HNUMO_LEAN_VHALF
+#define HNUMO_LEAN_VHALF 1
+#endif
 // The lean per-stage arenas of large meshes (StageCfg::LEAN); 0 keeps the round-2 layout for A/B.
 #ifndef HNUMO_LEAN
 #define HNUMO_LEAN 1
@@ -334,6 +339,8 @@ struct StageCfg {
   static constexpr int OVS = BS - 3 * P;
   static constexpr bool VSUM = HNUMO_VSUM && !SF && !OTF && 2 * WTMAX <= OVS &&
                                2 * WTMAX + P <= BS && OL >= 2 * WTMAX + P && OL + 4 * NGL <= BS;
+  // VHALF: the node-half split of the term tasks (VSUM; the LEAN arenas per HNUMO_LEAN_VHALF)
+  static constexpr bool VHALF = VSUM && (!LEAN || HNUMO_LEAN_VHALF);
   // (LEAN: the rhs is written only in the last D phase, by the VSUM lanes)
   static_assert(!LEAN || (VSUM && TSZ >= 32 * NQ && TSZ >= 5 * P && 3 * P <= 64 * EW + 64), "LEAN layout");
   static constexpr int TB_LAST = (NCH & 1) ? TB1 : TB0, TB_PREV = (NCH & 1) ? TB0 : TB1;
@@ -1575,11 +1582,11 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     auto tbuf = [&](int k) { return SB + ((k & 1) ? C::TB1 : C::TB0); };
     // (VSUM: task t >= WTMAX is the second node half of pair t - WTMAX: j from JH on; the halves
     // run the same code, the second's surplus iteration masked)
-    constexpr bool VSUM = C::VSUM;
-    constexpr int JH = VSUM ? (NGL + 1) / 2 : NGL;
+    constexpr bool VSUM = C::VSUM, VHALF = C::VHALF;
+    constexpr int JH = VHALF ? (NGL + 1) / 2 : NGL;
     auto term_task = [&](int k, int t) {
       double *T = tbuf(k);
-      const int h = (VSUM && t >= C::WTMAX) ? 1 : 0, tq = t - h * C::WTMAX;
+      const int h = (VHALF && t >= C::WTMAX) ? 1 : 0, tq = t - h * C::WTMAX;
       // task tq = i*nq_k + qi: consecutive lanes write consecutive quad points of one node's row
       // of the term buffer (pitch QCP = QC | 1), so a wave's ds_write_b64 lanes hit distinct banks
       // (qi-major, the lanes were QCP doubles apart: 2-way conflicts)
@@ -1781,7 +1788,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       const int WT = (k < NCH) ? ((k == NCH - 1) ? (Q - k * QC) : QC) * NGL : 0;  // term tasks
       if constexpr (VSUM) {
         // first node halves on [0, WT), second halves on [WTMAX, WTMAX + WT)
-        if ((tid < WT || (tid >= WTMAX && tid < WTMAX + WT)) && !(a.dbg & 64)) term_task(k, tid);
+        if ((tid < WT || (VHALF && tid >= WTMAX && tid < WTMAX + WT)) && !(a.dbg & 64)) term_task(k, tid);
         if (k >= 1 && tid >= C::OVS && !(a.dbg & 4)) vsum_chunk(k - 1);
       } else {
       for_tasks<BS>(tid, 0, WT, [&](int t, bool) { term_task(k, t); });
@@ -1980,6 +1987,9 @@ struct SubArgs {
   unsigned *done;                  // finished-workgroup counter (back to 0 after every launch)
   unsigned *arrive;                // residency rendezvous word (back to 0 after every launch)
   int *err;                        // the run's flag word: RUN_ABORT (see residency_rendezvous)
+  // test hook (hnumo_debug_force_abort): the launch whose epoch equals *abort_epoch gives up as a
+  // non-resident one does (NULL: never)
+  const unsigned long long *abort_epoch;
 };
 
 // Residency rendezvous of a persistent launch (one thread per workgroup).  The sub-cycle's
@@ -2026,7 +2036,15 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
   typedef const __attribute__((address_space(4))) StageArgs CStageArgs;
   CStageArgs *tab = (CStageArgs *)sa.stages;
   __shared__ int s_go;
-  if (tid == 0) s_go = residency_rendezvous(sa.arrive, sa.err, gridDim.x);
+  if (tid == 0) {
+    if (sa.abort_epoch && *sa.abort_epoch == ep) {  // (test hook: every workgroup leaves without work)
+      __hip_atomic_fetch_or(sa.arrive, RDV_ABORT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_or(sa.err, RUN_ABORT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_go = 0;
+    } else {
+      s_go = residency_rendezvous(sa.arrive, sa.err, gridDim.x);
+    }
+  }
   __syncthreads();
   const int NS = s_go ? sa.NS : 0;  // (not resident: no stage, straight to the exit count)
   double pacc[16];  // this thread's time averages (StageCfg::REGACC)

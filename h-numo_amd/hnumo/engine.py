@@ -60,6 +60,8 @@ def lib():
         L.hnumo_stage_path.argtypes = [vp]
         L.hnumo_stage_path.restype = C.c_int
         L.hnumo_persistent_info.argtypes = [vp, C.POINTER(C.c_int32)]
+        L.hnumo_persistent_stats.argtypes = [vp, C.POINTER(C.c_int32)]
+        L.hnumo_debug_force_abort.argtypes = [vp, C.c_int]
         _lib = L
     return _lib
 
@@ -174,6 +176,21 @@ class Engine:
         v = list(out)
         return {"persistent": v[0] == 1, "occupancy_blocks_per_cu": (v[1], v[2]), "cus": v[3],
                 "trial_launch": (v[4], v[5]), "fallbacks": v[6], "lds_bytes_per_workgroup": v[7]}
+
+    @property
+    def persistent_stats(self) -> dict:
+        """The persistent path's in-launch residency check over the engine's life
+        (hnumo_persistent_stats): launches that gave up, trial re-probes, re-probes that found the
+        grid resident again, and the runs left before the next re-probe (-1: not suspended)."""
+        out = (C.c_int32 * 4)()
+        self._check(lib().hnumo_persistent_stats(self.h, out))
+        v = list(out)
+        return {"aborts": v[0], "reprobes": v[1], "recovered": v[2], "wait": v[3]}
+
+    def debug_force_abort(self, k: int):
+        """Test hook: the k-th persistent sub-cycle launch from now (0 = the next) gives up as a
+        launch whose workgroups are not co-resident does (hnumo_debug_force_abort)."""
+        self._check(lib().hnumo_debug_force_abort(self.h, int(k)))
 
     def set_resident(self, on: bool):
         self._check(lib().hnumo_set_resident(self.h, int(on)))

@@ -75,3 +75,11 @@ def step_bytes(case) -> float:
 def element_updates_per_step(case) -> int:
     S = case.scalars
     return owned_elements(case) * 2 * S["N_btp"] * S["kstages"]
+
+
+def stage_bytes_cfg(cfg: dict) -> float:
+    """stage_bytes of a brick configuration (hnumo.case.make_config) without building it:
+    E = nelx*nely elements, F = (nelx+1)*nely + nelx*(nely+1) faces."""
+    ex, ey = int(cfg["nelx"]), int(cfg["nely"])
+    E, F = ex * ey, (ex + 1) * ey + ex * (ey + 1)
+    return E * stage_bytes_per_element(int(cfg["nop"]), F / E)

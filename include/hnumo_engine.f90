@@ -17,7 +17,7 @@ module hnumo_engine_c
         HNUMO_ERR_NONFINITE = 2, HNUMO_ERR_DEVICE = 3, HNUMO_ERR_INVALID = 4
     integer(c_int32_t), parameter, public :: HNUMO_SHEAR_CORRECTOR_REFERENCE = 0, &
         HNUMO_SHEAR_CORRECTOR_PREDICTED = 1
-    integer(c_int), parameter, public :: HNUMO_ABI_EXPECTED = 6   ! must equal hnumo_abi_version()
+    integer(c_int), parameter, public :: HNUMO_ABI_EXPECTED = 7   ! must equal hnumo_abi_version()
     integer(c_int), parameter, public :: HNUMO_SUM_REFERENCE = 0, HNUMO_SUM_FACTORED = 1
 
     ! = hnumo_mesh_desc (mod_grid, mod_face, mod_basis, mod_metrics; optional dense tables)
@@ -83,7 +83,7 @@ module hnumo_engine_c
         hnumo_ti_barotropic_ssprk, hnumo_btp_bcl_coeffs, hnumo_create_rhs_btp, hnumo_get_field_c, &
         hnumo_set_resident, hnumo_sync, hnumo_last_error_c, hnumo_last_error, hnumo_get_field, &
         hnumo_set_summation, hnumo_get_summation, hnumo_stage_path, hnumo_persistent_info, hnumo_predict, &
-        hnumo_rccl_unique_id
+        hnumo_rccl_unique_id, hnumo_persistent_stats
 
     interface
         integer(c_int) function hnumo_engine_create(mesh, statics, params, halo, device, eng) &
@@ -187,6 +187,13 @@ module hnumo_engine_c
             type(c_ptr), value :: eng
             integer(c_int32_t), intent(out) :: out(8)
         end function hnumo_persistent_info
+
+        ! the persistent path over the engine's life, out(4): see hnumo_engine.h (ABI v7)
+        integer(c_int) function hnumo_persistent_stats(eng, out) bind(C, name='hnumo_persistent_stats')
+            import :: c_int, c_int32_t, c_ptr
+            type(c_ptr), value :: eng
+            integer(c_int32_t), intent(out) :: out(4)
+        end function hnumo_persistent_stats
 
         ! the prediction half of ti_rk_bcl (ti_rk_bcl.F90:43-57): out q_df2, qb_df, qprime_df2
         integer(c_int) function hnumo_predict(eng, q_df, qb_df, qprime_df) bind(C, name='hnumo_predict')

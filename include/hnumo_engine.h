@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define HNUMO_ABI_VERSION 6
+#define HNUMO_ABI_VERSION 7
 
 enum {
   HNUMO_OK = 0,
@@ -199,7 +199,9 @@ int hnumo_btp_bcl_coeffs(hnumo_engine *eng, const double *qprime_df);
 
 /* = the prediction half of ti_rk_bcl (ti_rk_bcl.F90:43-57): btp_bcl_coeffs_qdf, the
  *   barotropic sub-cycle, momentum_mass (ABI v6).  In: the step-start state; out: q_df2,
- *   qb_df after the sub-cycle, qprime_df2 (the reference's arrays after :57).           */
+ *   qb_df after the sub-cycle, qprime_df2 (the reference's arrays after :57).  The engine's
+ *   device state becomes the caller's input, so a resident engine (hnumo_set_resident)
+ *   uploads the caller's arrays again on its next hnumo_ti_rk_bcl (ABI v7).             */
 int hnumo_predict(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df);
 
 /* = create_rhs_btp(rhs, qb_df, qprime_df) (mod_rhs_btp.F90:28-59); rhs(3,npoin).    */
@@ -240,12 +242,23 @@ int hnumo_stage_path(hnumo_engine *eng);
  * every element's workgroup can be resident at once: the occupancy estimate says so, a
  * stage-less trial launch at create finds all workgroups resident, and every launch
  * checks again (a rendezvous that gives up after 20 ms instead of waiting on a workgroup
- * that cannot start).  A launch that gives up does no work; the engine then drops the
- * persistent path and repeats the affected steps on per-stage launches (same bits).
+ * that cannot start).  A launch that gives up does no work; the engine then suspends the
+ * persistent path, repeats the affected steps on per-stage launches (same bits) and, after
+ * a back-off of 1, 2, 4 ... 1024 runs, re-probes with a stage-less trial launch: resident
+ * again -> persistent again (ABI v7).
  * out[8] = {stage path (as hnumo_stage_path), estimated workgroups per CU (reference /
  * factored summation), CU count, trial launch outcome (reference / factored: 1 resident,
  * 0 not, -1 not run), runs that fell back, LDS bytes per workgroup}.                   */
 int hnumo_persistent_info(hnumo_engine *eng, int32_t *out8);
+
+/* The persistent path over the engine's life (ABI v7): out[4] = {launches that gave up,
+ * trial re-probes, re-probes that found the grid resident again, runs before the next
+ * re-probe (-1: the path is not suspended)}.                                          */
+int hnumo_persistent_stats(hnumo_engine *eng, int32_t *out4);
+
+/* Test hook (ABI v7): the k-th persistent sub-cycle launch from now (0 = the next) gives
+ * up exactly as a launch whose workgroups are not all resident does.                  */
+int hnumo_debug_force_abort(hnumo_engine *eng, int k);
 
 /* RCCL unique id (128 bytes) for hnumo_halo_desc.comm_id: generated by one rank and
  * broadcast by the host (MPI / torch.distributed) before hnumo_engine_create.        */

@@ -10,18 +10,22 @@
  * It follows the reference Fortran loop for loop and operation for operation, on the
  * same dense per-quad-point tables (psih, dpsidx, dpsidy, indexq, wjac and their nodal
  * twins, Tensor_product.F90:1-128), so that with -O2 -ffp-contract=off it reproduces
- * the reference's arithmetic bitwise.  Pinning: tests/test_oracle_ref.py compares it
- * against the reference Fortran itself (oracle/_ref, built from /root/reference/src by
- * oracle/Makefile) and against the committed golden vectors in tests/golden/.
+ * the reference's arithmetic bitwise.  Pinning: tests/test_oracle.py compares it against
+ * the reference Fortran itself (oracle/_ref/ref_driver, built from /root/reference/src by
+ * oracle/build_ref.sh; the -m ref tests) and against the committed golden vectors in
+ * tests/golden/ (made by tests/golden/make_golden.py from the reference's own outputs).
  *
  * Each function cites the reference routine it restates.  Arrays use the reference's
  * Fortran layouts; the A*() macros index them 1-based exactly as the Fortran does.
  *
  * method_visc == 1 (quad-point LDG viscosity, mod_laplacian_quad.F90:125-223,252-355) is
- * restated below.  Not restated (unsupported, returns HNUMO_ERR_INVALID): ad_mlswe > 0
- * vertical shear stress (mod_create_rhs_mlswe.F90:146-279), whose reference reads two
- * uninitialised arrays (tau_u(nlayers+1) at :246-247, uv at mod_splitting.F90:158);
- * multi-rank halos (np=1).
+ * restated below, and so is ad_mlswe > 0 (the implicit vertical shear stress,
+ * mod_create_rhs_mlswe.F90:146-279, in momentum_mass / momentum): the reference reads two
+ * never-assigned arrays there, tau_u(nlayers+1) (:246-247) and, in the corrector, uv
+ * (mod_splitting.F90:158); both are taken as zero, as the reference build's -finit-real=zero
+ * makes them, and the predictor is pinned bit for bit against the reference Fortran run with
+ * oracle/zero_init_wrap.c (tests/test_oracle.py, fixtures *_predict).  Single rank only: the
+ * multi-rank reference runs are the reference Fortran itself under mpiexec.
  */
 #include <math.h>
 #include <stdio.h>

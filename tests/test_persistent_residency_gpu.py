@@ -116,3 +116,59 @@ def test_resident_run_falls_back(case_factory, monkeypatch):
     assert e.persistent_info["fallbacks"] == 1
     e.close()
     e0.close()
+
+
+def test_corrector_abort_is_redone_and_path_recovers(case_factory, monkeypatch):
+    """The corrector's persistent launch gives up after the predictor's sub-cycle and its
+    baroclinic kernels ran (hnumo_debug_force_abort: launch 0 of the step is the predictor's
+    sub-cycle, launch 1 the corrector's).  The step is redone on per-stage launches with the
+    reference's bits; the next step re-probes residency with a trial launch, finds the grid
+    resident and runs persistent again -- the same bits as an engine on per-stage launches from
+    the start."""
+    from hnumo.engine import Engine
+    g, case = golden_case("dg25L3_step1", case_factory)
+    e = Engine(case)
+    assert e.stage_path == "persistent"
+    e.debug_force_abort(1)
+    q, qb, qp = e.state()
+    e.ti_rk_bcl(q, qb, qp)
+    assert_golden(g, q, qb, qp)
+    st = e.persistent_stats
+    assert st["aborts"] == 1 and st["reprobes"] == 0 and e.stage_path == "per-stage", st
+    monkeypatch.setenv("HNUMO_PERSISTENT", "0")
+    e0 = Engine(case)
+    monkeypatch.delenv("HNUMO_PERSISTENT")
+    a = [x.copy(order="F") for x in (q, qb, qp)]
+    for _ in range(2):
+        e.ti_rk_bcl(q, qb, qp)
+        e0.ti_rk_bcl(*a)
+        assert e.stage_path == "persistent"
+    for x, y in zip((q, qb, qp), a):
+        assert np.array_equal(x, y)
+    st = e.persistent_stats
+    assert st == {"aborts": 1, "reprobes": 1, "recovered": 1, "wait": -1}, st
+    e.close()
+    e0.close()
+
+
+def test_predict_on_resident_engine_reuploads(case_factory):
+    """hnumo_predict replaces the device state with the caller's input (ABI v7): a resident
+    engine's next step then starts from the caller's arrays, not from its old device state."""
+    from hnumo.engine import Engine
+    _, case = golden_case("dg25L3_step1", case_factory)
+    e = Engine(case)
+    e.set_resident(True)
+    q, qb, qp = e.state()
+    e.ti_rk_bcl(q, qb, qp)                        # device state: step 1
+    p = [x.copy(order="F") for x in e.state()]
+    e.predict(*p)                                 # device state: the IC's predictor input
+    r = e.state()
+    e.ti_rk_bcl(*r)                               # must start from r (the IC), not from step 1
+    e.sync(*r)
+    e1 = Engine(case)
+    s = e1.state()
+    e1.ti_rk_bcl(*s)
+    for x, y in zip(r, s):
+        assert np.array_equal(x, y)
+    e.close()
+    e1.close()
