@@ -1584,6 +1584,18 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     // run the same code, the second's surplus iteration masked)
     constexpr bool VSUM = C::VSUM, VHALF = C::VHALF;
     constexpr int JH = VHALF ? (NGL + 1) / 2 : NGL;
+    // FULLCH (every chunk whole quad rows): a term lane's (i, qi) and its quad point's column iq and
+    // row offset are the same in every phase, so they are formed once, before the phases, and the
+    // per-phase LDS addresses are one per-lane base plus the phase's constant (immediate offsets)
+    constexpr bool FULLCH = (Q % QC == 0) && (QC % NQ == 0) && C::WTMAX * (VHALF ? 2 : 1) <= BS;  // (task t on thread t)
+    int tl_i = 0, tl_qi = 0, tl_iq = 0, tl_jr = 0;
+    if constexpr (FULLCH) {
+      const int h = (VHALF && tid >= C::WTMAX) ? 1 : 0, tq = tid - h * C::WTMAX;
+      tl_i = tq / QC;
+      tl_qi = tq - tl_i * QC;
+      tl_iq = (QC == NQ) ? tl_qi : tl_qi % NQ;
+      tl_jr = (QC == NQ) ? 0 : tl_qi / NQ;
+    }
     auto term_task = [&](int k, int t) {
       double *T = tbuf(k);
       const int h = (VHALF && t >= C::WTMAX) ? 1 : 0, tq = t - h * C::WTMAX;
@@ -1591,8 +1603,9 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       // of the term buffer (pitch QCP = QC | 1), so a wave's ds_write_b64 lanes hit distinct banks
       // (qi-major, the lanes were QCP doubles apart: 2-way conflicts)
       const int nq_k = (k == NCH - 1) ? Q - k * QC : QC;
-      const int i = tq / nq_k, qi = tq - i * nq_k;
-      const int q = k * QC + qi, iq = q % NQ, jq = q / NQ;
+      const int i = FULLCH ? tl_i : tq / nq_k, qi = FULLCH ? tl_qi : tq - i * nq_k;
+      const int q = k * QC + qi;
+      const int iq = FULLCH ? tl_iq : q % NQ, jq = FULLCH ? k * (QC / NQ) + tl_jr : q / NQ;
       const double wq = s_qk[qe_pos(QE_W, q, Q)], ex = s_qk[qe_pos(QE_EX, q, Q)], ey = s_qk[qe_pos(QE_EY, q, Q)];
       const double nx = s_qk[qe_pos(QE_NX, q, Q)], ny = s_qk[qe_pos(QE_NY, q, Q)];
       const double udp = s_qv[0 * Q + q], vdp = s_qv[1 * Q + q], scx = s_qv[2 * Q + q], A = s_qv[3 * Q + q];

@@ -37,27 +37,23 @@ def state_hash(e, st=None):
 
 def timed(e, steps, group=False):
     from hnumo.engine import group_ti_rk_bcl
-    import torch
+    # (no torch here: the engine calls synchronise their streams before returning)
     if group:
         e.set_resident(True)
         st = [e.state()]
         for _ in range(2):              # warm-up (uploads), as many steps as the resident variants
             group_ti_rk_bcl([e], st)
-        torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
             group_ti_rk_bcl([e], st)
-        torch.cuda.synchronize()
         t = (time.perf_counter() - t0) / steps
         return t, None
     e.set_resident(True)
     q, qb, qp = e.state()
     e.ti_rk_bcl(q, qb, qp)              # uploads, captures (or not) the step
     e.bench_steps(1)
-    torch.cuda.synchronize()
     t0 = time.perf_counter()
     _, k_ms, _ = e.bench_steps(steps)
-    torch.cuda.synchronize()
     return (time.perf_counter() - t0) / steps, k_ms
 
 
