@@ -104,6 +104,13 @@
 #ifndef HNUMO_PRIO_B
 #define HNUMO_PRIO_B 1
 #endif
+// diagnostics builds only (-DHNUMO_DBG_EXTRA=1, instruction-mix ablations: tools/pmc_ablate.sh):
+// more phase switches in StageArgs::dbg -- 128 A2 interpolations, 256 B quad-point tasks, 512 B
+// face tasks, 1024 B nodal tasks, 2048 E2 trace stores, 4096 the A copies of the records
+#ifndef HNUMO_DBG_EXTRA
+#define HNUMO_DBG_EXTRA 0
+#endif
+#define DBGX(bit) (HNUMO_DBG_EXTRA && (a.dbg & (bit)))
 #define SETPRIO_IF(cond, hi, lo)        \
   do {                                  \
     if (cond)                           \
@@ -528,7 +535,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   if (a.prof && tid == 0) s_prof[22] = 0;
   const bool use_q0 = !a.rhs_only && a.a1 != 0.0, use_q2 = !a.rhs_only && a.a3 != 0.0;
   const int qpm = (SF || !m.botfr || !a.qpq) ? 0 : a.qpq_mode;  // see StageArgs::qpq
-  {
+  if (!DBGX(4096)) {
     int rot = 0;
     if (!PERSIST || first) {
       glds_copy<BS, C::G16>(PDI ? m.basis_pd : m.basis, S + C::O_BASIS, 2 * C::NB, tid, rot);
@@ -741,6 +748,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     for (int w = tid; w < T_UV + NFP; w += BS) {
       asm volatile("" ::: "memory");
       if (w < nint) {
+        if (DBGX(128)) continue;
         const int g = w / TPG, r = w % TPG;
         if constexpr (SF) {
           const int mm = r / NQ, iq = r % NQ;
@@ -1026,6 +1034,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   for (int w = tid; w < C::BEND; w += BS) {
     asm volatile("" ::: "memory");
     if (w < Q) {
+      if (DBGX(256)) continue;
       // ---- quad-point physics (mod_rhs_btp.F90:136-192)
       const int q = w, iq = q % NQ, jq = q / NQ;
       double dp = 0, dpp = 0, udp = 0, vdp = 0, pp = 0, up = 0, vp = 0;
@@ -1135,8 +1144,9 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         QO(6, q) = Hq + qv;
       }
     } else if (!C::SLATE && w >= C::OF && w < C::OF + 4 * NQ) {
-      face_task(w - C::OF);
+      if (!DBGX(512)) face_task(w - C::OF);
     } else if (w >= C::OG && w < C::OL) {
+      if (DBGX(1024)) continue;
       const int p = w - C::OG, i = p % NGL, j = p / NGL;
       double g[4];
       if (PERSIST && (!first || a.self_trace)) {  // formed by the previous stage's E2 (or A2) for this state
@@ -1910,7 +1920,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   // (persistent: the state stays in LDS; only the sub-cycle's last stage writes it out)
   if (!PERSIST || !a.write_trace)
     for (int t = tid; t < 4 * P; t += BS) a.qb_out[(size_t)e * 4 * P + t] = s_qn[t];
-  if (a.write_trace) {
+  if (a.write_trace && !DBGX(2048)) {
     // traces of the new state on each interior face, into the neighbour's slot:
     // qb(4) and grad(u_bar)(4) at the face nodes
     for (int t = tid; t < 4 * 8 * NGL; t += BS) {

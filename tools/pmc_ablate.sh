@@ -1,7 +1,10 @@
 #!/bin/bash
 # Instruction mix of the per-stage kernel with diagnostic phase switches (HNUMO_STAGE_DBG bits:
-# 1 face lifts, 2 Laplacian, 4 volume sums, 32 time averages, 64 term tasks; timing/counting only,
-# they break the physics): SQ_INSTS_* per element-stage for each switch, one rocprofv3 run each.
+# 1 face lifts, 2 Laplacian, 4 volume sums, 32 time averages, 64 term tasks; with a
+# -DHNUMO_DBG_EXTRA=1 build also 128 A2 interpolations, 256 B quad tasks, 512 B face tasks, 1024 B
+# nodal tasks, 2048 E2 trace stores, 4096 the A record copies (only with 2048: the trace slots
+# come from the records); counting only, they break the physics): SQ_INSTS_* per element-stage
+# for each switch, one rocprofv3 run each.  DBGS overrides the list of switches.
 # Usage (via gpurun): bash tools/pmc_ablate.sh <outdir> [cfg] [lib.so ...]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -14,7 +17,7 @@ mkdir -p $OUT
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_FMA_F64"
 for lib in $LIBS; do
   tag=$(basename $lib .so)
-  for dbg in 0 64 4 1 2 32 68; do
+  for dbg in ${DBGS:-0 64 4 1 2 32 68}; do
     if [ "$lib" = default ]; then L=""; else L=$lib; fi
     HNUMO_LIB=$L HNUMO_STAGE_DBG=$dbg timeout -s KILL 180 rocprofv3 --kernel-trace --pmc $SQ -d $OUT/${tag}_d$dbg -o run --output-format csv -- python3 tools/stage_only.py $CFG 1 > $OUT/${tag}_d$dbg.log 2>&1 || { echo "pass $tag dbg $dbg failed"; tail -5 $OUT/${tag}_d$dbg.log; exit 1; }
   done
