@@ -80,6 +80,10 @@
 #ifndef HNUMO_LEAN_VHALF
 #define HNUMO_LEAN_VHALF 1
 #endif
+// VPACK (LEAN): the 3P summing chains on as few waves as they fill (see StageCfg::VPACK)
+#ifndef HNUMO_VPACK
+#define HNUMO_VPACK 0
+#endif
 // The lean per-stage arenas of large meshes (StageCfg::LEAN); 0 keeps the round-2 layout for A/B.
 #ifndef HNUMO_LEAN
 #define HNUMO_LEAN 1
@@ -348,6 +352,12 @@ struct StageCfg {
                                2 * WTMAX + P <= BS && OL >= 2 * WTMAX + P && OL + 4 * NGL <= BS;
   // VHALF: the node-half split of the term tasks (VSUM; the LEAN arenas per HNUMO_LEAN_VHALF)
   static constexpr bool VHALF = VSUM && (!LEAN || HNUMO_LEAN_VHALF);
+  // VPACK (LEAN): summing chains [0, 64) on the last wave, chains [64, 3P) on the lanes of wave 1
+  // past its term tasks ([2*WTMAX, ...)), instead of [OVS, BS): there the wave below the last held
+  // only 3P - 64 chains and issued every sum instruction for them (C4: 11 of 64 lanes)
+  static constexpr int VCH_HI = BS - 64, VCH_LO = VHALF ? 2 * WTMAX : WTMAX;
+  static constexpr bool VPACK = HNUMO_VPACK && LEAN && VSUM && 3 * P > 64 && VCH_LO >= 64 &&
+                                VCH_LO + 3 * P - 64 <= 128 && VCH_LO + 3 * P - 64 <= VCH_HI;
   // (LEAN: the rhs is written only in the last D phase, by the VSUM lanes)
   static_assert(!LEAN || (VSUM && TSZ >= 32 * NQ && TSZ >= 5 * P && 3 * P <= 64 * EW + 64), "LEAN layout");
   static constexpr int TB_LAST = (NCH & 1) ? TB1 : TB0, TB_PREV = (NCH & 1) ? TB0 : TB1;
@@ -1749,9 +1759,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     constexpr int WTMAX = C::WTMAX;
     constexpr int OSUM = (P <= 64 && WTMAX <= BS - 64) ? BS - 64 : WTMAX;
     // VSUM: thread OVS + (v*P + p) sums chain (v, p) of every chunk, the partial sum in vacc
+    // (VPACK: chain tid - VCH_HI on the last wave, 64 + tid - VCH_LO on wave 1)
+    const int vch = C::VPACK ? (tid >= C::VCH_HI ? tid - C::VCH_HI
+                                                 : (tid >= C::VCH_LO && tid < C::VCH_LO + 3 * P - 64 ? 64 + tid - C::VCH_LO : -1))
+                             : (tid >= C::OVS ? tid - C::OVS : -1);
     double vacc = 0.0;
     auto vsum_chunk = [&](int k) {
-      const int t = tid - C::OVS, v = t / P, p = t - v * P;
+      const int t = vch, v = t / P, p = t - v * P;
       const int nq_k = (k == NCH - 1) ? Q - k * QC : QC;
       const double *T = tbuf(k) + (v * P + p) * QCP;
       constexpr int SBK = 9;
@@ -1803,7 +1817,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     }
     // the term-task waves behind everything else, the summing waves ahead
     if (HNUMO_PRIO)
-      SETPRIO_IF(VSUM ? tid >= C::OVS - (C::OVS & 63) : (OSUM == BS - 64 && tid >= OSUM), HNUMO_PRIO_S, 0);
+      SETPRIO_IF(C::VPACK ? tid >= C::VCH_HI : VSUM ? tid >= C::OVS - (C::OVS & 63) : (OSUM == BS - 64 && tid >= OSUM),
+                 HNUMO_PRIO_S, 0);
 #pragma unroll
     for (int k = 0; k <= NCH; k++) {
       asm volatile("" ::: "memory");  // keep LDS reads inside their phase (no hoisting)
@@ -1812,7 +1827,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       if constexpr (VSUM) {
         // first node halves on [0, WT), second halves on [WTMAX, WTMAX + WT)
         if ((tid < WT || (VHALF && tid >= WTMAX && tid < WTMAX + WT)) && !(a.dbg & 64)) term_task(k, tid);
-        if (k >= 1 && tid >= C::OVS && !(a.dbg & 4)) vsum_chunk(k - 1);
+        if (k >= 1 && vch >= 0 && !(a.dbg & 4)) vsum_chunk(k - 1);
       } else {
       for_tasks<BS>(tid, 0, WT, [&](int t, bool) { term_task(k, t); });
       if (k >= 1 && k < NCH) for_tasks<BS>(tid, OSUM, P, [&](int t, bool) { sum_task(k - 1, t); });
