@@ -80,6 +80,11 @@
 #ifndef HNUMO_LEAN_VHALF
 #define HNUMO_LEAN_VHALF 1
 #endif
+// node groups of the LEAN arenas' term tasks (2: the VSUM halves; 3: thirds -- more, shorter
+// term lanes: the D phases' waves closer in length, at more set-ups)
+#ifndef HNUMO_LEAN_NSPLIT
+#define HNUMO_LEAN_NSPLIT 2
+#endif
 // VPACK (LEAN): the 3P summing chains on as few waves as they fill (see StageCfg::VPACK)
 #ifndef HNUMO_VPACK
 #define HNUMO_VPACK 0
@@ -352,10 +357,13 @@ struct StageCfg {
                                2 * WTMAX + P <= BS && OL >= 2 * WTMAX + P && OL + 4 * NGL <= BS;
   // VHALF: the node-half split of the term tasks (VSUM; the LEAN arenas per HNUMO_LEAN_VHALF)
   static constexpr bool VHALF = VSUM && (!LEAN || HNUMO_LEAN_VHALF);
+  // NSPLIT: node groups of the term tasks, task t = (group t / WTMAX, task t % WTMAX) on thread t
+  static constexpr int NSPLIT0 = !VHALF ? 1 : (LEAN ? HNUMO_LEAN_NSPLIT : 2);
+  static constexpr int NSPLIT = (NSPLIT0 > 2 && NSPLIT0 * WTMAX + P > OVS) ? 2 : NSPLIT0;
   // VPACK (LEAN): summing chains [0, 64) on the last wave, chains [64, 3P) on the lanes of wave 1
   // past its term tasks ([2*WTMAX, ...)), instead of [OVS, BS): there the wave below the last held
   // only 3P - 64 chains and issued every sum instruction for them (C4: 11 of 64 lanes)
-  static constexpr int VCH_HI = BS - 64, VCH_LO = VHALF ? 2 * WTMAX : WTMAX;
+  static constexpr int VCH_HI = BS - 64, VCH_LO = NSPLIT * WTMAX;
   static constexpr bool VPACK = HNUMO_VPACK && LEAN && VSUM && 3 * P > 64 && VCH_LO >= 64 &&
                                 VCH_LO + 3 * P - 64 <= 128 && VCH_LO + 3 * P - 64 <= VCH_HI;
   // (LEAN: the rhs is written only in the last D phase, by the VSUM lanes)
@@ -1602,15 +1610,15 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     auto tbuf = [&](int k) { return SB + ((k & 1) ? C::TB1 : C::TB0); };
     // (VSUM: task t >= WTMAX is the second node half of pair t - WTMAX: j from JH on; the halves
     // run the same code, the second's surplus iteration masked)
-    constexpr bool VSUM = C::VSUM, VHALF = C::VHALF;
-    constexpr int JH = VHALF ? (NGL + 1) / 2 : NGL;
+    constexpr bool VSUM = C::VSUM;
+    constexpr int NSP = C::NSPLIT, JH = (NGL + NSP - 1) / NSP;
     // FULLCH (every chunk whole quad rows): a term lane's (i, qi) and its quad point's column iq and
     // row offset are the same in every phase, so they are formed once, before the phases, and the
     // per-phase LDS addresses are one per-lane base plus the phase's constant (immediate offsets)
-    constexpr bool FULLCH = (Q % QC == 0) && (QC % NQ == 0) && C::WTMAX * (VHALF ? 2 : 1) <= BS;  // (task t on thread t)
+    constexpr bool FULLCH = (Q % QC == 0) && (QC % NQ == 0) && C::WTMAX * NSP <= BS;  // (task t on thread t)
     int tl_i = 0, tl_qi = 0, tl_iq = 0, tl_jr = 0;
     if constexpr (FULLCH) {
-      const int h = (VHALF && tid >= C::WTMAX) ? 1 : 0, tq = tid - h * C::WTMAX;
+      const int h = NSP == 2 ? (tid >= C::WTMAX ? 1 : 0) : (NSP > 1 ? tid / C::WTMAX : 0), tq = tid - h * C::WTMAX;
       tl_i = tq / QC;
       tl_qi = tq - tl_i * QC;
       tl_iq = (QC == NQ) ? tl_qi : tl_qi % NQ;
@@ -1618,7 +1626,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     }
     auto term_task = [&](int k, int t) {
       double *T = tbuf(k);
-      const int h = (VHALF && t >= C::WTMAX) ? 1 : 0, tq = t - h * C::WTMAX;
+      const int h = NSP == 2 ? (t >= C::WTMAX ? 1 : 0) : (NSP > 1 ? t / C::WTMAX : 0), tq = t - h * C::WTMAX;
       // task tq = i*nq_k + qi: consecutive lanes write consecutive quad points of one node's row
       // of the term buffer (pitch QCP = QC | 1), so a wave's ds_write_b64 lanes hit distinct banks
       // (qi-major, the lanes were QCP doubles apart: 2-way conflicts)
@@ -1826,7 +1834,9 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       const int WT = (k < NCH) ? ((k == NCH - 1) ? (Q - k * QC) : QC) * NGL : 0;  // term tasks
       if constexpr (VSUM) {
         // first node halves on [0, WT), second halves on [WTMAX, WTMAX + WT)
-        if ((tid < WT || (VHALF && tid >= WTMAX && tid < WTMAX + WT)) && !(a.dbg & 64)) term_task(k, tid);
+        if ((NSP == 2 ? (tid < WT || (tid >= WTMAX && tid < WTMAX + WT))
+                      : (tid < NSP * WTMAX && tid - (tid / WTMAX) * WTMAX < WT)) && !(a.dbg & 64))
+          term_task(k, tid);
         if (k >= 1 && vch >= 0 && !(a.dbg & 4)) vsum_chunk(k - 1);
       } else {
       for_tasks<BS>(tid, 0, WT, [&](int t, bool) { term_task(k, t); });
@@ -1838,7 +1848,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           for_tasks<BS>(tid, OSUM, P, [&](int t, bool) { sum_task(k - 1, t); });
       }
       }
-      if (k == 0) for_tasks<BS>(tid, VSUM ? 2 * WTMAX : WT, P, [&](int t, bool) { qq_task(t); });
+      if (k == 0) for_tasks<BS>(tid, VSUM ? C::NSPLIT * WTMAX : WT, P, [&](int t, bool) { qq_task(t); });
       if (k == 0) for_tasks<BS>(tid, C::OL, 4 * NGL, ldg_task);
       if (k == NCH && !(a.dbg & 2)) for_tasks<BS>(tid, 0, 2 * P, [&](int t, bool) { lap_task(t / P, t % P); });
       LDS_BARRIER();
