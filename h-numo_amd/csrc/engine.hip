@@ -932,6 +932,10 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
         nb.n = halo->num_send_recv[k];
         if (nb.rank < 0 || nb.rank >= halo->nranks || (nb.rank == halo->rank && halo->nranks > 1))
           return fail(eng, HNUMO_ERR_INVALID, "nbh_proc: bad neighbour rank (1-based ranks expected)");
+        // mod_parallel lists each neighbour process once (p4est.c:1343-1360); the transports pair a
+        // rank's message with the peer's one entry for it
+        for (const auto &pn : eng->fnb)
+          if (pn.rank == nb.rank) return fail(eng, HNUMO_ERR_INVALID, "nbh_proc: a neighbour rank is listed twice");
         if (nb.n < 0) return fail(eng, HNUMO_ERR_INVALID, "num_send_recv < 0");
         for (int i = 0; i < nb.n; i++) {
           const int f = halo->nbh_send_recv[o + i] - 1;
@@ -1335,6 +1339,8 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
       nb.nrecv = halo->num_ghost_recv ? halo->num_ghost_recv[k] : 0;
       if (nb.rank < 0 || nb.rank >= halo->nranks || nb.rank == halo->rank)
         return fail(eng, HNUMO_ERR_INVALID, "bad neighbour rank");
+      for (const auto &pn : eng->nbh)
+        if (pn.rank == nb.rank) return fail(eng, HNUMO_ERR_INVALID, "a neighbour rank is listed twice");
       std::vector<int> snd(nb.nsend), rcv(nb.nrecv);
       for (int i = 0; i < nb.nsend; i++) {
         snd[i] = halo->ghost_send[os + i] - 1;

@@ -47,3 +47,21 @@ def test_face_halo_matches_reference_mpi(name):
                 assert state_sha256(a) == str(g[f"{k}_sha256_r{r}"]), (name, r, k)
     for e in engines:
         e.close()
+
+
+def test_neighbour_listed_twice_is_rejected():
+    """mod_parallel lists each neighbour process once (p4est.c:1343-1360) and the transports pair a
+    rank's message with the peer's one entry for it: a halo that lists a neighbour rank twice is
+    an invalid argument (code 4), not a transfer of mismatched sizes."""
+    from hnumo.case import build_case, make_config
+    from hnumo.engine import Engine, EngineError
+    from hnumo.facepart import FaceNeighbour, face_partition
+    case = build_case(make_config("bump10"), dense=False)
+    pc = face_partition(case, 3, 1, "morton")
+    assert len(pc.fneighbours) == 2
+    f = pc.fneighbours
+    pc.fneighbours = [FaceNeighbour(f[0].rank, f[0].faces[: len(f[0].faces) // 2]),
+                      FaceNeighbour(f[0].rank, f[0].faces[len(f[0].faces) // 2:]), f[1]]
+    with pytest.raises(EngineError) as ei:
+        Engine(pc)
+    assert ei.value.code == 4 and "listed twice" in str(ei.value)

@@ -69,9 +69,12 @@ def main():
     g = build_case(make_config("dg316L3"), dense=False)
     pc = face_partition(g, 8, args.rank, "block")
     nbrs = [(n.rank, int(n.faces.size)) for n in pc.fneighbours]
-    pc.nranks = 1
-    for n in pc.fneighbours:
-        n.rank = 0
+    # the self-neighbour contract: every processor face listed under the rank itself, as ONE list
+    # (mod_parallel lists each neighbour once; the engine rejects a rank listed twice)
+    import numpy as np
+    from hnumo.facepart import FaceNeighbour
+    pc.nranks, pc.rank = 1, 0
+    pc.fneighbours = [FaceNeighbour(0, np.concatenate([n.faces for n in pc.fneighbours]))]
     E = pc.scalars["nelem"]
     S = g.scalars
     stages = 2 * S["N_btp"] * S["kstages"]
