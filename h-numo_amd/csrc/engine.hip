@@ -5,6 +5,7 @@
 // baroclinic step (2 barotropic sub-cycles = 2*N_btp*kstages fused stage kernels plus
 // ~20 baroclinic kernels) is captured once into a hipGraph and replayed.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <rccl/rccl.h>
 
@@ -86,6 +87,8 @@ struct hnumo_engine {
   hipEvent_t evk0 = nullptr, evk1 = nullptr;
   bool capturing = false, kernel_events = false, no_graph = false;
   bool no_fuse = false;                      // HNUMO_FUSE=0: face kernels and extract launches (A/B)
+  int sched_dbg = 0;                         // HNUMO_SCHED_DBG (timing experiments only, wrong results):
+                                             // 1 the interior launch skips its wait for the boundary one
   int summation = HNUMO_SUM_REFERENCE;        // hnumo_set_summation
   unsigned long long *stage_prof = nullptr;  // HNUMO_STAGE_PROF=1: per-element phase clocks
   int stage_dbg = 0;                         // HNUMO_STAGE_DBG: diagnostic phase switches (timing only)
@@ -134,6 +137,7 @@ struct hnumo_engine {
   double *cdef = nullptr;                    // consistency deficits [L][side][2][F*NQ]
   hipStream_t stream2 = nullptr;             // boundary elements + trace transport (two-stream schedule)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_I = nullptr, ev_B[2] = {nullptr, nullptr};
+  hipEvent_t ev_Is = nullptr, ev_Bs[2] = {nullptr, nullptr};  // kernel stop events of the same hand-offs
   // local exchange group, processor-face transport: device copies ordered by events
   hipEvent_t ev_tsent = nullptr, ev_bpacked = nullptr, ev_bdone = nullptr;
   // method_visc == 1 (quad-point LDG, kernels_lapq.hip)
@@ -181,14 +185,24 @@ template <int NGL, int NQ>
 struct Launch {
   static constexpr int BSE = ((NQ * NQ + 63) / 64) * 64;
   // one stage over the owned elements, or over the `n` elements of a.elist on stream `st`
-  static void stage(hnumo_engine *e, const StageArgs &a, int n = -1, hipStream_t st = nullptr) {
+  // (stop: an event the launch itself signals at completion -- the two-stream schedule's hand-offs
+  // without separate record packets, hipExtLaunchKernelGGL)
+  static void stage(hnumo_engine *e, const StageArgs &a, int n = -1, hipStream_t st = nullptr,
+                    hipEvent_t stop = nullptr) {
     if (n < 0) n = e->nelem_owned;
     if (!st) st = e->stream;
-    if (n == 0) return;
+    if (n == 0) {
+      if (stop) (void)hipEventRecord(stop, st);
+      return;
+    }
     if constexpr (NGL == 5) {
       if (e->summation == HNUMO_SUM_REFERENCE && e->stage_nb == 5) {
-        hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, 5>), dim3(n), dim3(StageCfg<NGL, NQ, false, 5>::BS), 0,
-                           st, a);
+        if (stop)
+          hipExtLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, 5>), dim3(n), dim3(StageCfg<NGL, NQ, false, 5>::BS),
+                                0, st, nullptr, stop, 0, a);
+        else
+          hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, 5>), dim3(n), dim3(StageCfg<NGL, NQ, false, 5>::BS), 0,
+                             st, a);
         return;
       }
       if (e->summation == HNUMO_SUM_REFERENCE && e->stage_nb == 4) {
@@ -201,6 +215,7 @@ struct Launch {
       hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false>), dim3(n), dim3(StageCfg<NGL, NQ, false>::BS), 0, st, a);
     else
       hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, true>), dim3(n), dim3(StageCfg<NGL, NQ, true>::BS), 0, st, a);
+    if (stop) (void)hipEventRecord(stop, st);
   }
   static void subcycle(hnumo_engine *e, const StageArgs *stages, int ns) {
     SubArgs sa{stages, ns, e->epoch, e->sub_done, e->sub_arrive, e->neg_flag, e->dbg_abort_epoch};
@@ -758,15 +773,22 @@ static void launch_subcycle(hnumo_engine *e, double *dst, const double *qp, bool
     (void)hipEventRecord(e->ev_I, e->stream);
     for (size_t i = 0; i < st.size(); i++) {
       StageArgs a = st[i];
-      (void)hipStreamWaitEvent(e->stream2, e->ev_I, 0);
+      // (stop events: each launch signals its own completion, no record packet between the
+      // interior launches; HNUMO_SCHED_DBG 2 restores the recorded events for A/B)
+      hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+      (void)hipStreamIsCapturing(e->stream, &cap);
+      const bool sev = !(e->sched_dbg & 2) && e->ev_Bs[0] && cap == hipStreamCaptureStatusNone;
+      (void)hipStreamWaitEvent(e->stream2, sev ? e->ev_Is : e->ev_I, 0);
       a.elist = e->d_elB;
-      DISPATCH(e, stage(e, a, e->nB, e->stream2));
-      (void)hipEventRecord(e->ev_B[i & 1], e->stream2);
+      DISPATCH(e, stage(e, a, e->nB, e->stream2, sev ? e->ev_Bs[i & 1] : nullptr));
+      if (!sev) (void)hipEventRecord(e->ev_B[i & 1], e->stream2);
       if (a.write_trace) trace_exchange(e, a.trace_out, e->stream2);
-      if (i > 0) (void)hipStreamWaitEvent(e->stream, e->ev_B[(i - 1) & 1], 0);
+      if (i > 0 && !(e->sched_dbg & 1))
+        (void)hipStreamWaitEvent(e->stream, sev ? e->ev_Bs[(i - 1) & 1] : e->ev_B[(i - 1) & 1], 0);
       a.elist = e->d_elI;
-      DISPATCH(e, stage(e, a, e->nI, e->stream));
-      (void)hipEventRecord(e->ev_I, e->stream);
+      a.tcontig = 1;  // (interior elements: trace slots 4e..4e+3, StageArgs::tcontig)
+      DISPATCH(e, stage(e, a, e->nI, e->stream, sev ? e->ev_Is : nullptr));
+      if (!sev) (void)hipEventRecord(e->ev_I, e->stream);
     }
     (void)hipEventRecord(e->ev_join, e->stream2);
     (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);
@@ -883,6 +905,8 @@ void hnumo_engine_destroy(hnumo_engine *eng) {
   if (eng->ev1) (void)hipEventDestroy(eng->ev1);
   if (eng->evk0) (void)hipEventDestroy(eng->evk0);
   if (eng->evk1) (void)hipEventDestroy(eng->evk1);
+  for (hipEvent_t ev : {eng->ev_Is, eng->ev_Bs[0], eng->ev_Bs[1]})
+    if (ev) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : {eng->ev_fork, eng->ev_join, eng->ev_I, eng->ev_B[0], eng->ev_B[1], eng->ev_tsent,
                         eng->ev_bpacked, eng->ev_bdone})
     if (ev) (void)hipEventDestroy(ev);
@@ -1265,6 +1289,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     eng->summation = (sm[0] == 'r' || sm[0] == '0') ? HNUMO_SUM_REFERENCE : HNUMO_SUM_FACTORED;
   if (const char *sd = getenv("HNUMO_STAGE_DBG")) eng->stage_dbg = atoi(sd);
   if (const char *fz = getenv("HNUMO_FUSE")) eng->no_fuse = fz[0] == '0';
+  if (const char *sd = getenv("HNUMO_SCHED_DBG")) eng->sched_dbg = atoi(sd);
   // per-stage kernel arena: on meshes that take several residency rounds per stage, the arena
   // sized for 4 workgroups per CU (1-row term chunks) -- 1.566 -> 1.517 ms per stage at C4
   // (tools/ab_env.py, round 2); small meshes keep the 3-per-CU arena
@@ -1319,6 +1344,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     for (hipEvent_t *ev : {&eng->ev_fork, &eng->ev_join, &eng->ev_I, &eng->ev_B[0], &eng->ev_B[1], &eng->ev_tsent,
                            &eng->ev_bpacked, &eng->ev_bdone})
       HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    for (hipEvent_t *ev : {&eng->ev_Is, &eng->ev_Bs[0], &eng->ev_Bs[1]}) HIPCHK(hipEventCreate(ev));
     if (halo->comm_id) {  // RCCL point-to-point over xGMI
       ncclUniqueId id;
       static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");

@@ -180,6 +180,9 @@ struct StageArgs {
   // processor-face halo: the elements of this launch (block b runs element elist[b]; NULL:
   // element b) -- the boundary / interior split of the two-stream schedule
   const int *elist;
+  // processor-face halo: 1 when no element of this launch has a processor face (the interior list):
+  // its four trace slots are then its own, contiguous, and copied as one block
+  int tcontig;
   // bottom-layer qprime at the quad points (pp, up, vp; mod_rhs_btp.F90:146-152), constant over a
   // sub-cycle: [E][3][Q] scratch (NULL: interpolated by every stage).  qpq_mode 1: this stage
   // interpolates and stores them (a sub-cycle's first stage), 2: loads them (the later stages)
@@ -566,7 +569,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       glds_copy<BS, C::G16>(a.qb_in + (size_t)e * 4 * P, s_qb, 8 * P, tid, rot);
       if (!C::SLIM && !C::LEAN && use_q0) glds_copy<BS, C::G16>(a.qb0 + (size_t)e * 4 * P, s_q0, 8 * P, tid, rot);
       if (!C::SLIM && !C::LEAN && use_q2) glds_copy<BS, C::G16>(a.qb2 + (size_t)e * 4 * P, s_q2, 8 * P, tid, rot);
-      if (m.etsrc) {
+      if (m.etsrc && !a.tcontig) {
         // processor-face halo: each face's neighbour trace from its own slot (the receive
         // slot of a processor face); the slot ids are uniform, scalar loads
 #pragma unroll

@@ -62,6 +62,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--rank", type=int, default=1, help="rank of the 4x2 partition (1: three neighbours)")
     ap.add_argument("--variants", default="block,local,rccl,rccl_g")
+    ap.add_argument("--no-projection", action="store_true")
     args = ap.parse_args()
     from hnumo.case import build_case, make_config
     from hnumo.engine import Engine, local_group
