@@ -200,6 +200,15 @@ struct StageArgs {
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 
+// the four face-slot ids of an element (processor-face halo), one scalar load issued and waited
+// for before the copies (a vector load's wait, vmcnt(0), would hold up every copy issued before it)
+__device__ __forceinline__ int4 slot_ids4(const int *p) {
+  typedef unsigned u4v __attribute__((ext_vector_type(4)));
+  u4v t;
+  asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "s"(p));
+  return make_int4((int)t.x, (int)t.y, (int)t.z, (int)t.w);
+}
+
 // Block-cooperative async copy of ndw dwords, global -> LDS, both contiguous.  One
 // global_load_lds_dword per lane; chunks of 64 dwords rotate over the waves.
 // G16: a 16-byte aligned source and destination move in whole 16-byte pieces first
@@ -558,6 +567,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   const int qpm = (SF || !m.botfr || !a.qpq) ? 0 : a.qpq_mode;  // see StageArgs::qpq
   if (!DBGX(4096)) {
     int rot = 0;
+    const bool tsl = !PERSIST && m.etsrc && !a.tcontig;
+    const int4 ts = tsl ? slot_ids4(m.etsrc + 4 * e) : make_int4(0, 0, 0, 0);
     if (!PERSIST || first) {
       glds_copy<BS, C::G16>(PDI ? m.basis_pd : m.basis, S + C::O_BASIS, 2 * C::NB, tid, rot);
       glds_copy<BS, C::G16>(m.erec + (size_t)e * C::ERS, S + C::O_EREC, C::ERS, tid, rot);
@@ -569,12 +580,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       glds_copy<BS, C::G16>(a.qb_in + (size_t)e * 4 * P, s_qb, 8 * P, tid, rot);
       if (!C::SLIM && !C::LEAN && use_q0) glds_copy<BS, C::G16>(a.qb0 + (size_t)e * 4 * P, s_q0, 8 * P, tid, rot);
       if (!C::SLIM && !C::LEAN && use_q2) glds_copy<BS, C::G16>(a.qb2 + (size_t)e * 4 * P, s_q2, 8 * P, tid, rot);
-      if (m.etsrc && !a.tcontig) {
+      if (tsl) {
         // processor-face halo: each face's neighbour trace from its own slot (the receive
-        // slot of a processor face); the slot ids are uniform, scalar loads
-#pragma unroll
-        for (int lf = 0; lf < 4; lf++)
-          glds_copy<BS, C::G16>(a.trace_in + (size_t)m.etsrc[4 * e + lf] * 8 * NGL, s_tr + lf * 8 * NGL, 2 * 8 * NGL, tid, rot);
+        // slot of a processor face)
+        glds_copy<BS, C::G16>(a.trace_in + (size_t)ts.x * 8 * NGL, s_tr + 0 * 8 * NGL, 2 * 8 * NGL, tid, rot);
+        glds_copy<BS, C::G16>(a.trace_in + (size_t)ts.y * 8 * NGL, s_tr + 1 * 8 * NGL, 2 * 8 * NGL, tid, rot);
+        glds_copy<BS, C::G16>(a.trace_in + (size_t)ts.z * 8 * NGL, s_tr + 2 * 8 * NGL, 2 * 8 * NGL, tid, rot);
+        glds_copy<BS, C::G16>(a.trace_in + (size_t)ts.w * 8 * NGL, s_tr + 3 * 8 * NGL, 2 * 8 * NGL, tid, rot);
       } else {
         glds_copy<BS, C::G16>(a.trace_in + (size_t)e * 32 * NGL, s_tr, 2 * 32 * NGL, tid, rot);
       }
