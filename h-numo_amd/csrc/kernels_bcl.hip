@@ -58,6 +58,67 @@ __device__ __forceinline__ void load_basis(const DevMesh &m, double *s_psiq, dou
   }
 }
 
+// Gathered staging (the element kernels' load phases): every gather's loads are issued before any
+// of them is stored to LDS, so a kernel's inputs arrive in one memory round trip (a strided
+// load-then-store loop waits for its own loads before the next loop's go out: mom_elem's sixteen
+// such loops were sixteen round trips, ~14.5k clocks of its ~70k at dg25).  N: the most entries
+// (MAXL layers), n >= 1: this call's; ld(t) returns entry t, st(t, v) stores it.  Within a wave the
+// loads are unconditional (a lane past n loads entry n-1 again, unused): loads under a lane
+// branch leave their registers to be merged at the join, which waits for them there.
+template <class T, int N, int BS>
+struct Gather {
+  static constexpr int NI = (N + BS - 1) / BS;
+  T v[NI];
+  template <class LoadF>
+  __device__ __forceinline__ void load(int tid, int n, LoadF &&ld) {
+    const int w0 = __builtin_amdgcn_readfirstlane(tid & ~63);  // (the wave's first thread)
+#pragma unroll
+    for (int j = 0; j < NI; j++) {
+      const int t = tid + j * BS;
+      if (w0 + j * BS < n) v[j] = ld(t < n ? t : n - 1);  // (a wave past n issues nothing)
+    }
+  }
+  template <class StoreF>
+  __device__ __forceinline__ void store(int tid, int n, StoreF &&st) const {
+#pragma unroll
+    for (int j = 0; j < NI; j++) {
+      const int t = tid + j * BS;
+      if (t < n) st(t, v[j]);
+    }
+  }
+  // st(t, j): entry t is v[j] (for stores that combine two gathers of the same layout)
+  template <class StoreF>
+  __device__ __forceinline__ void store_j(int tid, int n, StoreF &&st) const {
+#pragma unroll
+    for (int j = 0; j < NI; j++) {
+      const int t = tid + j * BS;
+      if (t < n) st(t, j);
+    }
+  }
+};
+// the basis tables (psiq, dpsiq, dpsi, psi: contiguous in m.basis) as one gather
+template <int NGL, int NQ, int BS>
+struct BasisGather {
+  static constexpr int NB = 2 * NGL * NQ + 2 * NGL * NGL;
+  Gather<double, NB, BS> g;
+  __device__ __forceinline__ void load(const DevMesh &m, int tid) {
+    g.load(tid, NB, [&](int t) { return m.basis[t]; });
+  }
+  __device__ __forceinline__ void store(double *s_psiq, double *s_dpsiq, double *s_dpsi, double *s_psi, int tid) const {
+    g.store(tid, NB, [&](int t, double v) {
+      constexpr int A = NGL * NQ, P = NGL * NGL;
+      if (t < A)
+        s_psiq[t] = v;
+      else if (t < 2 * A)
+        s_dpsiq[t - A] = v;
+      else if (t < 2 * A + P)
+        s_dpsi[t - 2 * A] = v;
+      else
+        s_psi[t - 2 * A - P] = v;
+    });
+  }
+};
+
 // Reference-order term definitions (Tensor_product.F90:71-114); see kernels_btp.hip.
 #define PSIH(n, m, iq, jq) (s_psiq[(n)*NQ + (iq)] * s_psiq[(m)*NQ + (jq)])
 #define HE(n, m, iq, jq) (s_dpsiq[(n)*NQ + (iq)] * s_psiq[(m)*NQ + (jq)])
@@ -419,37 +480,69 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   __shared__ double s_g[MAXL][4][P];
   __shared__ double s_qfF[4][MAXL][6 * NGL];  // (qf) the four faces' qf blocks (averaged)
   __shared__ int s_map[4 * NGL], s_face[4], s_side[4], s_bc[4];
-  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
+  // every load of the phase first (Gather), then the LDS stores (and the averaged copies): the
+  // element's face ids, sides and boundary codes (scalar loads) and the element-major inputs, then
+  // the face-indexed qf blocks
+  int fr[12];  // face ids, sides, boundary codes of the four faces
+#pragma unroll
+  for (int x = 0; x < 4; x++) {
+    fr[x] = m.efaces[e * 4 + x];
+    fr[4 + x] = m.eside[e * 4 + x];
+    fr[8 + x] = m.ebc[e * 4 + x];
+  }
+  auto sel4 = [&](const int *a, int lf) { return lf == 0 ? a[0] : (lf == 1 ? a[1] : (lf == 2 ? a[2] : a[3])); };
+  BasisGather<NGL, NQ, BS> g_bas;
+  g_bas.load(m, tid);
+  Gather<int, 4 * NGL, BS> g_map;
+  if (qf) g_map.load(tid, 4 * NGL, [&](int t) { return m.efmap[e * 4 * NGL + t]; });
+  auto qidx = [&](int t) { return (size_t)(t / (3 * P)) * 3 * npoin + (size_t)e * 3 * P + t % (3 * P); };
+  Gather<double, MAXL * 3 * P, BS> g_q, g_qa;
+  g_q.load(tid, L * 3 * P, [&](int t) { return qp[qidx(t)]; });
+  if (qp_avg) g_qa.load(tid, L * 3 * P, [&](int t) { return qp_avg[qidx(t)]; });
+  Gather<double, 4 * P, BS> g_nm;
+  g_nm.load(tid, 4 * P, [&](int t) { return m.nstat[(NS_EX + t / P) * (size_t)npoin + (size_t)e * P + t % P]; });
+  auto fidx = [&](int t, int &lf, int &rr) {
+    lf = t / (L * 6 * NGL);
+    const int r = t % (L * 6 * NGL), k = r / (6 * NGL);
+    rr = r % (6 * NGL);
+    return ((size_t)k * F + sel4(fr, lf)) * NGL * 6 + rr;
+  };
+  Gather<double, 4 * MAXL * 6 * NGL, BS> g_qf, g_qfa;
+  if (qf) {
+    int lf, rr;
+    g_qf.load(tid, 4 * L * 6 * NGL, [&](int t) { return qf[fidx(t, lf, rr)]; });
+    if (qf_avg) g_qfa.load(tid, 4 * L * 6 * NGL, [&](int t) { return qf_avg[fidx(t, lf, rr)]; });
+  }
+  // the stores
+  g_bas.store(s_psiq, s_dpsiq, s_dpsi, s_psi, tid);
   if (qf) {
     if (tid < 4) {
-      s_face[tid] = m.efaces[e * 4 + tid];
-      s_side[tid] = m.eside[e * 4 + tid];
-      s_bc[tid] = m.ebc[e * 4 + tid];
+      s_face[tid] = sel4(fr, tid);
+      s_side[tid] = sel4(fr + 4, tid);
+      s_bc[tid] = sel4(fr + 8, tid);
     }
-    for (int t = tid; t < 4 * NGL; t += BS) s_map[t] = m.efmap[e * 4 * NGL + t];
-    for (int t = tid; t < 4 * L * 6 * NGL; t += BS) {
-      const int lf = t / (L * 6 * NGL), r = t % (L * 6 * NGL), k = r / (6 * NGL), rr = r % (6 * NGL);
-      const size_t i = ((size_t)k * F + m.efaces[e * 4 + lf]) * NGL * 6 + rr;
-      double v = qf[i];
+    g_map.store(tid, 4 * NGL, [&](int t, int v) { s_map[t] = v; });
+    g_qf.store_j(tid, 4 * L * 6 * NGL, [&](int t, int j) {
+      int lf, rr;
+      const size_t i = fidx(t, lf, rr);
+      double v = g_qf.v[j];
       if (qf_avg) {
-        v = 0.5 * (qf_avg[i] + v);
-        if ((rr / 3) % 2 == m.eside[e * 4 + lf] || m.ebc[e * 4 + lf] <= 0) qf_out[i] = v;
+        v = 0.5 * (g_qfa.v[j] + v);
+        if ((rr / 3) % 2 == sel4(fr + 4, lf) || sel4(fr + 8, lf) <= 0) qf_out[i] = v;
       }
-      s_qfF[lf][k][rr] = v;
-    }
+      s_qfF[lf][(t % (L * 6 * NGL)) / (6 * NGL)][rr] = v;
+    });
   }
-  for (int t = tid; t < L * 3 * P; t += BS) {
-    int k = t / (3 * P), r = t % (3 * P);
-    const size_t i = (size_t)k * 3 * npoin + (size_t)e * 3 * P + r;
-    double v = qp[i];
+  g_q.store_j(tid, L * 3 * P, [&](int t, int j) {
+    const int k = t / (3 * P), r = t % (3 * P);
+    double v = g_q.v[j];
     if (qp_avg) {
-      v = 0.5 * (v + qp_avg[i]);
-      qp[i] = v;
+      v = 0.5 * (v + g_qa.v[j]);
+      qp[qidx(t)] = v;
     }
     s_q[k][r % 3][r / 3] = v;
-  }
-  for (int t = tid; t < 4 * P; t += BS)
-    s_nm[t / P][t % P] = m.nstat[(NS_EX + t / P) * (size_t)npoin + (size_t)e * P + t % P];
+  });
+  g_nm.store(tid, 4 * P, [&](int t, double v) { s_nm[t / P][t % P] = v; });
   __syncthreads();
   // GSPLIT: quad-point tasks on threads [0, Q), the nodal gradient tasks on the threads past them
   constexpr bool GSPLIT = BS - Q >= 128;
@@ -693,17 +786,31 @@ __global__ void __launch_bounds__(64)
 // create_layer_mass_flux at (face f, quad point iq) from the face's qf block staged as s_qf
 // [MAXL][6*NGL] (stage_qf): fm[k] = nx*flux_edge_u + ny*flux_edge_v per layer and the layer sums
 // (su, sv) -- one restatement for mass_flux_face_kernel and mass_elem_kernel's fused faces
+// (its global inputs at (f, iq): the normal and the face averages, MFIn -- loaded ahead by the
+// caller, mass_elem_kernel with its other loads)
+struct MFIn {
+  double nx, ny, qbl0, qbr0, qbl1, qbr1, qbl2, qbr2;
+};
+template <int NQ>
+__device__ __forceinline__ MFIn mass_flux_in(const DevMesh &m, const double *facc, int f, int sa, int iq) {
+  const size_t FQ = (size_t)m.nface * NQ, fq = (size_t)f * NQ + iq;
+  MFIn x;
+  x.nx = m.fstat[FS_NX * FQ + fq];
+  x.ny = m.fstat[FS_NY * FQ + fq];
+  x.qbl0 = facc[FACC_I(FA_OPEL, sa, iq)];
+  x.qbr0 = facc[FACC_I(FA_OPER, sa, iq)];
+  x.qbl1 = facc[FACC_I(FA_UL, sa, iq)];
+  x.qbr1 = facc[FACC_I(FA_UR, sa, iq)];
+  x.qbl2 = facc[FACC_I(FA_VL, sa, iq)];
+  x.qbr2 = facc[FACC_I(FA_VR, sa, iq)];
+  return x;
+}
 template <int NGL, int NQ>
 __device__ __forceinline__ void mass_flux_at(const DevMesh &m, const double (*s_qf)[6 * NGL], const double *s_psiq,
-                                              const double *facc, int f, int iq, double fm[MAXL], double &su,
-                                              double &sv) {
-  const int F = m.nface, L = m.L;
-  const size_t FQ = (size_t)F * NQ, fq = (size_t)f * NQ + iq;
-  double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
-  const int sa = m.fslotA[f];
-  double qbl0 = facc[FACC_I(FA_OPEL, sa, iq)], qbr0 = facc[FACC_I(FA_OPER, sa, iq)];
-  double qbl1 = facc[FACC_I(FA_UL, sa, iq)], qbr1 = facc[FACC_I(FA_UR, sa, iq)];
-  double qbl2 = facc[FACC_I(FA_VL, sa, iq)], qbr2 = facc[FACC_I(FA_VR, sa, iq)];
+                                              const MFIn &x, int iq, double fm[MAXL], double &su, double &sv) {
+  const int L = m.L;
+  const double nxl = x.nx, nyl = x.ny, qbl0 = x.qbl0, qbr0 = x.qbr0, qbl1 = x.qbl1, qbr1 = x.qbr1, qbl2 = x.qbl2,
+               qbr2 = x.qbr2;
   su = 0.0;
   sv = 0.0;
 #pragma unroll
@@ -742,7 +849,7 @@ __global__ void __launch_bounds__(64)
   if (tid < NQ) {
     const size_t fq = (size_t)f * NQ + tid;
     double fm[MAXL], su, sv;
-    mass_flux_at<NGL, NQ>(m, s_qf, s_psiq, facc, f, tid, fm, su, sv);
+    mass_flux_at<NGL, NQ>(m, s_qf, s_psiq, mass_flux_in<NQ>(m, facc, f, m.fslotA[f], tid), tid, fm, su, sv);
     for (int k = 0; k < L; k++) fmass[(size_t)k * FQ + fq] = fm[k];
     slmf_face[0 * FQ + fq] = su;
     slmf_face[1 * FQ + fq] = sv;
@@ -913,40 +1020,87 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   __shared__ double s_tb[QS::SIZE];                    // quad-sum term buffers
   __shared__ double s_qfF[4][MAXL][6 * NGL];           // (qf) the four faces' qf blocks
   __shared__ int s_map[4 * NGL], s_face[4], s_side[4];
-  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
-  if (tid < 4) {
-    s_face[tid] = m.efaces[e * 4 + tid];
-    s_side[tid] = m.eside[e * 4 + tid];
-  }
-  stage_face_quads<NQ>(s_fw, m.fstat + FS_W * (size_t)F * NQ, 0, 1, m.efaces + e * 4, tid, BS);
-  if (qf) {
-    for (int t = tid; t < 4 * L * 6 * NGL; t += BS) {
-      const int lf = t / (L * 6 * NGL), r = t % (L * 6 * NGL), k = r / (6 * NGL), rr = r % (6 * NGL);
-      s_qfF[lf][k][rr] = qf[((size_t)k * F + m.efaces[e * 4 + lf]) * NGL * 6 + rr];
-    }
-  } else {
-    stage_face_quads<NQ>(&s_fx[0][0], fmass, (size_t)F * NQ, L, m.efaces + e * 4, tid, BS);
-  }
-  for (int t = tid; t < 4 * NGL; t += BS) s_map[t] = m.efmap[e * 4 * NGL + t];
-  for (int t = tid; t < L * 3 * P; t += BS) {
-    int k = t / (3 * P), r = t % (3 * P);
-    s_q[k][r % 3][r / 3] = qp[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
-  }
-  for (int t = tid; t < 5 * Q; t += BS) {
+  // every load of the phase first (Gather), then the LDS stores: the face ids (scalar loads) and
+  // the element-major inputs in one round, the face-indexed ones (qf blocks or fluxes, the face
+  // tasks' averages) in a second
+  const int fid0 = m.efaces[e * 4], fid1 = m.efaces[e * 4 + 1], fid2 = m.efaces[e * 4 + 2], fid3 = m.efaces[e * 4 + 3];
+  auto fid = [&](int lf) { return lf == 0 ? fid0 : (lf == 1 ? fid1 : (lf == 2 ? fid2 : fid3)); };
+  // the face task's accumulator slot first (round 2 waits for it, and vmcnt counts in order)
+  constexpr int FT0 = ((Q + 63) / 64) * 64;
+  // (this thread's face task w = FT0 + ft is w = tid or tid + BS: at most one, 4*NQ <= BS)
+  static_assert(Q <= BS && 4 * NQ <= BS && FT0 + 4 * NQ <= 2 * BS, "at most one phase-1 task of each kind per thread");
+  const int ft = (tid - FT0 + BS) % BS, ft_lf = ft < 4 * NQ ? ft / NQ : 0, ft_iq = ft < 4 * NQ ? ft % NQ : 0;
+  const int ft_sa = qf ? m.fslotA[fid(ft_lf)] : 0;
+  BasisGather<NGL, NQ, BS> g_bas;
+  g_bas.load(m, tid);
+  Gather<int, 4, BS> g_side;
+  g_side.load(tid, 4, [&](int t) { return m.eside[e * 4 + t]; });
+  Gather<double, 4 * NQ, BS> g_fw;  // (efstat's EF_W: fstat's FS_W of the element's faces)
+  g_fw.load(tid, 4 * NQ, [&](int t) { return m.efstat[((size_t)e * 4 + t / NQ) * EFBLK(NGL, NQ) + EF_W * NQ + t % NQ]; });
+  Gather<int, 4 * NGL, BS> g_map;
+  g_map.load(tid, 4 * NGL, [&](int t) { return m.efmap[e * 4 * NGL + t]; });
+  Gather<double, MAXL * 3 * P, BS> g_q;
+  g_q.load(tid, L * 3 * P, [&](int t) { return qp[(size_t)(t / (3 * P)) * 3 * npoin + (size_t)e * 3 * P + t % (3 * P)]; });
+  Gather<double, 5 * Q, BS> g_qm;
+  g_qm.load(tid, 5 * Q, [&](int t) {
     const int c = t / Q;
-    s_qm[c][t % Q] = m.qstat[(c < 4 ? QS_EX + c : QS_W) * (size_t)npq + (size_t)e * Q + t % Q];
+    return m.qstat[(c < 4 ? QS_EX + c : QS_W) * (size_t)npq + (size_t)e * Q + t % Q];
+  });
+  // phase 1: the quad task's averages (quad point tid) and, with qf, the face task's inputs
+  // (thread FT0 + lf*NQ + iq); phase 3: pb' of node tid
+  double r_qb[3];
+  {
+    const int q = tid < Q ? tid : Q - 1;
+    r_qb[0] = qacc[QACC_I(QA_OPE, e, q)];
+    r_qb[1] = qacc[QACC_I(QA_UB, e, q)];
+    r_qb[2] = qacc[QACC_I(QA_VB, e, q)];
+  }
+  const double r_pb = m.nstat[NS_PB * (size_t)npoin + (size_t)e * P + (tid < P ? tid : P - 1)];
+  // (round 2) the face-indexed loads
+  Gather<double, 4 * MAXL * 6 * NGL, BS> g_qfF;
+  Gather<double, MAXL * 4 * NQ, BS> g_fx;
+  MFIn r_mf;
+  if (qf) {
+    g_qfF.load(tid, 4 * L * 6 * NGL, [&](int t) {
+      const int lf = t / (L * 6 * NGL), r = t % (L * 6 * NGL), k = r / (6 * NGL), rr = r % (6 * NGL);
+      return qf[((size_t)k * F + fid(lf)) * NGL * 6 + rr];
+    });
+    r_mf = mass_flux_in<NQ>(m, facc, fid(ft_lf), ft_sa, ft_iq);
+  } else {
+    g_fx.load(tid, L * 4 * NQ, [&](int t) {
+      const int c = t / (4 * NQ), lf = (t / NQ) % 4, iq = t % NQ;
+      return fmass[c * (size_t)F * NQ + (size_t)fid(lf) * NQ + iq];
+    });
+  }
+  // the stores
+  g_bas.store(s_psiq, s_dpsiq, s_dpsi, s_psi, tid);
+  if (tid < 4) s_face[tid] = fid(tid);
+  g_side.store(tid, 4, [&](int t, int v) { s_side[t] = v; });
+  g_fw.store(tid, 4 * NQ, [&](int t, double v) { s_fw[t] = v; });
+  g_map.store(tid, 4 * NGL, [&](int t, int v) { s_map[t] = v; });
+  g_q.store(tid, L * 3 * P, [&](int t, double v) {
+    const int k = t / (3 * P), r = t % (3 * P);
+    s_q[k][r % 3][r / 3] = v;
+  });
+  g_qm.store(tid, 5 * Q, [&](int t, double v) { s_qm[t / Q][t % Q] = v; });
+  if (qf) {
+    g_qfF.store(tid, 4 * L * 6 * NGL, [&](int t, double v) {
+      const int lf = t / (L * 6 * NGL), r = t % (L * 6 * NGL), k = r / (6 * NGL), rr = r % (6 * NGL);
+      s_qfF[lf][k][rr] = v;
+    });
+  } else {
+    g_fx.store(tid, L * 4 * NQ, [&](int t, double v) { (&s_fx[0][0])[t] = v; });
   }
   __syncthreads();
   if (*m.runflag & RUN_ABORT) return;  // (a persistent sub-cycle of this run did no work: DevMesh)
   BCL_MARK(0, 1)
   // quad points [0, Q); with qf, the four faces' flux tasks from the next whole wave on
-  constexpr int FT0 = ((Q + 63) / 64) * 64;
   for (int w = tid; w < (qf ? FT0 + 4 * NQ : Q); w += BS) {
     if (w >= Q) {
       if (w < FT0) continue;
       const int lf = (w - FT0) / NQ, iq = (w - FT0) % NQ, f = s_face[lf];
       double fm[MAXL], su, sv;
-      mass_flux_at<NGL, NQ>(m, s_qfF[lf], s_psiq, facc, f, iq, fm, su, sv);
+      mass_flux_at<NGL, NQ>(m, s_qfF[lf], s_psiq, r_mf, iq, fm, su, sv);
 #pragma unroll
       for (int k = 0; k < MAXL; k++)
         if (k < L) s_fx[k][lf * NQ + iq] = fm[k];
@@ -960,8 +1114,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     const int q = w;
     const int iq = q % NQ, jq = q / NQ;
     const size_t Iq = (size_t)e * Q + q;
-    double qb0 = qacc[QACC_I(QA_OPE, e, q)], qb1 = qacc[QACC_I(QA_UB, e, q)],
-           qb2 = qacc[QACC_I(QA_VB, e, q)];
+    const double qb0 = r_qb[0], qb1 = r_qb[1], qb2 = r_qb[2];
     double pa[NGL], pb[NGL];
 #pragma unroll
     for (int n = 0; n < NGL; n++) {
@@ -1018,7 +1171,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     const size_t I = (size_t)e * P + p;
     double sum = 0.0;
     for (int k = 0; k < L; k++) sum = sum + s_adv[k][p];
-    double ope = sum / m.nstat[NS_PB * (size_t)npoin + I];
+    double ope = sum / r_pb;  // (p == tid: P <= BS)
     for (int k = 0; k < L; k++) dpp[(size_t)k * npoin + I] = s_adv[k][p] / ope;
   }
   BCL_MARK(0, 5) BCL_WALL(0, 7)
@@ -1051,43 +1204,127 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   __shared__ double s_tb[QS::SIZE];                    // quad-sum term buffers
   __shared__ double s_dnF[4][MAXL][2][NGL];            // (facc) dp' at the four faces' left | right nodes
   __shared__ int s_map[4 * NGL], s_face[4], s_side[4], s_bc[4];
-  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
-  if (tid < 4) {
-    s_face[tid] = m.efaces[e * 4 + tid];
-    s_side[tid] = m.eside[e * 4 + tid];
-    s_bc[tid] = m.ebc[e * 4 + tid];
-  }
-  stage_face_quads<NQ>(s_fw, m.fstat + FS_W * (size_t)F * NQ, 0, 1, m.efaces + e * 4, tid, BS);
+  // every load of the phase first (Gather), then the LDS stores: the face ids (scalar loads), then
+  // the face-indexed tables (node ids, accumulator slots) and the element-major inputs, then the
+  // face-indexed data
+  const int fid0 = m.efaces[e * 4], fid1 = m.efaces[e * 4 + 1], fid2 = m.efaces[e * 4 + 2], fid3 = m.efaces[e * 4 + 3];
+  auto fid = [&](int lf) { return lf == 0 ? fid0 : (lf == 1 ? fid1 : (lf == 2 ? fid2 : fid3)); };
+  constexpr int FT0 = ((Q + 63) / 64) * 64;
+  // (this thread's face task w = FT0 + ft is w = tid or tid + BS: at most one, 4*NQ <= BS)
+  static_assert(Q <= BS && 4 * NQ <= BS && FT0 + 4 * NQ <= 2 * BS, "at most one phase-1 task of each kind per thread");
+  const int ft = (tid - FT0 + BS) % BS, ft_lf = ft < 4 * NQ ? ft / NQ : 0, ft_iq = ft < 4 * NQ ? ft % NQ : 0;
+  const int ft_f = fid(ft_lf);
+  const int ft_sa = facc ? m.fslotA[ft_f] : 0;
+  // (facc) dp' at the four faces' left | right nodes, entry t = (lf, k, sd, n): the node ids
+  // (fnodeL / fnodeR, -1 on a side without an element) first, the values after them
+  constexpr int NDI = (4 * MAXL * 2 * NGL + BS - 1) / BS;
+  const int nd = 4 * L * 2 * NGL;
+  auto dnf_idx = [&](int t, int &lf, int &k, int &sd, int &n) {
+    lf = t / (L * 2 * NGL);
+    const int r = t % (L * 2 * NGL);
+    k = r / (2 * NGL);
+    sd = (r / NGL) % 2;
+    n = r % NGL;
+  };
+  int dn_id[NDI];
+  double dn_v[NDI];
   if (facc) {
-    for (int t = tid; t < 4 * L * 2 * NGL; t += BS) {
-      const int lf = t / (L * 2 * NGL), r = t % (L * 2 * NGL), k = r / (2 * NGL), sd = (r / NGL) % 2, n = r % NGL;
-      const int f = m.efaces[e * 4 + lf];
-      if (sd == 1 && m.fer[f] <= 0) continue;
-      s_dnF[lf][k][sd][n] = dpp[(size_t)k * npoin + (sd ? m.fnodeR : m.fnodeL)[(size_t)f * NGL + n]];
+#pragma unroll
+    for (int j = 0; j < NDI; j++) {
+      const int t = tid + j * BS;
+      int lf, k, sd, n;
+      dnf_idx(t < nd ? t : nd - 1, lf, k, sd, n);
+      dn_id[j] = (sd ? m.fnodeR : m.fnodeL)[(size_t)fid(lf) * NGL + n];
+    }
+  }
+  BasisGather<NGL, NQ, BS> g_bas;
+  g_bas.load(m, tid);
+  Gather<int, 4, BS> g_side, g_bc;
+  g_side.load(tid, 4, [&](int t) { return m.eside[e * 4 + t]; });
+  g_bc.load(tid, 4, [&](int t) { return m.ebc[e * 4 + t]; });
+  Gather<double, 4 * NQ, BS> g_fw;  // (efstat's EF_W: fstat's FS_W of the element's faces)
+  g_fw.load(tid, 4 * NQ, [&](int t) { return m.efstat[((size_t)e * 4 + t / NQ) * EFBLK(NGL, NQ) + EF_W * NQ + t % NQ]; });
+  Gather<int, 4 * NGL, BS> g_map;
+  g_map.load(tid, 4 * NGL, [&](int t) { return m.efmap[e * 4 * NGL + t]; });
+  Gather<double, MAXL * P, BS> g_d;
+  g_d.load(tid, L * P, [&](int t) { return dpp[(size_t)(t / P) * npoin + (size_t)e * P + t % P]; });
+  Gather<double, 5 * Q, BS> g_qm;
+  g_qm.load(tid, 5 * Q, [&](int t) {
+    const int c = t / Q;
+    return m.qstat[(c < 4 ? QS_EX + c : QS_W) * (size_t)npq + (size_t)e * Q + t % Q];
+  });
+  // phase 1: the quad task's inputs (quad point tid) and, with facc, the face task's; the
+  // finalize: pb' of node tid
+  double r_pbq, r_dx0, r_dx1, r_dy0, r_dy1;
+  {
+    const size_t Iq = (size_t)e * Q + (tid < Q ? tid : Q - 1);
+    r_pbq = m.qstat[QS_PB * (size_t)npq + Iq];
+    r_dx0 = qacc[QACC_I(QA_MFX, e, 0) + (Iq - (size_t)e * Q)];
+    r_dx1 = slmf[0 * (size_t)npq + Iq];
+    r_dy0 = qacc[QACC_I(QA_MFY, e, 0) + (Iq - (size_t)e * Q)];
+    r_dy1 = slmf[1 * (size_t)npq + Iq];
+  }
+  const double r_pbn = m.nstat[NS_PB * (size_t)npoin + (size_t)e * P + (tid < P ? tid : P - 1)];
+  double f_nx = 0.0, f_ny = 0.0, f_s1 = 0.0, f_s2 = 0.0, f_pbl = 0.0, f_pbr = 0.0, f_a1 = 0.0, f_a2 = 0.0;
+  if (facc) {
+    const size_t FQ = (size_t)F * NQ, fq = (size_t)ft_f * NQ + ft_iq;
+    f_nx = m.fstat[FS_NX * FQ + fq];
+    f_ny = m.fstat[FS_NY * FQ + fq];
+    f_s1 = slmf_face[0 * FQ + fq];
+    f_s2 = slmf_face[1 * FQ + fq];
+    f_pbl = m.fstat[FS_PBL * FQ + fq];
+    f_pbr = m.fstat[FS_PBR * FQ + fq];
+    f_a1 = facc[FACC_I(FA_MFX, ft_sa, ft_iq)];
+    f_a2 = facc[FACC_I(FA_MFY, ft_sa, ft_iq)];
+  }
+  // the face-indexed data: dp' at the faces' nodes, or the faces' fluxes
+  Gather<double, MAXL * 4 * NQ, BS> g_fx;
+  if (facc) {
+#pragma unroll
+    for (int j = 0; j < NDI; j++) {
+      const int t = tid + j * BS;
+      int lf, k, sd, n;
+      dnf_idx(t < nd ? t : nd - 1, lf, k, sd, n);
+      dn_v[j] = dpp[(size_t)k * npoin + (dn_id[j] >= 0 ? dn_id[j] : 0)];
     }
   } else {
-    stage_face_quads<NQ>(&s_fx[0][0], fcons, (size_t)F * NQ, L, m.efaces + e * 4, tid, BS);
+    g_fx.load(tid, L * 4 * NQ, [&](int t) {
+      const int c = t / (4 * NQ), lf = (t / NQ) % 4, iq = t % NQ;
+      return fcons[c * (size_t)F * NQ + (size_t)fid(lf) * NQ + iq];
+    });
   }
-  for (int t = tid; t < 4 * NGL; t += BS) s_map[t] = m.efmap[e * 4 * NGL + t];
-  for (int t = tid; t < L * P; t += BS) s_d[t / P][t % P] = dpp[(size_t)(t / P) * npoin + (size_t)e * P + t % P];
-  for (int t = tid; t < 5 * Q; t += BS) {
-    const int c = t / Q;
-    s_qm[c][t % Q] = m.qstat[(c < 4 ? QS_EX + c : QS_W) * (size_t)npq + (size_t)e * Q + t % Q];
+  // the stores
+  g_bas.store(s_psiq, s_dpsiq, s_dpsi, s_psi, tid);
+  if (tid < 4) s_face[tid] = fid(tid);
+  g_side.store(tid, 4, [&](int t, int v) { s_side[t] = v; });
+  g_bc.store(tid, 4, [&](int t, int v) { s_bc[t] = v; });
+  g_fw.store(tid, 4 * NQ, [&](int t, double v) { s_fw[t] = v; });
+  g_map.store(tid, 4 * NGL, [&](int t, int v) { s_map[t] = v; });
+  g_d.store(tid, L * P, [&](int t, double v) { s_d[t / P][t % P] = v; });
+  g_qm.store(tid, 5 * Q, [&](int t, double v) { s_qm[t / Q][t % Q] = v; });
+  if (facc) {
+#pragma unroll
+    for (int j = 0; j < NDI; j++) {
+      const int t = tid + j * BS;
+      int lf, k, sd, n;
+      dnf_idx(t, lf, k, sd, n);
+      if (t < nd && dn_id[j] >= 0) s_dnF[lf][k][sd][n] = dn_v[j];  // (no right element: never read)
+    }
+  } else {
+    g_fx.store(tid, L * 4 * NQ, [&](int t, double v) { (&s_fx[0][0])[t] = v; });
   }
   __syncthreads();
   if (*m.runflag & RUN_ABORT) return;  // (a persistent sub-cycle of this run did no work: DevMesh)
   BCL_MARK(1, 1)
   // quad points [0, Q); with facc, the four faces' flux tasks from the next whole wave on
-  constexpr int FT0 = ((Q + 63) / 64) * 64;
   for (int w = tid; w < (facc ? FT0 + 4 * NQ : Q); w += BS) {
     if (w >= Q) {
       if (w < FT0) continue;
-      const int lf = (w - FT0) / NQ, iq = (w - FT0) % NQ, f = s_face[lf], er = s_bc[lf];
-      const size_t FQ = (size_t)F * NQ, fq = (size_t)f * NQ + iq;
-      const double nxl = m.fstat[FS_NX * FQ + fq], nyl = m.fstat[FS_NY * FQ + fq];
-      const double d1 = facc[FACC_I(FA_MFX, m.fslotA[f], iq)] - slmf_face[0 * FQ + fq];
-      const double d2 = facc[FACC_I(FA_MFY, m.fslotA[f], iq)] - slmf_face[1 * FQ + fq];
-      const double pbl = m.fstat[FS_PBL * FQ + fq], pbr = m.fstat[FS_PBR * FQ + fq];
+      const int lf = (w - FT0) / NQ, iq = (w - FT0) % NQ, er = s_bc[lf];  // (== ft_lf, ft_iq)
+      const double nxl = f_nx, nyl = f_ny;
+      const double d1 = f_a1 - f_s1;
+      const double d2 = f_a2 - f_s2;
+      const double pbl = f_pbl, pbr = f_pbr;
 #pragma unroll
       for (int k = 0; k < MAXL; k++) {
         if (k >= L) break;
@@ -1100,10 +1337,9 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     }
     const int q = w;
     const int iq = q % NQ, jq = q / NQ;
-    const size_t Iq = (size_t)e * Q + q;
-    double pb = m.qstat[QS_PB * (size_t)npq + Iq];
-    double dx = qacc[QACC_I(QA_MFX, e, q)] - slmf[0 * (size_t)npq + Iq];
-    double dy = qacc[QACC_I(QA_MFY, e, q)] - slmf[1 * (size_t)npq + Iq];
+    double pb = r_pbq;
+    double dx = r_dx0 - r_dx1;
+    double dy = r_dy0 - r_dy1;
     double pa[NGL], pbq[NGL];
 #pragma unroll
     for (int n = 0; n < NGL; n++) {
@@ -1152,7 +1388,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     const size_t I = (size_t)e * P + p;
     double sum = 0.0;
     for (int k = 0; k < L; k++) sum = sum + s_new[k][p];
-    double ope = sum / m.nstat[NS_PB * (size_t)npoin + I];
+    double ope = sum / r_pbn;  // (p == tid: P <= BS)
     double v[MAXL][3];
     for (int k = 0; k < L; k++) {
       v[k][0] = s_new[k][p] / ope;
@@ -1195,31 +1431,49 @@ __global__ void __launch_bounds__(64)
   __shared__ double s_gd[MAXL][10][NGL];          // graduv_dpp_face per layer
   __shared__ double s_fs[4][NQ];                  // nx, ny, zbot left, zbot right at the quad points
   __shared__ double s_fn[3][NGL];                 // nx, ny, w at the face nodes
-  for (int t = tid; t < NGL * NQ; t += 64) s_psiq[t] = m.basis[t];
-  for (int t = tid; t < NGL * NGL; t += 64) s_psi[t] = m.basis[2 * NGL * NQ + NGL * NGL + t];
-  for (int t = tid; t < L * 6 * NGL; t += 64) {
-    const int k = t / (6 * NGL), r = t % (6 * NGL);
-    const size_t i = ((size_t)k * F + f) * NGL * 6 + r;
-    double v = qf[i];
-    if (qf_avg0 && r % 3 == 0) v = 0.5 * (qf_avg0[i] + v);
-    s_qf[k][r] = v;
-  }
-  for (int t = tid; t < FA_N * NQ; t += 64) s_fa[t] = facc[FACC_I(0, slot, 0) + t];
-  for (int t = tid; t < 8 * NGL; t += 64) s_gf[t] = gfacc[GFACC_I(0, slot, 0) + t];
-  for (int t = tid; t < L * 10 * NGL; t += 64) {
+  // (Gather: every load, then the stores)
+  Gather<double, NGL * NQ, 64> g_psiq;
+  g_psiq.load(tid, NGL * NQ, [&](int t) { return m.basis[t]; });
+  Gather<double, NGL * NGL, 64> g_psi;
+  g_psi.load(tid, NGL * NGL, [&](int t) { return m.basis[2 * NGL * NQ + NGL * NGL + t]; });
+  auto qf_i = [&](int t) { return ((size_t)(t / (6 * NGL)) * F + f) * NGL * 6 + t % (6 * NGL); };
+  Gather<double, MAXL * 6 * NGL, 64> g_qf, g_qfa;
+  g_qf.load(tid, L * 6 * NGL, [&](int t) { return qf[qf_i(t)]; });
+  if (qf_avg0) g_qfa.load(tid, L * 6 * NGL, [&](int t) { return qf_avg0[qf_i(t)]; });
+  Gather<double, FA_N * NQ, 64> g_fa;
+  g_fa.load(tid, FA_N * NQ, [&](int t) { return facc[FACC_I(0, slot, 0) + t]; });
+  Gather<double, 8 * NGL, 64> g_gf;
+  g_gf.load(tid, 8 * NGL, [&](int t) { return gfacc[GFACC_I(0, slot, 0) + t]; });
+  Gather<double, MAXL * 10 * NGL, 64> g_gd;
+  g_gd.load(tid, L * 10 * NGL, [&](int t) {
     const int k = t / (10 * NGL), c = (t / NGL) % 10, n = t % NGL;
-    s_gd[k][c][n] = gdpp_face[((size_t)k * 10 + c) * FN + (size_t)f * NGL + n];
-  }
-  if (tid < 4 * NQ) {
-    const int c = tid / NQ, iq = tid % NQ;
-    const int fld[4] = {FS_NX, FS_NY, FS_ZBL, FS_ZBR};
-    s_fs[c][iq] = m.fstat[fld[c] * FQ + (size_t)f * NQ + iq];
-  }
-  if (tid < 3 * NGL) {
-    const int c = tid / NGL, n = tid % NGL;
-    const int fld[3] = {FN_NX, FN_NY, FN_W};
-    s_fn[c][n] = m.fnstat[fld[c] * FN + (size_t)f * NGL + n];
-  }
+    return gdpp_face[((size_t)k * 10 + c) * FN + (size_t)f * NGL + n];
+  });
+  Gather<double, 4 * NQ, 64> g_fs;
+  g_fs.load(tid, 4 * NQ, [&](int t) {
+    const int c = t / NQ, iq = t % NQ;
+    const int fld = c == 0 ? FS_NX : (c == 1 ? FS_NY : (c == 2 ? FS_ZBL : FS_ZBR));
+    return m.fstat[fld * FQ + (size_t)f * NQ + iq];
+  });
+  Gather<double, 3 * NGL, 64> g_fn;
+  g_fn.load(tid, 3 * NGL, [&](int t) {
+    const int c = t / NGL, n = t % NGL;
+    const int fld = c == 0 ? FN_NX : (c == 1 ? FN_NY : FN_W);
+    return m.fnstat[fld * FN + (size_t)f * NGL + n];
+  });
+  g_psiq.store(tid, NGL * NQ, [&](int t, double v) { s_psiq[t] = v; });
+  g_psi.store(tid, NGL * NGL, [&](int t, double v) { s_psi[t] = v; });
+  g_qf.store_j(tid, L * 6 * NGL, [&](int t, int j) {
+    const int k = t / (6 * NGL), r = t % (6 * NGL);
+    double v = g_qf.v[j];
+    if (qf_avg0 && r % 3 == 0) v = 0.5 * (g_qfa.v[j] + v);
+    s_qf[k][r] = v;
+  });
+  g_fa.store(tid, FA_N * NQ, [&](int t, double v) { s_fa[t] = v; });
+  g_gf.store(tid, 8 * NGL, [&](int t, double v) { s_gf[t] = v; });
+  g_gd.store(tid, L * 10 * NGL, [&](int t, double v) { (&s_gd[0][0][0])[t] = v; });
+  g_fs.store(tid, 4 * NQ, [&](int t, double v) { s_fs[t / NQ][t % NQ] = v; });
+  g_fn.store(tid, 3 * NGL, [&](int t, double v) { s_fn[t / NGL][t % NGL] = v; });
   __syncthreads();
   BCL_MARK(3, 1)
   const int er = m.fer[f];
@@ -1533,59 +1787,105 @@ __global__ void __launch_bounds__(256, 3)
     r_qs[1] = m.qstat[QS_TW2 * (size_t)npq + Iq];
     r_qs[2] = m.qstat[QS_PB * (size_t)npq + Iq];
   }
-  load_basis<NGL, NQ>(m, s_psiq, s_dpsiq, s_dpsi, s_psi, tid, BS);
-  if (tid < 4) {
-    s_face[tid] = m.efaces[e * 4 + tid];
-    s_side[tid] = m.eside[e * 4 + tid];
-    s_bc[tid] = m.ebc[e * 4 + tid];
-  }
-  for (int t = tid; t < 4 * NGL; t += BS) s_map[t] = m.efmap[e * 4 * NGL + t];
-  // the element's face data (Apply_layers_fluxes' lifts, the LDG face fluxes), staged with the
-  // other loads: momL or momR by the element's side of each face
-  // (element-major sources only: no load here waits for another)
-  for (int t = tid; t < 4 * NQ; t += BS)
-    s_fw[t] = m.efstat[((size_t)e * 4 + t / NQ) * EFBLK(NGL, NQ) + EF_W * NQ + t % NQ];
-  for (int t = tid; t < L * 2 * 4 * NQ; t += BS) {
+  // every load of the phase first (Gather), then the LDS stores: one memory round trip.  The
+  // sources are element-major (the element's face data -- Apply_layers_fluxes' lifts, the LDG face
+  // fluxes -- in its own element-side slots), so no load waits for another.
+  BasisGather<NGL, NQ, BS> g_bas;
+  g_bas.load(m, tid);
+  // element record: the face-node map, face ids, sides, boundary codes (one gather per array: a
+  // source selected per lane would load its pointer from the kernel arguments first)
+  Gather<int, 4 * NGL, BS> g_map;
+  g_map.load(tid, 4 * NGL, [&](int t) { return m.efmap[e * 4 * NGL + t]; });
+  Gather<int, 4, BS> g_face, g_side, g_bc;
+  g_face.load(tid, 4, [&](int t) { return m.efaces[e * 4 + t]; });
+  g_side.load(tid, 4, [&](int t) { return m.eside[e * 4 + t]; });
+  g_bc.load(tid, 4, [&](int t) { return m.ebc[e * 4 + t]; });
+  Gather<double, 4 * NQ, BS> g_fw;
+  g_fw.load(tid, 4 * NQ, [&](int t) { return m.efstat[((size_t)e * 4 + t / NQ) * EFBLK(NGL, NQ) + EF_W * NQ + t % NQ]; });
+  Gather<double, MAXL * 2 * 4 * NQ, BS> g_fm;
+  g_fm.load(tid, L * 2 * 4 * NQ, [&](int t) {
     const int ko = t / (4 * NQ), lf = (t / NQ) % 4, iq = t % NQ;
-    (&s_fm[0][0][0])[t] = momL[MSLOT(e * 4 + lf, ko >> 1, ko & 1, iq, NQ)];
-  }
-  for (int t = tid; t < L * 2 * 4 * NGL; t += BS) {
+    return momL[MSLOT(e * 4 + lf, ko >> 1, ko & 1, iq, NQ)];
+  });
+  Gather<double, MAXL * 2 * 4 * NGL, BS> g_fl;
+  g_fl.load(tid, L * 2 * 4 * NGL, [&](int t) {
     const int ko = t / (4 * NGL), lf = (t / NGL) % 4, n = t % NGL;
-    (&s_fl[0][0][0])[t] = lapf[MSLOT(e * 4 + lf, ko >> 1, ko & 1, n, NGL)];
-  }
-  for (int t = tid; t < L * 3 * P; t += BS) {
-    int k = t / (3 * P), r = t % (3 * P);
-    const size_t i = (size_t)k * 3 * npoin + (size_t)e * 3 * P + r;
-    s_qp[k][r % 3][r / 3] = (qp_avg0 && r % 3 == 0) ? 0.5 * (qp_avg0[i] + qp_in[i]) : qp_in[i];
-    if (r % 3) s_qm2[k][r % 3 - 1][r / 3] = q_in[(size_t)k * 3 * npoin + (size_t)e * 3 * P + r];
-  }
-  for (int t = tid; t < 5 * Q; t += BS) {
+    return lapf[MSLOT(e * 4 + lf, ko >> 1, ko & 1, n, NGL)];
+  });
+  // qprime (and, thickness: the corrector's qp_avg0 | momenta: q_in) of every layer
+  Gather<double, MAXL * 3 * P, BS> g_qp, g_qx;
+  auto qidx = [&](int t) { return (size_t)(t / (3 * P)) * 3 * npoin + (size_t)e * 3 * P + t % (3 * P); };
+  g_qp.load(tid, L * 3 * P, [&](int t) { return qp_in[qidx(t)]; });
+  g_qx.load(tid, L * 3 * P, [&](int t) {
+    const int r = t % (3 * P);
+    return ((r % 3 || !qp_avg0) ? q_in : qp_avg0)[qidx(t)];  // (r%3 == 0 without qp_avg0: unused)
+  });
+  Gather<double, 5 * Q, BS> g_qm;
+  g_qm.load(tid, 5 * Q, [&](int t) {
     const int c = t / Q;
-    s_qm[c][t % Q] = m.qstat[(c < 4 ? QS_EX + c : QS_W) * (size_t)npq + (size_t)e * Q + t % Q];
-  }
-  for (int t = tid; t < 5 * P; t += BS) {
+    return m.qstat[(c < 4 ? QS_EX + c : QS_W) * (size_t)npq + (size_t)e * Q + t % Q];
+  });
+  Gather<double, 5 * P, BS> g_nm;
+  g_nm.load(tid, 5 * P, [&](int t) {
     const int c = t / P;
-    s_nm[c][t % P] = m.nstat[(c < 4 ? NS_EX + c : NS_W) * (size_t)npoin + (size_t)e * P + t % P];
-  }
-  for (int t = tid; t < P4_N * P; t += BS) {
-    const int c = t / P, p = t - c * P;
+    return m.nstat[(c < 4 ? NS_EX + c : NS_W) * (size_t)npoin + (size_t)e * P + t % P];
+  });
+  Gather<double, P4_N * P, BS> g_p4;
+  // (one address per entry, selected: no load under a branch; entries without a source read
+  // massinv and are zeroed at the store)
+  auto p4_src = [&](int c, int p) -> const double * {
     const size_t I = (size_t)e * P + p;
-    double v = 0.0;
-    if (c < P4_QB) {
-      const int ns[4] = {NS_MINV, NS_F2, NS_A, NS_B};
-      v = m.nstat[ns[c] * (size_t)npoin + I];
-    } else if (c < P4_PB) {
-      v = qb[I * 4 + (c - P4_QB)];
-    } else if (c == P4_PB) {
-      v = m.nstat[NS_PB * (size_t)npoin + I];
-    } else if (c < P4_D) {
-      if (c - P4_H < L) v = q[((size_t)(c - P4_H) * npoin + I) * 3];
-    } else if (mode == 1 && c - P4_D < L) {
-      const int k = c - P4_D;
-      v = qp_avg0 ? qp_in[((size_t)k * npoin + I) * 3] : dpp2[(size_t)k * npoin + I];
-    }
-    s_p4[c][p] = v;
+    const int ns = c == 0 ? NS_MINV : (c == 1 ? NS_F2 : (c == 2 ? NS_A : (c == 3 ? NS_B : NS_PB)));
+    const int kh = c - P4_H, kd = c - P4_D;
+    if (c < P4_QB || c == P4_PB) return m.nstat + ns * (size_t)npoin + I;
+    if (c < P4_PB) return qb + I * 4 + (c - P4_QB);
+    if (c < P4_D) return kh < L ? q + ((size_t)kh * npoin + I) * 3 : m.nstat + NS_MINV * (size_t)npoin + I;
+    if (mode == 1 && kd < L) return qp_avg0 ? qp_in + ((size_t)kd * npoin + I) * 3 : dpp2 + (size_t)kd * npoin + I;
+    return m.nstat + NS_MINV * (size_t)npoin + I;
+  };
+  auto p4_zero = [&](int c) { return (c >= P4_H && c < P4_D && c - P4_H >= L) || (c >= P4_D && !(mode == 1 && c - P4_D < L)); };
+  g_p4.load(tid, P4_N * P, [&](int t) { return *p4_src(t / P, t % P); });
+  // phase 1's node task of this thread (task w = L*Q + p: at most one per thread), its inputs
+  int my_p = -1;
+  static_assert(P <= BS, "one node task per thread");
+#pragma unroll
+  for (int jw = 0; jw < (MAXL * Q + P + BS - 1) / BS; jw++) {
+    const int w = tid + jw * BS;
+    if (w >= L * Q && w < L * Q + P) my_p = w - L * Q;
   }
+  double r_z, r_so2, r_gs[4], r_dv[MAXL], r_dg[MAXL][4];
+  {
+    const size_t I = (size_t)e * P + (my_p >= 0 ? my_p : 0);  // (no node task: loaded, unused)
+    r_z = m.nstat[NS_ZB * (size_t)npoin + I];
+    r_so2 = nacc[NACC_I(NA_OPE2, e, 0) + (I - (size_t)e * P)];
+#pragma unroll
+    for (int c = 0; c < 4; c++) r_gs[c] = nacc[NACC_I((NA_G1 + c), e, 0) + (I - (size_t)e * P)];
+#pragma unroll
+    for (int k = 0; k < MAXL; k++) {
+      const int kk = k < L ? k : L - 1;  // (layers past L: loaded, unused)
+      r_dv[k] = dpprime_visc[(size_t)kk * npoin + I];
+#pragma unroll
+      for (int c = 0; c < 4; c++) r_dg[k][c] = dpp_graduv[((size_t)kk * 4 + c) * npoin + I];
+    }
+  }
+  // the stores
+  g_bas.store(s_psiq, s_dpsiq, s_dpsi, s_psi, tid);
+  g_map.store(tid, 4 * NGL, [&](int t, int v) { s_map[t] = v; });
+  g_face.store(tid, 4, [&](int t, int v) { s_face[t] = v; });
+  g_side.store(tid, 4, [&](int t, int v) { s_side[t] = v; });
+  g_bc.store(tid, 4, [&](int t, int v) { s_bc[t] = v; });
+  g_fw.store(tid, 4 * NQ, [&](int t, double v) { s_fw[t] = v; });
+  g_fm.store(tid, L * 2 * 4 * NQ, [&](int t, double v) { (&s_fm[0][0][0])[t] = v; });
+  g_fl.store(tid, L * 2 * 4 * NGL, [&](int t, double v) { (&s_fl[0][0][0])[t] = v; });
+  g_qp.store_j(tid, L * 3 * P, [&](int t, int j) {
+    const int k = t / (3 * P), r = t % (3 * P);
+    const double v = g_qp.v[j], x = g_qx.v[j];
+    s_qp[k][r % 3][r / 3] = (qp_avg0 && r % 3 == 0) ? 0.5 * (x + v) : v;
+    if (r % 3) s_qm2[k][r % 3 - 1][r / 3] = x;
+  });
+  g_qm.store(tid, 5 * Q, [&](int t, double v) { s_qm[t / Q][t % Q] = v; });
+  g_nm.store(tid, 5 * P, [&](int t, double v) { s_nm[t / P][t % P] = v; });
+  g_p4.store(tid, P4_N * P, [&](int t, double v) { s_p4[t / P][t % P] = p4_zero(t / P) ? 0.0 : v; });
   __syncthreads();
   if (*m.runflag & RUN_ABORT) return;  // (a persistent sub-cycle of this run did no work: DevMesh)
   // the corrector of a completed step (mode 1) counts it: the host's retry point after an abort
@@ -1624,13 +1924,9 @@ __global__ void __launch_bounds__(256, 3)
       s_iv[k][3][qd] = t0;
       s_iv[k][4][qd] = t1;
     } else {
-      const int p = w - L * Q;
-      const size_t I = (size_t)e * P + p;
-      double z = m.nstat[NS_ZB * (size_t)npoin + I];
-      const double so = sqrt(nacc[NACC_I(NA_OPE2, e, p)]);
-      double gsum[4];
-#pragma unroll
-      for (int c = 0; c < 4; c++) gsum[c] = nacc[NACC_I((NA_G1 + c), e, p)];
+      const int p = w - L * Q;  // (== my_p: its inputs were loaded with the others)
+      double z = r_z;
+      const double so = sqrt(r_so2);
       s_z[L][p] = z;
       for (int k = L - 1; k >= 0; k--) {
         z = z + (m.alpha[k] / g) * (so * s_qp[k][0][p]);
@@ -1639,9 +1935,8 @@ __global__ void __launch_bounds__(256, 3)
 #pragma unroll
       for (int k = 0; k < MAXL; k++) {
         if (k >= L) break;
-        const double d = dpprime_visc[(size_t)k * npoin + I];
 #pragma unroll
-        for (int c = 0; c < 4; c++) s_qq[k][c][p] = d * gsum[c] + dpp_graduv[((size_t)k * 4 + c) * npoin + I];
+        for (int c = 0; c < 4; c++) s_qq[k][c][p] = r_dv[k] * r_gs[c] + r_dg[k][c];
       }
     }
   }
