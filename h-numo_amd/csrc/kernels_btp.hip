@@ -1867,7 +1867,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       if (k == 0) for_tasks<BS>(tid, C::OL, 4 * NGL, ldg_task);
       if (k == NCH && !(a.dbg & 2)) for_tasks<BS>(tid, 0, 2 * P, [&](int t, bool) { lap_task(t / P, t % P); });
       LDS_BARRIER();
-      if (k < 6) STAGE_MARK(6 + k);
+      if (k < (PERSIST ? 2 : 6)) STAGE_MARK(6 + k);  // (persistent: slots 8-11 accumulate the phases)
     }
   }
   STAGE_MARK(3);
