@@ -1,6 +1,6 @@
 """A/B timing of engine builds (HNUMO_LIB) on a list of configurations: per-stage / persistent
 stage time, one-step time and a hash of the state after 2 steps (equal hashes = same bits).
-Usage (GPU): HNUMO_LIB=<so> python tools/ab_stage.py cfg[:persist|:stage] ..."""
+Usage (GPU): HNUMO_LIB=<so> python tools/ab_stage.py cfg[@k=v,...][:persist|:stage] ..."""
 import hashlib
 import os
 import sys
@@ -15,7 +15,10 @@ for arg in sys.argv[1:]:
     cfg, _, mode = arg.partition(":")
     os.environ["HNUMO_PERSISTENT"] = "0" if mode == "stage" else "1"
     from hnumo.engine import Engine
-    case = build_case(make_config(cfg), dense=False)
+    # cfg@k=v,k=v: integer overrides of the configuration (e.g. dg316L3@nelx=79,nely=158)
+    cfg, _, ov = cfg.partition("@")
+    over = {k: int(v) for k, v in (x.split("=") for x in ov.split(",") if x)}
+    case = build_case(make_config(cfg, **over), dense=False)
     e = Engine(case)
     e.set_resident(True)
     q, qb, qp = e.state()
