@@ -1500,8 +1500,22 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           double pi, dpi;
           PDQ(bi + iq, pi, dpi);
           const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
+          if (DBGX(16384)) {  // (diagnostics: no quad-point LDS reads at all)
+            const double x = (double)q, dhdx = h_e * x + h_n * x, dhdy = h_e * x + h_n * x;
+            a0 = a0 + x * (dhdx * x + x * dhdy);
+            a1 = a1 + x * ((hi * x + dhdx * x) + x * dhdy);
+            a2 = a2 + x * ((hi * x + dhdx * x) + x * dhdy);
+            continue;
+          }
           const double dhdx = h_e * QK(QE_EX, q) + h_n * QK(QE_NX, q);
           const double dhdy = h_e * QK(QE_EY, q) + h_n * QK(QE_NY, q);
+          if (DBGX(8192)) {  // (diagnostics: the quad-point values from registers, no LDS reads)
+            const double x = (double)q;
+            a0 = a0 + x * (dhdx * x + x * dhdy);
+            a1 = a1 + x * ((hi * x + dhdx * x) + x * dhdy);
+            a2 = a2 + x * ((hi * x + dhdx * x) + x * dhdy);
+            continue;
+          }
           const double w = QW(q), uv = QO(4, q);
           a0 = a0 + w * (dhdx * QO(0, q) + QO(1, q) * dhdy);
           a1 = a1 + w * ((hi * QO(2, q) + dhdx * QO(3, q)) + uv * dhdy);
