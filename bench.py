@@ -185,7 +185,8 @@ def _limiter(frac: float, dram_frac: float | None, E: int) -> str:
     if dram_frac >= 0.6:
         return f"HBM: DRAM traffic at {dram_frac:.0%} of peak"
     why = (f"{E} elements on 256 CUs ({E / 256.0:.1f} per CU), state and statics resident in LDS across the "
-           "stages" if E < 4096 else "VALU issue (SQ counters: profiles/roofline_pmc.json sq_per_element_stage)")
+           "stages" if E < 4096 else "instruction issue and latency with 5 workgroups per CU, the LDS arena's limit (SQ "
+           "counters: profiles/roofline_pmc.json sq_per_element_stage; DESIGN.md section 9)")
     return f"not HBM: DRAM traffic at {dram_frac:.1%} of peak while the algorithmic bytes run at {frac:.1%}; {why}"
 
 
