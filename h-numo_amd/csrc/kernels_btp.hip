@@ -61,6 +61,11 @@
 #ifndef HNUMO_QPM
 #define HNUMO_QPM 1
 #endif
+// diagnostics builds only (timing; wrong results): N=7 volume sums without their quad-point
+// LDS reads (1: the integrand factors and weight, 2: also the metric terms; profiles/r04x2)
+#ifndef HNUMO_SUMX
+#define HNUMO_SUMX 0
+#endif
 #ifndef HNUMO_OTF_TRIPLE
 #define HNUMO_OTF_TRIPLE 1
 #endif
@@ -1500,7 +1505,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           double pi, dpi;
           PDQ(bi + iq, pi, dpi);
           const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
-          if (DBGX(16384)) {  // (diagnostics: no quad-point LDS reads at all)
+          if constexpr (HNUMO_SUMX == 2) {  // (diagnostics: no quad-point LDS reads at all)
             const double x = (double)q, dhdx = h_e * x + h_n * x, dhdy = h_e * x + h_n * x;
             a0 = a0 + x * (dhdx * x + x * dhdy);
             a1 = a1 + x * ((hi * x + dhdx * x) + x * dhdy);
@@ -1509,7 +1514,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           }
           const double dhdx = h_e * QK(QE_EX, q) + h_n * QK(QE_NX, q);
           const double dhdy = h_e * QK(QE_EY, q) + h_n * QK(QE_NY, q);
-          if (DBGX(8192)) {  // (diagnostics: the quad-point values from registers, no LDS reads)
+          if constexpr (HNUMO_SUMX == 1) {  // (diagnostics: the quad-point values from registers)
             const double x = (double)q;
             a0 = a0 + x * (dhdx * x + x * dhdy);
             a1 = a1 + x * ((hi * x + dhdx * x) + x * dhdy);
