@@ -14,4 +14,4 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -2 $O/smoke.log
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -30 $O/bench.err; exit 1; }
 cat $O/bench.json
-bash tools/gpu_profiles.sh $TAG
+[ -n "$SKIP_PROFILES" ] || bash tools/gpu_profiles.sh $TAG
