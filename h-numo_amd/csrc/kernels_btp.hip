@@ -66,6 +66,11 @@
 #ifndef HNUMO_SUMX
 #define HNUMO_SUMX 0
 #endif
+// E (EW0 == 0): the new state's grad(u_bar) on four waves, one component each (nodal_grad, the
+// same terms and order as nodal_grad4's), after a barrier, instead of on the E1 wave alone
+#ifndef HNUMO_EGRAD4
+#define HNUMO_EGRAD4 1
+#endif
 #ifndef HNUMO_OTF_TRIPLE
 #define HNUMO_OTF_TRIPLE 1
 #endif
@@ -1958,7 +1963,14 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     s_v[p] = qn[3] / qn[0];
   }
   if (a.rhs_only) return;
-  if (a.write_trace) {
+  if (a.write_trace && HNUMO_EGRAD4 && EW0 == 0 && BS == 256) {
+    LDS_BARRIER();  // u_bar, v_bar of every node
+    if ((tid & 63) < P) {
+      const int c = tid >> 6, p = tid & 63, i = p % NGL, j = p / NGL;
+      const double ex = s_ns[((c & 1) ? NE_EY : NE_EX) * P + p], nx = s_ns[((c & 1) ? NE_NY : NE_NX) * P + p];
+      s_grad[c * P + p] = nodal_grad<NGL>(s_dpsi, i, j, ex, nx, (c >> 1) ? s_v : s_u);
+    }
+  } else if (a.write_trace) {
     // grad(u_bar) of the new state at every node, once (the sums B's nodal task forms): the
     // traces below read it, and the persistent kernel's next stage takes it as its own.  The
     // nodes' u_bar, v_bar were written by this same wave (P <= 64).
