@@ -1481,7 +1481,6 @@ __global__ void __launch_bounds__(64)
 #define FA(k) s_fa[(k) * NQ + iq]
   if (tid < NQ) {
     const int iq = tid;
-    const size_t fq = (size_t)f * NQ + iq;
     const double *alpha = m.alpha;
     double nxl = s_fs[0][iq], nyl = s_fs[1][iq];
     double qbl0 = FA(FA_OPEL), qbr0 = FA(FA_OPER);
@@ -1689,7 +1688,6 @@ __global__ void __launch_bounds__(64)
   } else if (tid >= 32 && tid < 32 + NGL) {
     // layer LDG flux at face node n for every layer
     const int n = tid - 32;
-    const size_t fn = (size_t)f * NGL + n;
     double nx = s_fn[0][n], ny = s_fn[1][n], wq = s_fn[2][n];
     const double beta = 0.5, alpha = 1.0 - beta;
 #pragma unroll
