@@ -18,6 +18,14 @@ Workloads (BASELINE.json configs):
                    3 layers, dt=40 s, dt_btp=2 s, split over the N GPUs (strong scaling:
                    rank grid 2x1, 2x2, 4x2 of 158x316 / 158x158 / 79x158 element blocks).
   --weak        -- labelled extra: N blocks of 25x25 elements (weak scaling).
+  --config lake200 at N>1 -- configs[4] (C5), the lake at rest on 200x200 elements, 2 layers, on
+                   a Morton processor-face partition (the C5 reference fixture's).
+  --emulate W:R -- the N>1 code path on ONE GPU (torch.distributed.run --nproc-per-node 1): rank R
+                   of the W-rank partition as its own neighbour (the self-neighbour contract:
+                   its processor faces listed under itself), with the real run's nccl process
+                   group, id broadcast, RCCL engine, two-stream schedule, timed loop, halo check
+                   and strong-scaling base -- the per-GPU cost of a W-GPU run and the setup time
+                   of every phase, measured where no W-GPU node is available.
 Multi-GPU runs one rank per GPU (torch.distributed.run).  Each rank holds one block of the
 brick partitioned the way h-NUMO itself partitions -- processor faces (hnumo/facepart.py,
 p4est.c:1686-1712): the reference's halo contract, with the stage traces exchanged over RCCL
@@ -124,16 +132,17 @@ def cpu_baseline(case, steps: int, cores: int, repeats: int = 3):
             "sample": sample + f", {steps} baroclinic steps of the C restatement (oracle/hnumo_oracle.c, -O2), {t:.2f} s"}
 
 
-def single_gpu_line(cfg: str, workload: str, steps: int = 3):
+def single_gpu_line(cfg: str, workload: str, steps: int = 3, case=None, device: int = 0, breakdown: bool = True):
     """Another BASELINE config on this one GPU, reported beside the N=1 configs[1] line: the C4
     mesh (dg316L3, 99,856 elements; the base of the N>1 strong-scaling lines) and C3 (dg25N7L3,
-    N=7)."""
+    N=7).  Also the strong-scaling base of an N>1 run (rank 0's GPU, the whole mesh)."""
     import torch
     from hnumo.case import build_case, make_config
     from hnumo.engine import Engine
     from hnumo.roofline import element_updates_per_step
-    case = build_case(make_config(cfg), dense=False)
-    eng = Engine(case)
+    if case is None:
+        case = build_case(make_config(cfg), dense=False)
+    eng = Engine(case, device=device)
     eng.set_resident(True)
     q, qb, qp = eng.state()
     eng.ti_rk_bcl(q, qb, qp)
@@ -145,6 +154,7 @@ def single_gpu_line(cfg: str, workload: str, steps: int = 3):
     k_ms = eng.time_stage_kernel(1)
     path = eng.stage_path
     stats = eng.persistent_stats
+    bd = step_breakdown(eng, case, 1) if breakdown else None
     from hnumo.roofline import HBM_PEAK_GBS, stage_bytes
     eng.close()
     ach = stage_bytes(case) / (k_ms * 1e-3) / 1e9
@@ -154,7 +164,68 @@ def single_gpu_line(cfg: str, workload: str, steps: int = 3):
            "stage_kernel_us": round(k_ms * 1e3, 2), "stage_kernel_frac": round(ach / HBM_PEAK_GBS, 4),
            "algorithmic_bytes_per_stage": int(stage_bytes(case)), "persistent_fallbacks": stats["aborts"]}
     out.update(_profiled(cfg, "btp_subcycle_kernel" if path == "persistent" else "btp_stage_kernel", k_ms))
+    if bd:
+        out.update(bd)
     return out
+
+
+def step_breakdown(eng, case, nsteps: int = 2) -> dict:
+    """Per-kernel microseconds of one step (hnumo_step_breakdown: direct launches with an event
+    after each on the engine stream; the state advances) and the sub-cycle-only rate: element-
+    updates of the two barotropic sub-cycles over their own time."""
+    from hnumo.roofline import element_updates_per_step
+    try:
+        bd = eng.step_breakdown(nsteps)
+    except Exception as exc:  # pragma: no cover - diagnostic only
+        return {"step_breakdown_error": f"{type(exc).__name__}: {exc}"}
+    sub = sum(v for k, v in bd.items() if k in ("btp_subcycle", "btp_stage", "subcycle_prologue", "grad_trace",
+                                                "btp_finalize"))
+    tot = sum(bd.values())
+    return {"step_breakdown_us": {k: round(v, 2) for k, v in bd.items()},
+            "step_breakdown_total_us": round(tot, 2),
+            "step_breakdown_note": f"direct launches, an event after each ({nsteps} steps averaged); spans "
+                                   "between events, so they include the launch gaps the captured graph avoids",
+            "subcycle_us_per_step": round(sub, 2),
+            "subcycle_eu_per_s": round(element_updates_per_step(case) / (sub * 1e-6), 1) if sub > 0 else None,
+            "glue_us_per_step": round(tot - sub, 2)}
+
+
+def stream_copy(device: int = 0) -> dict | None:
+    """The measured HBM denominator (achieved bandwidth against the nominal peak
+    AND a stream copy on the same GPU): hnumo_stream_copy_bw over 2 x 2 GiB buffers."""
+    from hnumo.engine import Engine
+    try:
+        best, mean = Engine.stream_copy_bw(device, 2 << 30, 10)
+    except Exception as exc:  # pragma: no cover - diagnostic only
+        print(f"[bench] stream copy failed: {exc}", file=sys.stderr)
+        return None
+    return {"best": round(best, 1), "mean": round(mean, 1),
+            "how": "hnumo_stream_copy_bw: 16-byte grid-stride copy kernel, 2 GiB -> 2 GiB, read + write bytes, "
+                   "best / mean of 10 launches, this GPU, this run"}
+
+
+def c4_cpu_baseline(gcase, cores: int) -> dict | None:
+    """The reference Fortran on the C4 workload itself: ONE baroclinic step of the 316x316 mesh under
+    `mpiexec -n cores` on a Morton processor-face partition (its own MPI halo), each rank reading
+    the dense tables of its own elements (facepart.add_dense_tables)."""
+    from hnumo.facepart import add_dense_tables, face_partition
+    from hnumo.roofline import element_updates_per_step
+    try:
+        t0 = time.perf_counter()
+        parts = [add_dense_tables(face_partition(gcase, cores, r, "morton")) for r in range(cores)]
+        t = _run_reference(parts, 1, cores)
+        wall = time.perf_counter() - t0
+    except Exception as exc:  # pragma: no cover - diagnostic only
+        print(f"[bench] C4 reference baseline failed: {exc}", file=sys.stderr)
+        return None
+    if not t:
+        return None
+    eu = element_updates_per_step(gcase)
+    return {"value": round(eu / t, 1), "unit": "element-updates/s", "cores": cores, "kind": "reference",
+            "sample": f"dg316L3 (C4, {gcase.scalars['nelem']} elements), 1 baroclinic step of the reference Fortran "
+                      f"(amdflang -O2) under mpiexec -n {cores} (Morton processor-face partition, its own MPI "
+                      f"halo), one rank per core: {t:.2f} s (MPI_Wtime, max over ranks; {wall:.0f} s with the "
+                      "per-rank dense tables and bundles)"}
 
 
 def _profiled(cfg: str, kname: str, k_ms: float) -> dict:
@@ -190,20 +261,39 @@ def _limiter(frac: float, dram_frac: float | None, E: int) -> str:
     return f"not HBM: DRAM traffic at {dram_frac:.1%} of peak while the algorithmic bytes run at {frac:.1%}; {why}"
 
 
+def _self_neighbour(pc):
+    """The self-neighbour contract (tests/test_rccl_self_gpu.py): every processor face of the rank
+    listed under the rank itself, as ONE list, in a one-rank communicator -- the same streams,
+    element split, launches, events and RCCL group calls per stage as the real rank, each message
+    going to itself instead of over xGMI."""
+    import numpy as np
+    from hnumo.facepart import FaceNeighbour
+    pc.nranks, pc.rank = 1, 0
+    faces = [n.faces for n in pc.fneighbours]
+    pc.fneighbours = [FaceNeighbour(0, np.concatenate(faces))] if faces else []
+    return pc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None, help="default: 20 at N=1 (dg25L3), 5 at N>1 (C4)")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default=None, help="default: dg25L3 at N=1, dg316L3 (C4) at N>1")
+    ap.add_argument("--config", default=None, help="default: dg25L3 at N=1, dg316L3 (C4) at N>1; lake200 = C5")
     ap.add_argument("--weak", action="store_true", help="N>1: N blocks of the 1-GPU mesh (weak scaling)")
     ap.add_argument("--halo", default="faces", choices=["faces", "ghost"],
                     help="N>1: processor faces (the reference's contract) or a one-element ghost layer")
+    ap.add_argument("--order", default=None, choices=["block", "morton"],
+                    help="N>1 processor-face partition: block (default; C4's 4x2 blocks) or morton (default for lake200)")
+    ap.add_argument("--emulate", default=None, metavar="W:R",
+                    help="one GPU: rank R of a W-rank run as its own neighbour (see the module docstring)")
     ap.add_argument("--cpu-steps", type=int, default=8)
     ap.add_argument("--cpu-cores", type=int, default=16,
                     help="MPI ranks (= host cores) of the reference CPU baseline (the GPU box's share is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c4-cpu", action="store_true", help="N=1: skip the reference C4 step on the host cores")
     ap.add_argument("--no-c4", action="store_true", help="N=1: skip the c4_single_gpu / c3_single_gpu figures")
+    ap.add_argument("--no-base", action="store_true", help="N>1: skip the strong-scaling base (whole mesh on rank 0's GPU)")
     ap.add_argument("--summation", default="reference", choices=["reference", "factored"],
                     help="stage summation order (hnumo_set_summation); only 'reference' meets the 1e-10 bar")
     args = ap.parse_args()
@@ -211,26 +301,44 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    emu = None
+    if args.emulate:
+        if world != 1:
+            sys.exit("--emulate runs on one GPU (one rank)")
+        W, R = (int(x) for x in args.emulate.split(":"))
+        if not (W > 1 and 0 <= R < W):
+            sys.exit("--emulate W:R needs W > 1 and 0 <= R < W")
+        emu = (W, R)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    nparts, prank = emu if emu else (world, rank)   # the partition this process runs
+    multi = nparts > 1
     import torch
     dist = None
-    if world > 1:
+    setup = {}
+    if multi:
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
+        t0 = time.perf_counter()
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        setup["init_process_group_s"] = round(time.perf_counter() - t0, 2)
 
     from hnumo.case import build_case, make_config
     from hnumo.engine import Engine
     from hnumo.roofline import HBM_PEAK_GBS, element_updates_per_step, stage_bytes, step_bytes
 
-    weak = world > 1 and args.weak
-    cfg_name = args.config or ("dg316L3" if world > 1 and not weak else "dg25L3")
-    steps = args.steps if args.steps is not None else (20 if world == 1 or weak else 5)
+    weak = multi and args.weak
+    cfg_name = args.config or ("dg316L3" if multi and not weak else "dg25L3")
+    order = args.order or ("morton" if cfg_name.startswith("lake") else "block")
+    steps = args.steps if args.steps is not None else (20 if not multi or weak else 5)
     base_cfg = make_config(cfg_name)
     eng, parallelism, scaling = None, "single", "weak"
     case, gcase, live_halo = None, None, False
-    if world > 1:
+    if multi:
         from hnumo.partition import partition, rank_grid
-        px, py = rank_grid(world)
+        px, py = rank_grid(nparts) if (order == "block" or args.halo == "ghost" or weak) else (nparts, 1)
         if weak:
             x0, x1 = base_cfg["xdims"]
             y0, y1 = base_cfg["ydims"]
@@ -239,20 +347,32 @@ def main():
         else:
             gcfg = base_cfg
             scaling = "strong"
+        t0 = time.perf_counter()
         gcase = build_case(gcfg, dense=False)
+        setup["case_build_s"] = round(time.perf_counter() - t0, 2)
         obj = [Engine.rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         err = None
         try:
+            t0 = time.perf_counter()
             if args.halo == "faces":
                 from hnumo.facepart import face_partition
-                case = face_partition(gcase, world, rank, "block")
+                case = face_partition(gcase, nparts, prank, order)
+                if emu:
+                    case = _self_neighbour(case)
             else:
-                case = partition(gcase, world, rank)
+                if emu:
+                    raise ValueError("--emulate needs the processor-face halo")
+                case = partition(gcase, nparts, prank)
+            setup["partition_s"] = round(time.perf_counter() - t0, 2)
+            t0 = time.perf_counter()
             eng = Engine(case, device=local_rank, comm_id=obj[0], summation=args.summation)
+            setup["engine_create_s"] = round(time.perf_counter() - t0, 2)
             eng.set_resident(True)
             q, qb, qp = eng.state()
+            t0 = time.perf_counter()
             eng.ti_rk_bcl(q, qb, qp)                 # first step: uploads, captures the graph, exchanges
+            setup["first_step_s"] = round(time.perf_counter() - t0, 2)
         except Exception as exc:  # pragma: no cover - depends on the node
             err = f"{type(exc).__name__}: {exc}"
         bad = torch.tensor([1 if err else 0], device="cuda")
@@ -267,11 +387,17 @@ def main():
             dist.destroy_process_group()
             sys.exit(1)
         else:
-            bx, by = gcfg["nelx"] // px, gcfg["nely"] // py
             how = ("processor-face halo (reference contract) over RCCL p2p, traces on a 2nd stream overlapped with "
                    "interior elements" if args.halo == "faces" else "one-element ghost halo over RCCL p2p")
-            parallelism = (f"domain decomposition {px}x{py} blocks of {bx}x{by} elements "
-                           f"({gcfg['nelx']}x{gcfg['nely']} total), {how}")
+            if order == "block" or args.halo == "ghost" or weak:
+                bx, by = gcfg["nelx"] // px, gcfg["nely"] // py
+                parallelism = (f"domain decomposition {px}x{py} blocks of {bx}x{by} elements "
+                               f"({gcfg['nelx']}x{gcfg['nely']} total), {how}")
+            else:
+                parallelism = (f"domain decomposition: {nparts} Morton (Z-order) pieces of the "
+                               f"{gcfg['nelx']}x{gcfg['nely']} elements, {how}")
+            if emu:
+                parallelism = f"EMULATED on one GPU: rank {prank} of [{parallelism}] as its own neighbour"
             live_halo = True
     if eng is None:
         if case is None:
@@ -312,7 +438,7 @@ def main():
     k_src = "graph event nodes around the corrector sub-cycle"
     if not (k_ms and k_ms > 0):
         k_ms = eng.time_stage_kernel(2)
-        k_src = "events around 2 direct corrector sub-cycles" + (" (incl. halo exchanges)" if world > 1 else "")
+        k_src = "events around 2 direct corrector sub-cycles" + (" (incl. halo exchanges)" if multi else "")
     if path == "persistent":
         k_src += "; one launch per sub-cycle, time per stage = launch time / (N_btp*kstages)"
     eng.sync(q, qb, qp)
@@ -323,14 +449,26 @@ def main():
         # the halo proves itself: one step from the IC over the live RCCL transport against the
         # same step computed on this GPU alone (hnumo/halocheck.py); a mismatch is an error
         from hnumo import halocheck as HC
+        t0 = time.perf_counter()
         mine = HC.owned(case, HC.step_from_ic(eng))
-        if args.halo == "faces":
-            _, ref = HC.reference_faces(gcase, world, rank, "block", local_rank)
+        if emu:
+            # the self-neighbour partition's own local-exchange-group step is what the RCCL run must
+            # equal; the real run's check (all W partitions as a local group) is built and stepped
+            # too, to time it, but not compared (a real rank's neighbours are other ranks)
+            _, ref = HC.reference_faces_cases([case], 0, local_rank)
+            ref = HC.owned(case, ref)
+            t1 = time.perf_counter()
+            HC.reference_faces(gcase, nparts, prank, order, local_rank)
+            setup["halocheck_real_run_s"] = round(time.perf_counter() - t1, 2)
+            against = "the same self-neighbour partition as a local exchange group on this GPU (device copies)"
+        elif args.halo == "faces":
+            _, ref = HC.reference_faces(gcase, world, rank, order, local_rank)
             ref = HC.owned(case, ref)
             against = "the same processor-face partitions as one local exchange group on each GPU (device copies)"
         else:
             ref = HC.reference_ghost(gcase, case, local_rank)
             against = "the whole mesh as one rank on each GPU"
+        setup["halocheck_s"] = round(time.perf_counter() - t0, 2)
         same, rel = HC.compare(mine, ref)
         bad = torch.tensor([0 if same else 1], device="cuda")
         dist.all_reduce(bad, op=dist.ReduceOp.MAX)
@@ -347,6 +485,11 @@ def main():
     ms_per_step = 1e3 * elapsed / steps
     sb = stage_bytes(case)
     roof = None
+    bd = None
+    copy_bw = None
+    if not multi:
+        bd = step_breakdown(eng, case, 2)
+        copy_bw = stream_copy(local_rank)
     if k_ms and k_ms > 0:
         achieved = sb / (k_ms * 1e-3) / 1e9
         step_ach = step_bytes(case) * steps / elapsed / 1e9
@@ -361,19 +504,28 @@ def main():
                 "step_achieved": round(step_ach, 1), "step_frac": round(step_ach / HBM_PEAK_GBS, 4),
                 "step_bytes": int(step_bytes(case)),
                 "step_model": "E*(2*N_btp*kstages*B_stage + B_bcl_step)/T_step per GPU (hnumo/roofline.py)"}
-        roof.update(_profiled(cfg_name, kname, k_ms) if world == 1 or weak else {})
+        if copy_bw:
+            roof["peak_measured"] = copy_bw["best"]
+            roof["frac_measured"] = round(achieved / copy_bw["best"], 4)
+            roof["step_frac_measured"] = round(step_ach / copy_bw["best"], 4)
+            roof["peak_measured_how"] = copy_bw["how"] + f" (mean {copy_bw['mean']} GB/s)"
+        roof.update(_profiled(cfg_name, kname, k_ms) if not multi or weak else {})
         roof["limiter"] = _limiter(roof["frac"], roof.get("dram_frac"), E)
+        if bd:
+            roof.update(bd)
     S = case.scalars
-    if world > 1 and not weak:
-        wl = (f"{cfg_name} (C4): double-gyre {base_cfg['nelx']}x{base_cfg['nely']} = "
-              f"{base_cfg['nelx'] * base_cfg['nely']} elements split over {world} GPUs")
+    if multi and not weak:
+        what = "C5" if cfg_name.startswith("lake") else "C4"
+        wl = (f"{cfg_name} ({what}): {base_cfg['test_case']} {base_cfg['nelx']}x{base_cfg['nely']} = "
+              f"{base_cfg['nelx'] * base_cfg['nely']} elements split over {nparts} GPUs")
     else:
-        wl = f"{cfg_name}: double-gyre {base_cfg['nelx']}x{base_cfg['nely']} elements per GPU"
+        wl = f"{cfg_name}: {base_cfg['test_case']} {base_cfg['nelx']}x{base_cfg['nely']} elements per GPU"
     out = {
         "metric": "DG element-updates/sec (all layers, per RK stage)",
         "value": round(value, 1), "unit": "element-updates/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-        "scaling": scaling, "vs_baseline": None, "dtype": "f64", "data": "synthetic (analytic double-gyre IC)",
+        "scaling": scaling, "vs_baseline": None, "dtype": "f64",
+        "data": f"synthetic (analytic {base_cfg['test_case']} IC)",
         "config": {"workload": wl + f", N={S['ngl'] - 1}, {S['nlayers']} layers, "
                                f"N_btp={S['N_btp']}, kstages={S['kstages']}",
                    "elements": int(eu_total / steps / (2 * S["N_btp"] * S["kstages"])),
@@ -389,14 +541,50 @@ def main():
     # per-stage launches), trial re-probes, and re-probes that found the grid resident again
     out["persistent"] = eng.persistent_stats
     eng.close()
-    if rank == 0 and world == 1 and not args.no_c4 and args.config is None:
+    if multi and not weak and not args.no_base:
+        # the strong-scaling base: the whole mesh on rank 0's GPU alone, timed in this run, so the
+        # N>1 line carries the 1-GPU number of the SAME workload (the N=1 line is configs[1])
+        base = None
+        if rank == 0:
+            t0 = time.perf_counter()
+            try:
+                base = single_gpu_line(cfg_name, f"{cfg_name} (whole mesh) on rank 0's GPU", 3, case=gcase,
+                                       device=local_rank, breakdown=False)
+            except Exception as exc:  # pragma: no cover - diagnostic only
+                base = {"error": f"{type(exc).__name__}: {exc}"}
+            setup["strong_scaling_base_s"] = round(time.perf_counter() - t0, 2)
+        dist.barrier()
+        if rank == 0 and base is not None:
+            out["strong_scaling_base"] = base
+            if "value" in base:
+                v = value if not emu else gcase.scalars["nelem"] * 2 * S["N_btp"] * S["kstages"] * 1e3 / ms_per_step
+                out["speedup_vs_base"] = round(v / base["value"], 3)
+    if emu:
+        E_g = gcase.scalars["nelem"]
+        out["emulation"] = {
+            "world": nparts, "rank": prank, "order": order,
+            "rank_elements": S["nelem"], "processor_faces": int(sum(n.faces.size for n in case.fneighbours)),
+            "projection_eu_per_s": round(E_g * 2 * S["N_btp"] * S["kstages"] * 1e3 / ms_per_step, 1),
+            "note": f"this GPU ran rank {prank}'s block at {ms_per_step:.3f} ms per step with every exchange going to "
+                    f"itself; if each of the {nparts} GPUs runs its block in that time, the whole-mesh rate is the "
+                    "projection (xGMI transfer time of the real messages not included)"}
+    if multi:
+        out["setup_s"] = setup
+    if rank == 0 and not multi and not args.no_c4 and args.config is None:
         for key, cfg, wl, n in [("c4_single_gpu", "dg316L3", "dg316L3 (C4: 316x316 elements, N=4, 3 layers)", 3),
                                 ("c3_single_gpu", "dg25N7L3", "dg25N7L3 (C3: 25x25 elements, N=7, 3 layers)", 5)]:
             try:
-                out[key] = single_gpu_line(cfg, wl, n)
+                c = build_case(make_config(cfg), dense=False)
+                out[key] = single_gpu_line(cfg, wl, n, case=c)
+                if key == "c4_single_gpu" and not args.no_cpu_baseline and not args.no_c4_cpu:
+                    ncores = max(1, min(args.cpu_cores, len(os.sched_getaffinity(0))))
+                    cb = c4_cpu_baseline(c, ncores)
+                    if cb:
+                        out[key]["cpu_baseline"] = cb
+                del c
             except Exception as exc:  # pragma: no cover - diagnostic only
                 out[key] = {"error": f"{type(exc).__name__}: {exc}"}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not multi and not args.no_cpu_baseline:
         ncores = max(1, min(args.cpu_cores, len(os.sched_getaffinity(0))))
         out["cpu_baseline"] = cpu_baseline(build_case(make_config(cfg_name)), args.cpu_steps, ncores)
     if rank == 0:

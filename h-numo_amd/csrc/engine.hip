@@ -150,7 +150,29 @@ struct hnumo_engine {
   // botfr != 0; HNUMO_QPQ=0: every stage interpolates, for A/B timing)
   double *qpq = nullptr;      // [E][3][Q]
   double *qsv = nullptr;      // [E][2][P][4] Shu-Osher states of the slim persistent sub-cycle (StageArgs::qsv)
+  // hnumo_step_breakdown: events recorded on the engine stream after every launch of a direct
+  // (uncaptured) step, each with the name of the kernel family it closes (kmark)
+  struct KMarks {
+    std::vector<hipEvent_t> ev;
+    std::vector<const char *> name;
+    size_t n = 0;
+  } *km = nullptr;
 };
+
+// the per-kernel breakdown's mark after a launch on the engine stream (no-op outside
+// hnumo_step_breakdown; never inside a capture)
+static void kmark(hnumo_engine *e, const char *name) {
+  if (!e->km) return;
+  auto &k = *e->km;
+  if (k.n == k.ev.size()) {
+    hipEvent_t ev = nullptr;
+    if (hipEventCreate(&ev) != hipSuccess) return;
+    k.ev.push_back(ev);
+    k.name.push_back(nullptr);
+  }
+  (void)hipEventRecord(k.ev[k.n], e->stream);
+  k.name[k.n++] = name;
+}
 
 template <typename T>
 static T *dalloc(hnumo_engine *eng, size_t n) {
@@ -206,8 +228,12 @@ struct Launch {
         return;
       }
       if (e->summation == HNUMO_SUM_REFERENCE && e->stage_nb == 4) {
-        hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, 4>), dim3(n), dim3(StageCfg<NGL, NQ, false, 4>::BS), 0,
-                           st, a);
+        if (stop)
+          hipExtLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, 4>), dim3(n), dim3(StageCfg<NGL, NQ, false, 4>::BS),
+                                0, st, nullptr, stop, 0, a);
+        else
+          hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, 4>), dim3(n), dim3(StageCfg<NGL, NQ, false, 4>::BS), 0,
+                             st, a);
         return;
       }
     }
@@ -260,9 +286,11 @@ struct Launch {
   }
   // face traces of elements [e0, e0+n) into their neighbours' slots
   static void grad_trace(hnumo_engine *e, const double *qb, double *gt, int e0, int n, TraceGranule *gtr = nullptr) {
-    if (n > 0)
+    if (n > 0) {
       hipLaunchKernelGGL((grad_trace_kernel<NGL, NQ>), dim3(n), dim3(64), 0, e->stream, e->m, qb, gt, e0, gtr,
                          e->epoch);
+      kmark(e, "grad_trace");
+    }
   }
   // extract_qprime_df_face / extract_dprime_df_face + bcl_create_communicator (ti_rk_bcl.F90:43-44,
   // :62, :75-76): processor faces take the neighbour's side 1 as their side 2
@@ -270,6 +298,7 @@ struct Launch {
     size_t n = (size_t)e->nface * NGL;
     hipLaunchKernelGGL((extract_face_kernel<NGL>), dim3((n + 255) / 256), dim3(256), 0, e->stream, e->m, qp, qf,
                        only_dp);
+    kmark(e, "extract_face");
     face_exchange_qf(e, qf, only_dp ? 1 : 3);
   }
   // (qp_avg, qf_avg: the corrector's averages qp = 0.5*(qp + qp_avg), qf = 0.5*(qf_avg + qf) formed
@@ -282,9 +311,11 @@ struct Launch {
     hipLaunchKernelGGL((bcl_coeffs_elem_kernel<NGL, NQ>), dim3(e->nelem), dim3(Blk<NGL, NQ>::BSW), 0, e->stream, e->m, qp,
                        qp_avg, e->qcoef, e->ncoef, e->dpp_graduv, e->dpprime_visc, e->ecoef, fz ? qf : nullptr,
                        qf_avg, qf_out, e->fcoef, e->fncoef, e->gdpp_face, e->efcoef);
+    kmark(e, "bcl_coeffs_elem");
     if (!fz)
       hipLaunchKernelGGL((bcl_coeffs_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, qf_avg,
                          e->dpp_graduv, e->dpprime_visc, e->fcoef, e->fncoef, e->gdpp_face, e->efcoef);
+    if (!fz) kmark(e, "bcl_coeffs_face");
     if (e->face_halo) {  // graduv_dpp_face halo (mod_barotropic_terms.F90:393) and its layer sums
       face_exchange_gdpp(e);
       if (e->NS)
@@ -294,6 +325,7 @@ struct Launch {
     if (e->lapq_on)  // interpolate_dpp right after dpprime_visc is set (ti_rk_bcl.F90:48,67)
       hipLaunchKernelGGL((lapq_dpp_kernel<NGL, NQ>), dim3(std::min<size_t>(((size_t)e->L * e->npq + 255) / 256, 4096)),
                          dim3(256), 0, e->stream, e->m, e->dpprime_visc, e->dpq);
+    if (e->lapq_on) kmark(e, "lapq_dpp");
   }
   // method_visc == 1, one barotropic stage: btp_create_laplacian_v2's Laplacian of state qb
   static void lapq_btp(hnumo_engine *e, const double *qb, const double *qp) {
@@ -322,9 +354,11 @@ struct Launch {
     if (!fz)
       hipLaunchKernelGGL((mass_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
                          e->fmass, e->slmf_face);
+    if (!fz) kmark(e, "mass_flux_face");
     hipLaunchKernelGGL((mass_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(Blk<NGL, NQ>::BSW), 0, e->stream, e->m, qp,
                        e->qacc, e->fmass, q_in, q, e->slmf, e->dpp, e->neg_flag, fz ? qf : nullptr, e->facc,
                        e->slmf_face);
+    kmark(e, "mass_elem");
   }
   // (qf: the face traces of qp_out's thickness written by cons_elem itself -- fused extract)
   static void cons(hnumo_engine *e, double *q, double *qp_out, int finalize_dp, double *qf = nullptr) {
@@ -332,6 +366,7 @@ struct Launch {
     if (!fz)
       hipLaunchKernelGGL((cons_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, e->dpp,
                          e->facc, e->slmf_face, e->fcons, e->face_halo ? e->cdef : nullptr);
+    if (!fz) kmark(e, "cons_flux_face");
     if (e->face_halo) {  // mass_deficit_mass_face halo (mod_layer_terms.F90:135)
       face_exchange_cdef(e);
       if (e->NS)
@@ -341,6 +376,7 @@ struct Launch {
     hipLaunchKernelGGL((cons_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(Blk<NGL, NQ>::BSW), 0, e->stream, e->m, e->dpp,
                        e->qacc, e->slmf, e->fcons, q, qp_out, finalize_dp, qf, fz ? e->facc : nullptr,
                        e->slmf_face);
+    kmark(e, "cons_elem");
   }
   // (q_in: the momenta entering the update; mode 1 writes the final qprime, see mom_elem_kernel)
   // (qp_avg0, qf_avg0: the corrector's thickness averages of ti_rk_bcl.F90:78-80, formed by the two
@@ -351,9 +387,11 @@ struct Launch {
     if (e->lapq_on) lapq_bcl(e, qp_in);
     hipLaunchKernelGGL((mom_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
                        e->gdpp_face, e->gfacc, e->momL, e->momR, e->lapf, qf_avg0);
+    kmark(e, "mom_flux_face");
     hipLaunchKernelGGL((mom_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(MomCfg<NGL, NQ>::BS), 0, e->stream, e->m, qp_in, e->qacc,
                        e->nacc, e->dpp_graduv, e->dpprime_visc, e->momL, e->momR, e->lapf, qb, q_in, q, qp_out, mode,
                        e->lapq_on ? e->lapq : nullptr, e->dpp2, e->neg_flag, qp_avg0, qf_out);
+    kmark(e, "mom_elem");
   }
 };
 
@@ -662,6 +700,7 @@ static void subcycle_prologue(hnumo_engine *e, const double *qb_state, unsigned 
   hipLaunchKernelGGL(subcycle_prologue_kernel, dim3(blocks), dim3(256), 0, e->stream, e->qacc, nqa, e->facc, nfa,
                      e->nacc, z * NA_N * (size_t)e->npoin, e->gfacc, z * 8 * 4 * (size_t)e->nelem * e->ngl,
                      e->qbuf[0], qb_state, 4 * (size_t)e->npoin, epoch);
+  kmark(e, "subcycle_prologue");
 }
 
 static void launch_bcl_coeffs(hnumo_engine *e, double *qp, double *qf) {
@@ -754,6 +793,7 @@ static void launch_subcycle(hnumo_engine *e, double *dst, const double *qp, bool
   if (pers) {
     if (timed && e->kernel_events) (void)hipEventRecord(e->evk0, e->stream);
     DISPATCH(e, subcycle(e, e->d_stages[tab], K * NB));
+    kmark(e, "btp_subcycle");
     if (timed && e->kernel_events) (void)hipEventRecord(e->evk1, e->stream);
     if (racc) return;
     cur = -1;  // (the last stage wrote dst)
@@ -804,6 +844,7 @@ static void launch_subcycle(hnumo_engine *e, double *dst, const double *qp, bool
     for (const StageArgs &a : st) {
       if (e->lapq_on) DISPATCH(e, lapq_btp(e, a.qb_in, a.qprime));
       DISPATCH(e, stage(e, a));
+      kmark(e, "btp_stage");
       if (a.write_trace && e->face_halo) {
         trace_exchange(e, a.trace_out, e->stream);
       } else if (a.write_trace && e->comm_mode) {
@@ -818,6 +859,7 @@ static void launch_subcycle(hnumo_engine *e, double *dst, const double *qp, bool
   hipLaunchKernelGGL(btp_finalize_kernel, dim3(nblk), dim3(256), 0, e->stream, e->qacc, e->facc, e->nacc, e->gfacc,
                      e->tau_wind_ave, e->tau_wind, e->npq, 4 * e->nelem * e->nq, e->npoin, 4 * e->nelem * e->ngl, NB,
                      1.0 / (double)(K * NB), dst, cur >= 0 ? e->qbuf[cur] : dst, 1);
+  kmark(e, "btp_finalize");
 }
 
 // the prediction half of ti_rk_bcl (ti_rk_bcl.F90:43-57) on device state (e->q, e->qb, e->qp):
@@ -1289,7 +1331,8 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     eng->summation = (sm[0] == 'r' || sm[0] == '0') ? HNUMO_SUM_REFERENCE : HNUMO_SUM_FACTORED;
   if (const char *sd = getenv("HNUMO_STAGE_DBG")) eng->stage_dbg = atoi(sd);
   if (const char *fz = getenv("HNUMO_FUSE")) eng->no_fuse = fz[0] == '0';
-  if (const char *sd = getenv("HNUMO_SCHED_DBG")) eng->sched_dbg = atoi(sd);
+  // (bit 1 drops a required stream dependency -- wrong results, timing only: diagnostics builds)
+  if (const char *sd = getenv("HNUMO_SCHED_DBG")) eng->sched_dbg = atoi(sd) & (HNUMO_DBG_EXTRA ? ~0 : ~1);
   // per-stage kernel arena: on meshes that take several residency rounds per stage, the arena
   // sized for 4 workgroups per CU (1-row term chunks) -- 1.566 -> 1.517 ms per stage at C4
   // (tools/ab_env.py, round 2); small meshes keep the 3-per-CU arena
@@ -2120,4 +2163,129 @@ int hnumo_group_ti_rk_bcl(hnumo_engine **engines, int n, double **q_df, double *
   return 0;
 }
 
+// Per-kernel breakdown of a step: `nsteps` direct (uncaptured) steps of the resident device state
+// with an event after every launch on the engine stream; the span between two marks is charged to
+// the kernel family of the later one.  Single-stream engines (one rank) only.
+int hnumo_step_breakdown(hnumo_engine *eng, int nsteps, char *names, int64_t names_len, double *us_per_step,
+                         int max_kernels, int *count) {
+  if (!eng || nsteps < 1 || !names || names_len < 1 || !us_per_step || max_kernels < 1 || !count)
+    return HNUMO_ERR_INVALID;
+  if (eng->comm_mode != 0 || eng->nranks != 1 || eng->face_halo)
+    return fail(eng, HNUMO_ERR_INVALID, "step breakdown: single-rank engines only");
+  if (!eng->resident || !eng->uploaded)
+    return fail(eng, HNUMO_ERR_INVALID, "step breakdown: needs a resident, uploaded state (hnumo_set_resident)");
+  HIPCHK(hipSetDevice(eng->device));
+  int rc = maybe_reprobe(eng);
+  if (rc) return rc;
+  hnumo_engine::KMarks km;
+  HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
+  eng->km = &km;
+  kmark(eng, "start");
+  for (int s = 0; s < nsteps; s++) launch_step(eng);
+  eng->km = nullptr;
+  auto release = [&]() {
+    for (hipEvent_t ev : km.ev) (void)hipEventDestroy(ev);
+  };
+  if (hipStreamSynchronize(eng->stream) != hipSuccess || hipMemcpy(eng->h_neg, eng->neg_flag, sizeof(int),
+                                                                    hipMemcpyDeviceToHost) != hipSuccess) {
+    release();
+    return fail(eng, HNUMO_ERR_DEVICE, "step breakdown: HIP error");
+  }
+  if ((*eng->h_neg & RUN_ABORT) && use_persistent(eng)) {
+    release();
+    persistent_abort(eng);
+    return hnumo_step_breakdown(eng, nsteps, names, names_len, us_per_step, max_kernels, count);
+  }
+  if ((rc = flag_error(eng, *eng->h_neg))) {
+    release();
+    return rc;
+  }
+  std::vector<std::string> nm;
+  std::vector<double> ms;
+  for (size_t i = 1; i < km.n; i++) {
+    float dt = 0.f;
+    if (hipEventElapsedTime(&dt, km.ev[i - 1], km.ev[i]) != hipSuccess) {
+      release();
+      return fail(eng, HNUMO_ERR_DEVICE, "step breakdown: event timing failed");
+    }
+    size_t j = 0;
+    while (j < nm.size() && nm[j] != km.name[i]) j++;
+    if (j == nm.size()) {
+      nm.emplace_back(km.name[i]);
+      ms.push_back(0.0);
+    }
+    ms[j] += dt;
+  }
+  release();
+  std::string joined;
+  const int nk = std::min<int>((int)nm.size(), max_kernels);
+  for (int j = 0; j < nk; j++) {
+    joined += (j ? "\n" : "") + nm[j];
+    us_per_step[j] = 1e3 * ms[j] / nsteps;
+  }
+  if ((int64_t)joined.size() + 1 > names_len) return fail(eng, HNUMO_ERR_INVALID, "step breakdown: names buffer too small");
+  std::memcpy(names, joined.c_str(), joined.size() + 1);
+  *count = nk;
+  return 0;
+}
+
 }  // extern "C"
+
+// ------------------------------------------------------------------ stream-copy bandwidth
+// The measured HBM denominator of the roofline: a grid-stride 16-byte copy,
+// four independent loads in flight per thread before their stores.
+__global__ void __launch_bounds__(256) stream_copy_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
+                                                          size_t n) {
+  const size_t s = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * s < n; i += 4 * s) {
+    const uint4 a = src[i], b = src[i + s], c = src[i + 2 * s], d = src[i + 3 * s];
+    dst[i] = a;
+    dst[i + s] = b;
+    dst[i + 2 * s] = c;
+    dst[i + 3 * s] = d;
+  }
+  for (; i < n; i += s) dst[i] = src[i];
+}
+
+extern "C" int hnumo_stream_copy_bw(int device, int64_t bytes, int reps, double *gbs_out2) {
+  if (bytes < (1 << 20) || reps < 1 || !gbs_out2) return HNUMO_ERR_INVALID;
+  if (hipSetDevice(device) != hipSuccess) return HNUMO_ERR_DEVICE;
+  const size_t n = (size_t)bytes / 16;
+  void *a = nullptr, *b = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipStream_t st = nullptr;
+  int rc = HNUMO_ERR_DEVICE;
+  if (hipMalloc(&a, n * 16) == hipSuccess && hipMalloc(&b, n * 16) == hipSuccess && hipMemset(a, 0, n * 16) == hipSuccess &&
+      hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess && hipEventCreate(&e0) == hipSuccess &&
+      hipEventCreate(&e1) == hipSuccess) {
+    int ncu = 256;
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
+    const unsigned grid = (unsigned)std::min<size_t>((size_t)ncu * 16, (n + 255) / 256);
+    double best = 0.0, sum = 0.0;
+    bool ok = true;
+    for (int r = -2; r < reps && ok; r++) {  // (two untimed warm-ups)
+      ok = hipEventRecord(e0, st) == hipSuccess;
+      hipLaunchKernelGGL(stream_copy_kernel, dim3(grid), dim3(256), 0, st, (const uint4 *)a, (uint4 *)b, n);
+      ok = ok && hipEventRecord(e1, st) == hipSuccess && hipEventSynchronize(e1) == hipSuccess;
+      float ms = 0.f;
+      ok = ok && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms > 0.f;
+      if (ok && r >= 0) {
+        const double g = 2.0 * (double)(n * 16) / (ms * 1e-3) / 1e9;
+        best = std::max(best, g);
+        sum += g;
+      }
+    }
+    if (ok && hipGetLastError() == hipSuccess) {
+      gbs_out2[0] = best;
+      gbs_out2[1] = sum / reps;
+      rc = 0;
+    }
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (st) (void)hipStreamDestroy(st);
+  if (a) (void)hipFree(a);
+  if (b) (void)hipFree(b);
+  return rc;
+}

@@ -49,6 +49,11 @@ CONFIGS = {
     "lake10": dict(test_case="lakeAtrest", nelx=10, nely=10, nop=4, nlayers=2,
                    xdims=(0.0, 2000.0), ydims=(0.0, 2000.0), dt=100.0, dt_btp=1.8,
                    method_visc=0, visc=0.0, botfr=0, cd=0.0, f0=0.0, beta=0.0),
+    # C5 at its performance size: the lake at rest on 200x200 elements (the 10x10 steps scaled with
+    # the element size; the reference fixture lake200_mpi4m_step1 runs it on 4 Morton ranks)
+    "lake200": dict(test_case="lakeAtrest", nelx=200, nely=200, nop=4, nlayers=2,
+                    xdims=(0.0, 2000.0), ydims=(0.0, 2000.0), dt=5.0, dt_btp=0.09,
+                    method_visc=0, visc=0.0, botfr=0, cd=0.0, f0=0.0, beta=0.0),
     # C2: shipped double-gyre namelist (Examples/double_gyre/numo3d.in), L=2
     "dg25": dict(test_case="double-gyre", nelx=25, nely=25, nop=4, nlayers=2,
                  xdims=(0.0, 2.0e6), ydims=(0.0, 2.0e6), dt=500.0, dt_btp=25.0,

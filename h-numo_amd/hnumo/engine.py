@@ -62,6 +62,8 @@ def lib():
         L.hnumo_persistent_info.argtypes = [vp, C.POINTER(C.c_int32)]
         L.hnumo_persistent_stats.argtypes = [vp, C.POINTER(C.c_int32)]
         L.hnumo_debug_force_abort.argtypes = [vp, C.c_int]
+        L.hnumo_step_breakdown.argtypes = [vp, C.c_int, C.c_char_p, C.c_int64, dp, C.c_int, C.POINTER(C.c_int)]
+        L.hnumo_stream_copy_bw.argtypes = [C.c_int, C.c_int64, C.c_int, dp]
         _lib = L
     return _lib
 
@@ -216,6 +218,26 @@ class Engine:
         out = np.zeros(n, dtype=np.uint64)
         self._check(lib().hnumo_debug_stage_profile(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), n))
         return out.reshape(-1, 32)
+
+    def step_breakdown(self, nsteps: int = 2) -> dict:
+        """Microseconds per step of every kernel family of the step, in launch order
+        (hnumo_step_breakdown: direct launches with an event after each; the state advances)."""
+        names = C.create_string_buffer(4096)
+        us = (C.c_double * 64)()
+        n = C.c_int()
+        self._check(lib().hnumo_step_breakdown(self.h, nsteps, names, len(names), us, 64, C.byref(n)))
+        keys = names.value.decode().split("\n") if n.value else []
+        return {k: us[i] for i, k in enumerate(keys)}
+
+    @staticmethod
+    def stream_copy_bw(device: int = 0, nbytes: int = 1 << 30, reps: int = 10) -> tuple:
+        """(best, mean) GB/s of a 16-byte stream copy between two buffers of nbytes
+        (read + write counted; hnumo_stream_copy_bw)."""
+        out = (C.c_double * 2)()
+        rc = lib().hnumo_stream_copy_bw(device, nbytes, reps, out)
+        if rc:
+            raise EngineError(rc, "stream copy measurement failed")
+        return out[0], out[1]
 
     @staticmethod
     def rccl_unique_id() -> bytes:

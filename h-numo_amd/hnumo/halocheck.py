@@ -55,9 +55,15 @@ def step_from_ic(eng):
 def reference_faces(gcase, nranks, rank, order, device):
     """This rank's state after one step of the processor-face partition run as a local exchange
     group on `device` (every rank's engine in this process)."""
-    from .engine import Engine, group_ti_rk_bcl, local_group
     from .facepart import face_partition
     parts = [face_partition(gcase, nranks, r, order) for r in range(nranks)]
+    return reference_faces_cases(parts, rank, device)
+
+
+def reference_faces_cases(parts, rank, device):
+    """reference_faces for given partition cases (ranks 0..n-1 of one partition; a single
+    self-neighbour case for bench.py --emulate)."""
+    from .engine import Engine, group_ti_rk_bcl, local_group
     engines = [Engine(p, device=device) for p in parts]
     try:
         local_group(engines)

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define HNUMO_ABI_VERSION 7
+#define HNUMO_ABI_VERSION 8
 
 enum {
   HNUMO_OK = 0,
@@ -284,6 +284,19 @@ int hnumo_time_stage_kernel(hnumo_engine *eng, int nsubcycles, double *ms_kernel
 /* Diagnostics: per-element phase clocks of the last stage launch, [nelem][32] uint64
  * (engine created with HNUMO_STAGE_PROF=1 in the environment).                        */
 int hnumo_debug_stage_profile(hnumo_engine *eng, uint64_t *out, int64_t n);
+
+/* Per-kernel breakdown of a step (ABI v8; single-rank engines, resident uploaded state):
+ * `nsteps` direct steps of the device state with an event after every launch on the
+ * engine stream.  On return `*count` kernel families (in launch order) with their names
+ * '\n'-joined in `names` (names_len bytes incl. the terminator) and their microseconds
+ * per step in us_per_step[0..count).  The state advances by nsteps steps.               */
+int hnumo_step_breakdown(hnumo_engine *eng, int nsteps, char *names, int64_t names_len,
+                         double *us_per_step, int max_kernels, int *count);
+
+/* Stream-copy bandwidth of `device` (ABI v8): a 16-byte grid-stride copy kernel between two
+ * buffers of `bytes` each, `reps` timed launches after two warm-ups; out2 = {best, mean}
+ * GB/s counting bytes read + written.  The measured denominator of the roofline.        */
+int hnumo_stream_copy_bw(int device, int64_t bytes, int reps, double *out2);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,67 @@
+#!/bin/bash
+# One parameterised GPU session (via gpurun): the named steps in order, each under its own time
+# limit, stopping at the first failure.  Output under gpurun_out/<tag>/.
+#
+#   bash tools/gpu_session.sh <tag> <step> [<step> ...]
+#
+# steps:
+#   tests        pytest -m gpu (the whole GPU suite)
+#   test:<expr>  pytest -m gpu -k <expr>
+#   smoke        __graft_entry__.smoke()
+#   bench        the default bench line (N=1: dg25L3 + C4 + C3 + CPU baselines)
+#   benchq       the bench line without the CPU baselines
+#   emu8         bench.py --emulate 8:1 (C4 rank 1 of 8) under torch.distributed.run, one process
+#   emu4lake     bench.py --emulate 4:1 --config lake200 (C5 rank 1 of 4) the same way
+#   rank         tools/c4_rank_cost.py (C4/8 rank 1 variants)
+#   profiles     tools/gpu_profiles.sh <tag> (kernel trace + FETCH/WRITE + SQ passes)
+#   prof:<cfg>   tools/gpu_profiles.sh <tag> <cfg>
+#   ab:<args>    tools/ab_stage.py <args, commas for spaces>
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+TAG=${1:?tag}
+shift
+O=gpurun_out/$TAG
+mkdir -p $O
+fail() { echo "step $1 failed (rc $2)"; tail -30 "$3"; exit 1; }
+TR="python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541"
+for step in "$@"; do
+  echo "[$(date +%T)] $step"
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || fail $step $? $O/pytest_gpu.log
+      tail -1 $O/pytest_gpu.log ;;
+    test:*)
+      k=${step#test:}
+      timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "$k" > $O/pytest_k.log 2>&1 || fail $step $? $O/pytest_k.log
+      tail -1 $O/pytest_k.log ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || fail $step $? $O/smoke.log
+      tail -1 $O/smoke.log ;;
+    bench)
+      timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err || fail $step $? $O/bench.err
+      cat $O/bench.json ;;
+    benchq)
+      timeout -k 10 600 python bench.py --no-cpu-baseline > $O/benchq.json 2> $O/benchq.err || fail $step $? $O/benchq.err
+      cat $O/benchq.json ;;
+    emu8)
+      timeout -k 10 600 $TR bench.py --emulate 8:1 > $O/emu8.json 2> $O/emu8.err || fail $step $? $O/emu8.err
+      cat $O/emu8.json ;;
+    emu4lake)
+      timeout -k 10 600 $TR bench.py --emulate 4:1 --config lake200 > $O/emu4lake.json 2> $O/emu4lake.err || fail $step $? $O/emu4lake.err
+      cat $O/emu4lake.json ;;
+    rank)
+      timeout -k 10 600 python tools/c4_rank_cost.py > $O/c4_rank_cost.log 2>&1 || fail $step $? $O/c4_rank_cost.log
+      tail -1 $O/c4_rank_cost.log ;;
+    profiles)
+      bash tools/gpu_profiles.sh $TAG || exit 1 ;;
+    prof:*)
+      bash tools/gpu_profiles.sh $TAG ${step#prof:} || exit 1 ;;
+    ab:*)
+      a=${step#ab:}
+      timeout -k 10 900 python tools/ab_stage.py ${a//,/ } > $O/ab.log 2>&1 || fail $step $? $O/ab.log
+      tail -20 $O/ab.log ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[$(date +%T)] session $TAG done"
