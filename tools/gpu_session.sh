@@ -50,6 +50,12 @@ for step in "$@"; do
     emu4lake)
       timeout -k 10 600 $TR bench.py --emulate 4:1 --config lake200 > $O/emu4lake.json 2> $O/emu4lake.err || fail $step $? $O/emu4lake.err
       cat $O/emu4lake.json ;;
+    lake1)
+      timeout -k 10 600 python bench.py --config lake200 --no-cpu-baseline --steps 10 > $O/lake1.json 2> $O/lake1.err || fail $step $? $O/lake1.err
+      cat $O/lake1.json ;;
+    emu4lake2)
+      timeout -k 10 600 $TR bench.py --emulate 4:1 --config lake200 --warmup 1 --steps 2 > $O/emu4lake2.json 2> $O/emu4lake2.err || fail $step $? $O/emu4lake2.err
+      cat $O/emu4lake2.json ;;
     rank)
       timeout -k 10 600 python tools/c4_rank_cost.py > $O/c4_rank_cost.log 2>&1 || fail $step $? $O/c4_rank_cost.log
       tail -1 $O/c4_rank_cost.log ;;
