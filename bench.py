@@ -241,9 +241,14 @@ def _profiled(cfg: str, kname: str, k_ms: float) -> dict:
         return {}
     if not d or d.get("kernel") != kname or "hbm_bytes_per_stage" not in d:
         return {}
-    from hnumo.roofline import HBM_PEAK_GBS
+    from hnumo.roofline import HBM_PEAK_GBS, kernel_src_sha16
+    cur = kernel_src_sha16()
+    if d.get("kernel_src_sha16") != cur:
+        # a summary taken from other kernel sources is not this kernel's traffic
+        return {"traffic_stale": f"{d['source']} was measured on kernel sources {d.get('kernel_src_sha16')}, "
+                                 f"these are {cur}: PMC fields omitted"}
     dram = d["hbm_bytes_per_stage"] / (k_ms * 1e-3) / 1e9
-    return {"traffic": d["hbm_bytes_per_stage"], "traffic_source": d["source"],
+    return {"traffic": d["hbm_bytes_per_stage"], "traffic_source": f"{d['source']} (kernel sources {cur})",
             "rocprof_stage_us": d["stage_us"], "traffic_over_algorithmic": d["traffic_over_algorithmic"],
             "dram_achieved": round(dram, 1), "dram_frac": round(dram / HBM_PEAK_GBS, 4)}
 

@@ -218,22 +218,12 @@ struct Launch {
       return;
     }
     if constexpr (NGL == 5) {
-      if (e->summation == HNUMO_SUM_REFERENCE && e->stage_nb == 5) {
-        if (stop)
-          hipExtLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, 5>), dim3(n), dim3(StageCfg<NGL, NQ, false, 5>::BS),
-                                0, st, nullptr, stop, 0, a);
+      // the LEAN arenas of large meshes (StageCfg NBK workgroups per CU; HNUMO_STAGE_NB)
+      if (e->summation == HNUMO_SUM_REFERENCE && (e->stage_nb == 4 || e->stage_nb == 5)) {
+        if (e->stage_nb == 5)
+          launch_nb<5>(n, st, stop, a);
         else
-          hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, 5>), dim3(n), dim3(StageCfg<NGL, NQ, false, 5>::BS), 0,
-                             st, a);
-        return;
-      }
-      if (e->summation == HNUMO_SUM_REFERENCE && e->stage_nb == 4) {
-        if (stop)
-          hipExtLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, 4>), dim3(n), dim3(StageCfg<NGL, NQ, false, 4>::BS),
-                                0, st, nullptr, stop, 0, a);
-        else
-          hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, 4>), dim3(n), dim3(StageCfg<NGL, NQ, false, 4>::BS), 0,
-                             st, a);
+          launch_nb<4>(n, st, stop, a);
         return;
       }
     }
@@ -242,6 +232,14 @@ struct Launch {
     else
       hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, true>), dim3(n), dim3(StageCfg<NGL, NQ, true>::BS), 0, st, a);
     if (stop) (void)hipEventRecord(stop, st);
+  }
+  template <int NB>
+  static void launch_nb(int n, hipStream_t st, hipEvent_t stop, const StageArgs &a) {
+    using K = StageCfg<NGL, NQ, false, NB>;
+    if (stop)
+      hipExtLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, NB>), dim3(n), dim3(K::BS), 0, st, nullptr, stop, 0, a);
+    else
+      hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, NB>), dim3(n), dim3(K::BS), 0, st, a);
   }
   static void subcycle(hnumo_engine *e, const StageArgs *stages, int ns) {
     SubArgs sa{stages, ns, e->epoch, e->sub_done, e->sub_arrive, e->neg_flag, e->dbg_abort_epoch};
@@ -808,17 +806,19 @@ static void launch_subcycle(hnumo_engine *e, double *dst, const double *qp, bool
     std::vector<StageArgs> st;
     cur = stage_table(e, qp, st);
     if (timed && e->kernel_events) (void)hipEventRecord(e->evk0, e->stream);
+    // (stop events: each launch signals its own completion, no record packet between the
+    // interior launches; HNUMO_SCHED_DBG 2, diagnostics builds, restores the recorded events for A/B)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(e->stream, &cap);
+    const bool sev = !(e->sched_dbg & 2) && e->ev_Bs[0] && cap == hipStreamCaptureStatusNone;
+    // ev_fork orders stream2 after the sub-cycle input's traces (grad_trace, trace_exchange above):
+    // that is B_0's whole dependency, so B_0 waits for nothing else
     (void)hipEventRecord(e->ev_fork, e->stream);
     (void)hipStreamWaitEvent(e->stream2, e->ev_fork, 0);
-    (void)hipEventRecord(e->ev_I, e->stream);
+    if (!sev) (void)hipEventRecord(e->ev_I, e->stream);
     for (size_t i = 0; i < st.size(); i++) {
       StageArgs a = st[i];
-      // (stop events: each launch signals its own completion, no record packet between the
-      // interior launches; HNUMO_SCHED_DBG 2 restores the recorded events for A/B)
-      hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-      (void)hipStreamIsCapturing(e->stream, &cap);
-      const bool sev = !(e->sched_dbg & 2) && e->ev_Bs[0] && cap == hipStreamCaptureStatusNone;
-      (void)hipStreamWaitEvent(e->stream2, sev ? e->ev_Is : e->ev_I, 0);
+      if (i > 0 || !sev) (void)hipStreamWaitEvent(e->stream2, sev ? e->ev_Is : e->ev_I, 0);
       a.elist = e->d_elB;
       DISPATCH(e, stage(e, a, e->nB, e->stream2, sev ? e->ev_Bs[i & 1] : nullptr));
       if (!sev) (void)hipEventRecord(e->ev_B[i & 1], e->stream2);
@@ -1329,10 +1329,12 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   eng->neg_flag = dalloc<int>(eng, 1);
   if (const char *sm = getenv("HNUMO_SUMMATION"))
     eng->summation = (sm[0] == 'r' || sm[0] == '0') ? HNUMO_SUM_REFERENCE : HNUMO_SUM_FACTORED;
-  if (const char *sd = getenv("HNUMO_STAGE_DBG")) eng->stage_dbg = atoi(sd);
+  if (HNUMO_DIAG)  // (diagnostics builds only; see engine_internal.h)
+    if (const char *sd = getenv("HNUMO_STAGE_DBG")) eng->stage_dbg = atoi(sd);
   if (const char *fz = getenv("HNUMO_FUSE")) eng->no_fuse = fz[0] == '0';
   // (bit 1 drops a required stream dependency -- wrong results, timing only: diagnostics builds)
-  if (const char *sd = getenv("HNUMO_SCHED_DBG")) eng->sched_dbg = atoi(sd) & (HNUMO_DBG_EXTRA ? ~0 : ~1);
+  if (HNUMO_DIAG)
+    if (const char *sd = getenv("HNUMO_SCHED_DBG")) eng->sched_dbg = atoi(sd);
   // per-stage kernel arena: on meshes that take several residency rounds per stage, the arena
   // sized for 4 workgroups per CU (1-row term chunks) -- 1.566 -> 1.517 ms per stage at C4
   // (tools/ab_env.py, round 2); small meshes keep the 3-per-CU arena
@@ -1344,7 +1346,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     const char *qv = getenv("HNUMO_QPQ");
     if (par->botfr && !(qv && atoi(qv) == 0)) eng->qpq = dalloc<double>(eng, (size_t)E * 3 * eng->nq * eng->nq);
   }
-  if (const char *sp = getenv("HNUMO_STAGE_PROF"))
+  if (const char *sp = HNUMO_DIAG ? getenv("HNUMO_STAGE_PROF") : nullptr)
     if (sp[0] == '1') eng->stage_prof = dalloc<unsigned long long>(eng, (size_t)eng->nelem * 32);
   if (eng->face_halo) {
     eng->rank = halo->rank;
@@ -1658,8 +1660,10 @@ static int launch_steps(hnumo_engine *eng, int nsteps) {
   return 0;
 }
 
-static int run_steps(hnumo_engine *eng, int nsteps) {
-  int rc = maybe_reprobe(eng);
+// (retry: the per-stage repeat of a run whose persistent launch gave up -- it does not count as a
+// run of the back-off wait that abort just set)
+static int run_steps(hnumo_engine *eng, int nsteps, bool retry = false) {
+  int rc = retry ? 0 : maybe_reprobe(eng);
   if (rc) return rc;
   const bool pers = use_persistent(eng);
   HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
@@ -1677,7 +1681,7 @@ static int run_steps(hnumo_engine *eng, int nsteps) {
     // an error of a step that completed before the abort is reported, not cleared by the retry
     if ((rc = flag_error(eng, *eng->h_neg & ~RUN_ABORT))) return rc;
     persistent_abort(eng);
-    return done < nsteps ? run_steps(eng, nsteps - done) : 0;
+    return done < nsteps ? run_steps(eng, nsteps - done, true) : 0;
   }
   if (pers) eng->persist_backoff = 1;  // a completed persistent run
   return flag_error(eng, *eng->h_neg);
@@ -1822,6 +1826,7 @@ int hnumo_ti_barotropic_ssprk(hnumo_engine *eng, double *qb_df, const double *qp
     if (!(*eng->h_neg & RUN_ABORT) || !use_persistent(eng)) break;
     persistent_abort(eng);  // (the launch did no work: qb is still the input)
   }
+  if (use_persistent(eng)) eng->persist_backoff = 1;  // a completed persistent run
   if ((rc = flag_error(eng, *eng->h_neg & ~RUN_ABORT))) return rc;
   launch_copy(eng, eng->qb, eng->qbp, 4 * (size_t)eng->npoin);
   return download_state(eng, nullptr, qb_df, nullptr);
@@ -1845,6 +1850,7 @@ int hnumo_predict(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime
     if (!(*eng->h_neg & RUN_ABORT) || !use_persistent(eng)) break;
     persistent_abort(eng);  // (the predictor writes only q_df2, qbp, qprime_df2: redo it)
   }
+  if (use_persistent(eng)) eng->persist_backoff = 1;  // a completed persistent run
   if ((rc = flag_error(eng, *eng->h_neg & ~RUN_ABORT))) return rc;
   const size_t n3 = 3 * (size_t)eng->npoin * eng->L;
   HIPCHK(hipMemcpyAsync(q_df, eng->q2, n3 * 8, hipMemcpyDeviceToHost, eng->stream));
@@ -2094,7 +2100,9 @@ int hnumo_time_stage_kernel(hnumo_engine *eng, int nsubcycles, double *ms_kernel
 
 int hnumo_debug_stage_profile(hnumo_engine *eng, uint64_t *out, int64_t n) {
   if (!eng || !out) return HNUMO_ERR_INVALID;
-  if (!eng->stage_prof) return fail(eng, HNUMO_ERR_INVALID, "engine created without HNUMO_STAGE_PROF=1");
+  if (!eng->stage_prof)
+    return fail(eng, HNUMO_ERR_INVALID, HNUMO_DIAG ? "engine created without HNUMO_STAGE_PROF=1"
+                                                   : "phase clocks: diagnostics builds only (-DHNUMO_DIAG=1)");
   if (n < (int64_t)eng->nelem * 32) return fail(eng, HNUMO_ERR_INVALID, "buffer too small");
   HIPCHK(hipSetDevice(eng->device));
   HIPCHK(hipStreamSynchronize(eng->stream));
@@ -2233,19 +2241,46 @@ int hnumo_step_breakdown(hnumo_engine *eng, int nsteps, char *names, int64_t nam
 
 // ------------------------------------------------------------------ stream-copy bandwidth
 // The measured HBM denominator of the roofline: a grid-stride 16-byte copy,
-// four independent loads in flight per thread before their stores.
-__global__ void __launch_bounds__(256) stream_copy_kernel(const uint4 *__restrict__ src, uint4 *__restrict__ dst,
+// four independent loads in flight per thread before their stores; NT: non-temporal loads and
+// stores (the streaming policy); and a one-pass form (stream_copy_pass_kernel).  hnumo_stream_copy_bw
+// reports the fastest.
+typedef unsigned copy_v4u __attribute__((ext_vector_type(4)));
+template <bool NT>
+__global__ void __launch_bounds__(256) stream_copy_kernel(const copy_v4u *__restrict__ src, copy_v4u *__restrict__ dst,
                                                           size_t n) {
   const size_t s = (size_t)gridDim.x * blockDim.x;
   size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  auto ld = [&](size_t k) -> copy_v4u { return NT ? __builtin_nontemporal_load(src + k) : src[k]; };
+  auto st = [&](size_t k, copy_v4u v) {
+    if (NT)
+      __builtin_nontemporal_store(v, dst + k);
+    else
+      dst[k] = v;
+  };
   for (; i + 3 * s < n; i += 4 * s) {
-    const uint4 a = src[i], b = src[i + s], c = src[i + 2 * s], d = src[i + 3 * s];
-    dst[i] = a;
-    dst[i + s] = b;
-    dst[i + 2 * s] = c;
-    dst[i + 3 * s] = d;
+    const copy_v4u a = ld(i), b = ld(i + s), c = ld(i + 2 * s), d = ld(i + 3 * s);
+    st(i, a);
+    st(i + s, b);
+    st(i + 2 * s, c);
+    st(i + 3 * s, d);
   }
-  for (; i < n; i += s) dst[i] = src[i];
+  for (; i < n; i += s) st(i, ld(i));
+}
+
+// one pass: every block copies its own contiguous 16 KiB (4 x 256 lanes x 16 B), grid = n / 1024
+__global__ void __launch_bounds__(256) stream_copy_pass_kernel(const copy_v4u *__restrict__ src,
+                                                               copy_v4u *__restrict__ dst, size_t n) {
+  const size_t b = (size_t)blockIdx.x * 1024 + threadIdx.x;
+  if (b + 768 < n) {
+    const copy_v4u x0 = __builtin_nontemporal_load(src + b), x1 = __builtin_nontemporal_load(src + b + 256),
+                   x2 = __builtin_nontemporal_load(src + b + 512), x3 = __builtin_nontemporal_load(src + b + 768);
+    __builtin_nontemporal_store(x0, dst + b);
+    __builtin_nontemporal_store(x1, dst + b + 256);
+    __builtin_nontemporal_store(x2, dst + b + 512);
+    __builtin_nontemporal_store(x3, dst + b + 768);
+  } else {
+    for (size_t k = b; k < n && k < b + 1024 - threadIdx.x; k += 256) dst[k] = src[k];
+  }
 }
 
 extern "C" int hnumo_stream_copy_bw(int device, int64_t bytes, int reps, double *gbs_out2) {
@@ -2262,23 +2297,31 @@ extern "C" int hnumo_stream_copy_bw(int device, int64_t bytes, int reps, double 
     int ncu = 256;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
     const unsigned grid = (unsigned)std::min<size_t>((size_t)ncu * 16, (n + 255) / 256);
-    double best = 0.0, sum = 0.0;
+    double best[3] = {0.0, 0.0, 0.0}, sum[3] = {0.0, 0.0, 0.0};
     bool ok = true;
-    for (int r = -2; r < reps && ok; r++) {  // (two untimed warm-ups)
+    for (int r = -3; r < 3 * reps && ok; r++) {  // (three untimed warm-ups; the variants rotate)
+      const int v = (r + 3) % 3;
       ok = hipEventRecord(e0, st) == hipSuccess;
-      hipLaunchKernelGGL(stream_copy_kernel, dim3(grid), dim3(256), 0, st, (const uint4 *)a, (uint4 *)b, n);
+      if (v == 2)
+        hipLaunchKernelGGL(stream_copy_pass_kernel, dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, st,
+                           (const copy_v4u *)a, (copy_v4u *)b, n);
+      else if (v == 1)
+        hipLaunchKernelGGL(stream_copy_kernel<true>, dim3(grid), dim3(256), 0, st, (const copy_v4u *)a, (copy_v4u *)b, n);
+      else
+        hipLaunchKernelGGL(stream_copy_kernel<false>, dim3(grid), dim3(256), 0, st, (const copy_v4u *)a, (copy_v4u *)b, n);
       ok = ok && hipEventRecord(e1, st) == hipSuccess && hipEventSynchronize(e1) == hipSuccess;
       float ms = 0.f;
       ok = ok && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms > 0.f;
       if (ok && r >= 0) {
         const double g = 2.0 * (double)(n * 16) / (ms * 1e-3) / 1e9;
-        best = std::max(best, g);
-        sum += g;
+        best[v] = std::max(best[v], g);
+        sum[v] += g;
       }
     }
     if (ok && hipGetLastError() == hipSuccess) {
-      gbs_out2[0] = best;
-      gbs_out2[1] = sum / reps;
+      const int w = (best[1] > best[0]) ? (best[2] > best[1] ? 2 : 1) : (best[2] > best[0] ? 2 : 0);
+      gbs_out2[0] = best[w];
+      gbs_out2[1] = sum[w] / reps;
       rc = 0;
     }
   }

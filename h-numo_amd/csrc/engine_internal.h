@@ -28,6 +28,13 @@
 //                                     facc [E][4][FA_N][NQ], gfacc [E][4][8][NGL]
 //                                     (face slots e*4+lf of the face's left element, or of its
 //                                     right element when the left one is a ghost: fslotA)
+// HNUMO_DIAG=1 (HNUMO_EXTRA_FLAGS=-DHNUMO_DIAG=1 csrc/build.sh): the diagnostics build -- phase
+// switches and phase clocks of the stage kernels (HNUMO_STAGE_DBG, HNUMO_STAGE_PROF), the two-stream
+// schedule's timing switches (HNUMO_SCHED_DBG), the element kernels' phase clocks (HNUMO_BCL_PROF).
+// Timing experiments only: most switches break the physics.  The product build reads none of them.
+#ifndef HNUMO_DIAG
+#define HNUMO_DIAG 0
+#endif
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

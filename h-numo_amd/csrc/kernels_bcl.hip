@@ -26,7 +26,7 @@ namespace hnumo {
 // [kernel][block][8]: marks 0..5 clock64 at the phase boundaries of thread 0, 6/7 wall clock
 // at its start / end (read by hnumo_bcl_prof; tools/bcl_profile.py)
 #ifndef HNUMO_BCL_PROF
-#define HNUMO_BCL_PROF 0
+#define HNUMO_BCL_PROF HNUMO_DIAG
 #endif
 #if HNUMO_BCL_PROF
 __device__ unsigned long long g_bcl_prof[4][8192][8];

@@ -61,11 +61,6 @@
 #ifndef HNUMO_QPM
 #define HNUMO_QPM 1
 #endif
-// diagnostics builds only (timing; wrong results): N=7 volume sums without their quad-point
-// LDS reads (1: the integrand factors and weight, 2: also the metric terms; profiles/r04x2)
-#ifndef HNUMO_SUMX
-#define HNUMO_SUMX 0
-#endif
 // E (EW0 == 0): the new state's grad(u_bar) on four waves, one component each (nodal_grad, the
 // same terms and order as nodal_grad4's), after a barrier, instead of on the E1 wave alone
 #ifndef HNUMO_EGRAD4
@@ -84,20 +79,6 @@
 // per (component, node) for the whole volume integral (its partial sum in a register)
 #ifndef HNUMO_VSUM
 #define HNUMO_VSUM 1
-#endif
-// VSUM's node halves in the LEAN arenas too (0: one term task forms all NGL nodes of its (i, q) --
-// fewer wave-iterations and task set-ups per phase, a longer lane)
-#ifndef HNUMO_LEAN_VHALF
-#define HNUMO_LEAN_VHALF 1
-#endif
-// node groups of the LEAN arenas' term tasks (2: the VSUM halves; 3: thirds -- more, shorter
-// term lanes: the D phases' waves closer in length, at more set-ups)
-#ifndef HNUMO_LEAN_NSPLIT
-#define HNUMO_LEAN_NSPLIT 2
-#endif
-// VPACK (LEAN): the 3P summing chains on as few waves as they fill (see StageCfg::VPACK)
-#ifndef HNUMO_VPACK
-#define HNUMO_VPACK 0
 #endif
 // The lean per-stage arenas of large meshes (StageCfg::LEAN); 0 keeps the round-2 layout for A/B.
 #ifndef HNUMO_LEAN
@@ -123,13 +104,15 @@
 #ifndef HNUMO_PRIO_B
 #define HNUMO_PRIO_B 1
 #endif
-// diagnostics builds only (-DHNUMO_DBG_EXTRA=1, instruction-mix ablations: tools/pmc_ablate.sh):
-// more phase switches in StageArgs::dbg -- 128 A2 interpolations, 256 B quad-point tasks, 512 B
-// face tasks, 1024 B nodal tasks, 2048 E2 trace stores, 4096 the A copies of the records
-#ifndef HNUMO_DBG_EXTRA
-#define HNUMO_DBG_EXTRA 0
-#endif
-#define DBGX(bit) (HNUMO_DBG_EXTRA && (a.dbg & (bit)))
+// Diagnostics (HNUMO_DIAG builds only, engine_internal.h; timing experiments, most break the
+// physics): StageArgs::dbg phase switches -- 1 the face lifts of the volume sums, 2 the Laplacian,
+// 4 the volume sums, 16 the persistent trace waits, 32 the time averages (engine), 64 the term
+// tasks, 128 A2 interpolations, 256 B quad-point tasks, 512 B face tasks, 1024 B nodal tasks,
+// 2048 E2 trace stores, 4096 the A copies of the records (tools/dbg_sweep.py, tools/pmc_ablate.sh)
+// -- and StageArgs::prof, the per-element phase clocks (tools/stage_profile.py)
+#define DBG(bit) (HNUMO_DIAG && (a.dbg & (bit)))
+#define DBGX(bit) DBG(bit)
+#define PROF (HNUMO_DIAG && a.prof)
 #define SETPRIO_IF(cond, hi, lo)        \
   do {                                  \
     if (cond)                           \
@@ -377,17 +360,10 @@ struct StageCfg {
   static constexpr int OVS = BS - 3 * P;
   static constexpr bool VSUM = HNUMO_VSUM && !SF && !OTF && 2 * WTMAX <= OVS &&
                                2 * WTMAX + P <= BS && OL >= 2 * WTMAX + P && OL + 4 * NGL <= BS;
-  // VHALF: the node-half split of the term tasks (VSUM; the LEAN arenas per HNUMO_LEAN_VHALF)
-  static constexpr bool VHALF = VSUM && (!LEAN || HNUMO_LEAN_VHALF);
-  // NSPLIT: node groups of the term tasks, task t = (group t / WTMAX, task t % WTMAX) on thread t
-  static constexpr int NSPLIT0 = !VHALF ? 1 : (LEAN ? HNUMO_LEAN_NSPLIT : 2);
-  static constexpr int NSPLIT = (NSPLIT0 > 2 && NSPLIT0 * WTMAX + P > OVS) ? 2 : NSPLIT0;
-  // VPACK (LEAN): summing chains [0, 64) on the last wave, chains [64, 3P) on the lanes of wave 1
-  // past its term tasks ([2*WTMAX, ...)), instead of [OVS, BS): there the wave below the last held
-  // only 3P - 64 chains and issued every sum instruction for them (C4: 11 of 64 lanes)
-  static constexpr int VCH_HI = BS - 64, VCH_LO = NSPLIT * WTMAX;
-  static constexpr bool VPACK = HNUMO_VPACK && LEAN && VSUM && 3 * P > 64 && VCH_LO >= 64 &&
-                                VCH_LO + 3 * P - 64 <= 128 && VCH_LO + 3 * P - 64 <= VCH_HI;
+  // NSPLIT: node groups of the term tasks (VSUM: two node halves), task t = (group t / WTMAX,
+  // task t % WTMAX) on thread t.  (Measured, not kept: one group in the LEAN arenas, thirds, and the
+  // summing chains packed onto fewer waves -- DESIGN.md §9.)
+  static constexpr int NSPLIT = VSUM ? 2 : 1;
   // (LEAN: the rhs is written only in the last D phase, by the VSUM lanes)
   static_assert(!LEAN || (VSUM && TSZ >= 32 * NQ && TSZ >= 5 * P && 3 * P <= 64 * EW + 64), "LEAN layout");
   static constexpr int TB_LAST = (NCH & 1) ? TB1 : TB0, TB_PREV = (NCH & 1) ? TB0 : TB1;
@@ -482,7 +458,7 @@ __device__ __forceinline__ void for_tasks(int tid, int o, int n, F &&f) {
 }
 
 #define STAGE_MARK(k) \
-  if (a.prof && tid == 0) s_prof[k] = clock64();
+  if (PROF && tid == 0) s_prof[k] = clock64();
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for
 // its outstanding global stores (accumulators / outputs are read by later kernels only),
@@ -565,14 +541,14 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   double *s_ec = SI + C::B_EC;     // [4][EFC]
 
   // ------------------------------------------------------------- A: async loads
-  if (a.prof && tid == 0) s_prof[30] = wall_clock64();
-  if (a.prof && (tid & 63) == 0) {
+  if (PROF && tid == 0) s_prof[30] = wall_clock64();
+  if (PROF && (tid & 63) == 0) {
     s_prof[16 + (tid >> 6)] = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_ID
     if (tid == 0) s_prof[20] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
   }
   STAGE_MARK(0);
   if (HNUMO_PRIO) __builtin_amdgcn_s_setprio(HNUMO_PRIO_B);
-  if (a.prof && tid == 0) s_prof[22] = 0;
+  if (PROF && tid == 0) s_prof[22] = 0;
   const bool use_q0 = !a.rhs_only && a.a1 != 0.0, use_q2 = !a.rhs_only && a.a3 != 0.0;
   const int qpm = (SF || !m.botfr || !a.qpq) ? 0 : a.qpq_mode;  // see StageArgs::qpq
   if (!DBGX(4096)) {
@@ -710,7 +686,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   auto poll_traces = [&]() {
     if constexpr (PERSIST) {
       const unsigned long long want = (ep << 20) | a.tag_in;
-      const unsigned long long c0 = a.prof ? clock64() : 0;
+      const unsigned long long c0 = PROF ? clock64() : 0;
       for (int t = tid; t < 32 * NGL; t += BS) {
         bool w_ = GR1 ? gwant : s_bc[t / (8 * NGL)] > 0;
         if (!w_) continue;
@@ -724,7 +700,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           ld_granule(g, v, tag);
         }
         unsigned spins = 0;
-        while (tag != want && !(a.dbg & 16)) {
+        while (tag != want && !DBG(16)) {
           __builtin_amdgcn_s_sleep(1);
           ld_granule(g, v, tag);
           if (++spins > (1u << 20)) {  // never expected: report instead of hanging the GPU
@@ -734,7 +710,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         }
         s_tr[t] = v;
       }
-      if (a.prof) atomicMax(&s_prof[22], clock64() - c0);  // longest trace wait of the stage
+      if (PROF) atomicMax(&s_prof[22], clock64() - c0);  // longest trace wait of the stage
     }
   };
   // SLATE: the last wave loads every granule of the element (NGR per lane) and checks them in D
@@ -754,7 +730,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   auto poll_wave = [&]() {
     if constexpr (PERSIST && C::SLATE) {
       const unsigned long long want = (ep << 20) | a.tag_in;
-      const unsigned long long c0 = a.prof ? clock64() : 0;
+      const unsigned long long c0 = PROF ? clock64() : 0;
 #pragma unroll
       for (int k = 0; k < C::NGR; k++) {
         const int t = (tid & 63) + 64 * k;
@@ -762,7 +738,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         double v = __builtin_bit_cast(double, ((unsigned long long)gxr[k][1] << 32) | gxr[k][0]);
         unsigned long long tag = ((unsigned long long)gxr[k][3] << 32) | gxr[k][2];
         unsigned spins = 0;
-        while (tag != want && !(a.dbg & 16)) {
+        while (tag != want && !DBG(16)) {
           __builtin_amdgcn_s_sleep(1);
           ld_granule(a.gtr_in + (size_t)e * 32 * NGL + t, v, tag);
           if (++spins > (1u << 20)) {  // never expected: report instead of hanging the GPU
@@ -772,7 +748,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         }
         s_tr[t] = v;
       }
-      if (a.prof) atomicMax(&s_prof[22], clock64() - c0);
+      if (PROF) atomicMax(&s_prof[22], clock64() - c0);
     }
   };
   if constexpr (!C::SLATE) issue_granule();
@@ -1220,7 +1196,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       }
     }
   }
-  if (a.prof && (tid & 63) == 0) s_prof[12 + (tid >> 6)] = clock64();
+  if (PROF && (tid & 63) == 0) s_prof[12 + (tid >> 6)] = clock64();
   LDS_BARRIER();
   STAGE_MARK(2);
 
@@ -1510,22 +1486,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           double pi, dpi;
           PDQ(bi + iq, pi, dpi);
           const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
-          if constexpr (HNUMO_SUMX == 2) {  // (diagnostics: no quad-point LDS reads at all)
-            const double x = (double)q, dhdx = h_e * x + h_n * x, dhdy = h_e * x + h_n * x;
-            a0 = a0 + x * (dhdx * x + x * dhdy);
-            a1 = a1 + x * ((hi * x + dhdx * x) + x * dhdy);
-            a2 = a2 + x * ((hi * x + dhdx * x) + x * dhdy);
-            continue;
-          }
           const double dhdx = h_e * QK(QE_EX, q) + h_n * QK(QE_NX, q);
           const double dhdy = h_e * QK(QE_EY, q) + h_n * QK(QE_NY, q);
-          if constexpr (HNUMO_SUMX == 1) {  // (diagnostics: the quad-point values from registers)
-            const double x = (double)q;
-            a0 = a0 + x * (dhdx * x + x * dhdy);
-            a1 = a1 + x * ((hi * x + dhdx * x) + x * dhdy);
-            a2 = a2 + x * ((hi * x + dhdx * x) + x * dhdy);
-            continue;
-          }
           const double w = QW(q), uv = QO(4, q);
           a0 = a0 + w * (dhdx * QO(0, q) + QO(1, q) * dhdy);
           a1 = a1 + w * ((hi * QO(2, q) + dhdx * QO(3, q)) + uv * dhdy);
@@ -1550,16 +1512,16 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
             s_rhs[P + tid] = a1_;  // (lifted after the barrier by waves 1 and 2)
             s_rhs[2 * P + tid] = a2_;
           }
-          if (a.prof && tid == 0) s_prof[28] = clock64();
+          if (PROF && tid == 0) s_prof[28] = clock64();
         } else if constexpr (C::OPAIR && (!PERSIST || HNUMO_OPAIR_PERSIST)) {
           if (tid < P)
             acc_r = otf_sum0(tid);
           else if (tid >= 64 && tid < 64 + P)
             otf_sum12(tid - 64, acc_r, acc_r2);
-          if (a.prof && tid == 0) s_prof[28] = clock64();
+          if (PROF && tid == 0) s_prof[28] = clock64();
         } else if constexpr (C::SLATE) {
           if (tid < 3 * P) acc_r = otf_sum(tid);
-          if (a.prof && tid == 0) s_prof[28] = clock64();
+          if (PROF && tid == 0) s_prof[28] = clock64();
         } else {
           for (int t = tid; t < 3 * P; t += C::EW * 64) otf_task(t, true);
         }
@@ -1599,12 +1561,12 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         }
         if (p < 4 * NGL) ldg_task(p, false);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (p < P && !(a.dbg & 2)) {
+        if (p < P && !DBG(2)) {
           r_lap[0] = lap_val(0, p);
           r_lap[1] = lap_val(1, p);
         }
         if constexpr (C::SLATE) load_e1();
-        if (a.prof && p == 0) s_prof[23] = clock64();  // (the last wave's D work done)
+        if (PROF && p == 0) s_prof[23] = clock64();  // (the last wave's D work done)
       }
       if constexpr (C::SLATE) {
         LDS_BARRIER();  // the face fluxes are in
@@ -1720,7 +1682,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
             for (int v = 0; v < 3; v++) acc[v] = acc[v] + tv[v][qi - q0];
           }
       }
-      if (k == NCH - 1 && !(a.dbg & 1)) {
+      if (k == NCH - 1 && !DBG(1)) {
         // face projections of the three components, each in the reference order; a face's
         // NQ points are loaded as one batch, and acc - c is formed as acc + (-c) (exact) so
         // only the adds sit on the dependent chain
@@ -1774,7 +1736,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         for (int qi = 0; qi < SBK; qi++)
           if (q0 + qi < nq_k) acc = acc + tv[qi];
       }
-      if (!(a.dbg & 1)) {
+      if (!DBG(1)) {
 #pragma unroll
         for (int kf = 0; kf < 2; kf++) {
           asm volatile("" ::: "memory");
@@ -1807,9 +1769,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     constexpr int OSUM = (P <= 64 && WTMAX <= BS - 64) ? BS - 64 : WTMAX;
     // VSUM: thread OVS + (v*P + p) sums chain (v, p) of every chunk, the partial sum in vacc
     // (VPACK: chain tid - VCH_HI on the last wave, 64 + tid - VCH_LO on wave 1)
-    const int vch = C::VPACK ? (tid >= C::VCH_HI ? tid - C::VCH_HI
-                                                 : (tid >= C::VCH_LO && tid < C::VCH_LO + 3 * P - 64 ? 64 + tid - C::VCH_LO : -1))
-                             : (tid >= C::OVS ? tid - C::OVS : -1);
+    const int vch = tid >= C::OVS ? tid - C::OVS : -1;
     double vacc = 0.0;
     auto vsum_chunk = [&](int k) {
       const int t = vch, v = t / P, p = t - v * P;
@@ -1827,7 +1787,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           if (q0 + qi < nq_k) vacc = vacc + tv[qi];
       }
       if (k == NCH - 1) {
-        if (!(a.dbg & 1)) {  // the face projections of component v (sum_last_v's)
+        if (!DBG(1)) {  // the face projections of component v (sum_last_v's)
 #pragma unroll
           for (int kf = 0; kf < 2; kf++) {
             asm volatile("" ::: "memory");
@@ -1864,7 +1824,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     }
     // the term-task waves behind everything else, the summing waves ahead
     if (HNUMO_PRIO)
-      SETPRIO_IF(C::VPACK ? tid >= C::VCH_HI : VSUM ? tid >= C::OVS - (C::OVS & 63) : (OSUM == BS - 64 && tid >= OSUM),
+      SETPRIO_IF(VSUM ? tid >= C::OVS - (C::OVS & 63) : (OSUM == BS - 64 && tid >= OSUM),
                  HNUMO_PRIO_S, 0);
 #pragma unroll
     for (int k = 0; k <= NCH; k++) {
@@ -1874,13 +1834,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       if constexpr (VSUM) {
         // first node halves on [0, WT), second halves on [WTMAX, WTMAX + WT)
         if ((NSP == 2 ? (tid < WT || (tid >= WTMAX && tid < WTMAX + WT))
-                      : (tid < NSP * WTMAX && tid - (tid / WTMAX) * WTMAX < WT)) && !(a.dbg & 64))
+                      : (tid < NSP * WTMAX && tid - (tid / WTMAX) * WTMAX < WT)) && !DBG(64))
           term_task(k, tid);
-        if (k >= 1 && vch >= 0 && !(a.dbg & 4)) vsum_chunk(k - 1);
+        if (k >= 1 && vch >= 0 && !DBG(4)) vsum_chunk(k - 1);
       } else {
       for_tasks<BS>(tid, 0, WT, [&](int t, bool) { term_task(k, t); });
       if (k >= 1 && k < NCH) for_tasks<BS>(tid, OSUM, P, [&](int t, bool) { sum_task(k - 1, t); });
-      if (k == NCH && !(a.dbg & 4)) {
+      if (k == NCH && !DBG(4)) {
         if constexpr (VSPLIT)
           for_tasks<BS>(tid, OSV, 3 * P, [&](int t, bool) { sum_last_v(t / P, t % P); });
         else
@@ -1889,7 +1849,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       }
       if (k == 0) for_tasks<BS>(tid, VSUM ? C::NSPLIT * WTMAX : WT, P, [&](int t, bool) { qq_task(t); });
       if (k == 0) for_tasks<BS>(tid, C::OL, 4 * NGL, ldg_task);
-      if (k == NCH && !(a.dbg & 2)) for_tasks<BS>(tid, 0, 2 * P, [&](int t, bool) { lap_task(t / P, t % P); });
+      if (k == NCH && !DBG(2)) for_tasks<BS>(tid, 0, 2 * P, [&](int t, bool) { lap_task(t / P, t % P); });
       LDS_BARRIER();
       if (k < (PERSIST ? 2 : 6)) STAGE_MARK(6 + k);  // (persistent: slots 8-11 accumulate the phases)
     }
@@ -2032,7 +1992,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       }
     }
   }
-  if (a.prof) {
+  if (PROF) {
     LDS_BARRIER();
     STAGE_MARK(5);
     if (tid == 0) {
@@ -2059,7 +2019,7 @@ template <int NGL, int NQ, bool SF, int NB = 0>
 __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF, NB>::BS), (StageCfg<NGL, NQ, SF, NB>::MINW))
     btp_stage_kernel(StageArgs a) {
   __shared__ __attribute__((aligned(16))) double s_arena[StageCfg<NGL, NQ, SF, NB>::ARENA];
-  __shared__ unsigned long long s_prof[32];
+  __shared__ unsigned long long s_prof[HNUMO_DIAG ? 32 : 1];
   stage_body<NGL, NQ, SF, false, StageArgs, NB>(a, s_arena, s_prof, true,
                                                 a.elist ? a.elist[blockIdx.x] : (int)blockIdx.x, threadIdx.x);
 }
@@ -2124,7 +2084,7 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
     btp_subcycle_kernel(SubArgs sa) {
   using C = StageCfg<NGL, NQ, SF>;
   __shared__ __attribute__((aligned(16))) double s_arena[C::ARENA];
-  __shared__ unsigned long long s_prof[32];
+  __shared__ unsigned long long s_prof[HNUMO_DIAG ? 32 : 1];
   const int e = blockIdx.x, tid = threadIdx.x;
   const unsigned long long ep = *sa.epoch;
   typedef const __attribute__((address_space(4))) StageArgs CStageArgs;

@@ -22,6 +22,19 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md chip table
 HBM_MEASURED_GBS = 6290.0    # float4 copy measured on MI355X (same table)
 
 
+def kernel_src_sha16() -> str:
+    """sha256[:16] of the stage kernels' sources (csrc/kernels_btp.hip, csrc/engine_internal.h): the
+    key that ties a committed PMC summary (profiles/roofline_pmc.json) to the kernels it measured."""
+    import hashlib
+    import os
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "csrc")
+    h = hashlib.sha256()
+    for f in ("kernels_btp.hip", "engine_internal.h"):
+        with open(os.path.join(d, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def stage_bytes_per_element(nop: int, faces_per_element: float) -> float:
     n, m = nop + 1, 2 * nop + 1
     P, Q = n * n, m * m

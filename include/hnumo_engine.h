@@ -282,7 +282,7 @@ int hnumo_bench_steps(hnumo_engine *eng, int nsteps, double *ms_total,
 int hnumo_time_stage_kernel(hnumo_engine *eng, int nsubcycles, double *ms_kernel_avg);
 
 /* Diagnostics: per-element phase clocks of the last stage launch, [nelem][32] uint64
- * (engine created with HNUMO_STAGE_PROF=1 in the environment).                        */
+ * (diagnostics builds, -DHNUMO_DIAG=1, with HNUMO_STAGE_PROF=1 in the environment).   */
 int hnumo_debug_stage_profile(hnumo_engine *eng, uint64_t *out, int64_t n);
 
 /* Per-kernel breakdown of a step (ABI v8; single-rank engines, resident uploaded state):
@@ -294,7 +294,9 @@ int hnumo_step_breakdown(hnumo_engine *eng, int nsteps, char *names, int64_t nam
                          double *us_per_step, int max_kernels, int *count);
 
 /* Stream-copy bandwidth of `device` (ABI v8): a 16-byte grid-stride copy kernel between two
- * buffers of `bytes` each, `reps` timed launches after two warm-ups; out2 = {best, mean}
+ * buffers of `bytes` each, `reps` timed launches per variant (grid-stride default and non-temporal,
+ * one-pass non-temporal) after three
+ * warm-ups; out2 = {best, mean} of the fastest variant,
  * GB/s counting bytes read + written.  The measured denominator of the roofline.        */
 int hnumo_stream_copy_bw(int device, int64_t bytes, int reps, double *out2);
 

@@ -1,12 +1,13 @@
 """C4 (BASELINE.json configs[3]): the double gyre at ~1e5 elements (316x316, N=4, 3 layers,
 dt=40 s, dt_btp=2 s), the size the 8-GPU metric is quoted on.
 
-The oracle needs the reference's dense psih/dpsidx tables (~5 GB at this size) and minutes
-per step, so at full size the checks are size-independent properties (finite state, per-layer
-mass conserved to the reference CI's 1e-12, CI/bump/check.F90:58) plus the multi-rank
-identity: the 8-way domain decomposition (4x2 blocks of 79x158 elements, ghost halo, local
-exchange group on this one GPU) reproduces the single-rank engine bit for bit.  Parity of the
-arithmetic itself is pinned at small sizes (test_engine_gpu.py)."""
+Parity at full size is pinned against the reference Fortran itself: the fixture
+dg316L3_mpi8b_step1 (the reference under mpiexec -n 8 on the 4x2 block partition of the 8-GPU
+metric; strided samples + the sha256 of every rank's whole state) runs in
+test_facehalo_gpu.py.  This file adds size-independent properties at full size (finite state,
+per-layer mass conserved to the reference CI's 1e-12, CI/bump/check.F90:58) and the multi-rank
+identity: the 8-way ghost-halo decomposition (4x2 blocks of 79x158 elements, local exchange
+group on this one GPU) reproduces the single-rank engine bit for bit."""
 import numpy as np
 import pytest
 

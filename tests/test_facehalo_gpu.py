@@ -24,6 +24,21 @@ GOLD = os.path.join(HERE, "golden")
                                   # metric); strided samples + sha256 of every rank's whole state
                                   "lake200_mpi4m_step1", "dg316L3_mpi8b_step1"])
 def test_face_halo_matches_reference_mpi(name):
+    _face_halo_run(name)
+
+
+@pytest.mark.parametrize("nb", ["0", "4"])
+def test_face_halo_every_stage_arena_matches_reference_mpi(nb, monkeypatch):
+    """The two-stream schedule's hand-offs are the per-stage launches' own stop events
+    (Launch::stage; a recorded event for the arena without hipExtLaunchKernelGGL): with each
+    other arena forced on a large mesh (HNUMO_STAGE_NB; the default there is the 5-per-CU LEAN
+    arena), C5 at its stated size (10,000 elements per rank) still equals the reference under
+    mpiexec bit for bit on every rank."""
+    monkeypatch.setenv("HNUMO_STAGE_NB", nb)
+    _face_halo_run("lake200_mpi4m_step1")
+
+
+def _face_halo_run(name):
     from util import overrides_of, state_sha256
     from hnumo.case import build_case, make_config
     from hnumo.engine import Engine, group_ti_rk_bcl, local_group

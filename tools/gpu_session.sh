@@ -12,6 +12,10 @@
 #   benchq       the bench line without the CPU baselines
 #   emu8         bench.py --emulate 8:1 (C4 rank 1 of 8) under torch.distributed.run, one process
 #   emu4lake     bench.py --emulate 4:1 --config lake200 (C5 rank 1 of 4) the same way
+#   nb56         tools/ab_env.py: C4 per-stage kernel, LEAN arena for 5 vs 6 workgroups per CU
+#   sprof:<cfg>  tools/stage_profile.py with the diagnostics build diag/libhnumo_diag.so (phase clocks)
+#   abl:<lib>:<cfgs>  tools/ab_stage.py with HNUMO_LIB=<lib> (A/B of builds)
+#   emu:W:R:cfg:order[:warmup:steps]  bench.py --emulate W:R --config cfg --order order
 #   rank         tools/c4_rank_cost.py (C4/8 rank 1 variants)
 #   profiles     tools/gpu_profiles.sh <tag> (kernel trace + FETCH/WRITE + SQ passes)
 #   prof:<cfg>   tools/gpu_profiles.sh <tag> <cfg>
@@ -56,6 +60,24 @@ for step in "$@"; do
     emu4lake2)
       timeout -k 10 600 $TR bench.py --emulate 4:1 --config lake200 --warmup 1 --steps 2 > $O/emu4lake2.json 2> $O/emu4lake2.err || fail $step $? $O/emu4lake2.err
       cat $O/emu4lake2.json ;;
+    nb56)
+      AB_REPS=2 timeout -k 10 600 python -u tools/ab_env.py dg316L3:stage HNUMO_STAGE_NB=5 HNUMO_STAGE_NB=6 > $O/nb56.log 2>&1 || fail $step $? $O/nb56.log
+      cat $O/nb56.log ;;
+    sprof:*)
+      c=${step#sprof:}
+      HNUMO_LIB=diag/libhnumo_diag.so timeout -k 10 300 python -u tools/stage_profile.py $c > $O/sprof_$c.txt 2>&1 || fail $step $? $O/sprof_$c.txt
+      cat $O/sprof_$c.txt ;;
+    abl:*)
+      # abl:<lib>:<cfg>[,<cfg>...]  tools/ab_stage.py with HNUMO_LIB=<lib> (default: the product library)
+      x=${step#abl:}; lib=${x%%:*}; cf=${x#*:}
+      [ "$lib" = default ] && lib=h-numo_amd/libhnumo_engine.so
+      HNUMO_LIB=$lib timeout -k 10 600 python -u tools/ab_stage.py ${cf//,/ } >> $O/abl.log 2>&1 || fail $step $? $O/abl.log
+      tail -4 $O/abl.log ;;
+    emu:*)
+      # emu:W:R:cfg:order[:warmup:steps]  bench.py --emulate W:R under torch.distributed.run
+      IFS=: read -r _ W R cf od wu ns <<< "$step"
+      timeout -k 10 600 $TR bench.py --emulate $W:$R --config $cf --order $od --warmup ${wu:-3} --steps ${ns:-5} > $O/emu_${cf}_${od}.json 2> $O/emu_${cf}_${od}.err || fail $step $? $O/emu_${cf}_${od}.err
+      cat $O/emu_${cf}_${od}.json ;;
     rank)
       timeout -k 10 600 python tools/c4_rank_cost.py > $O/c4_rank_cost.log 2>&1 || fail $step $? $O/c4_rank_cost.log
       tail -1 $O/c4_rank_cost.log ;;

@@ -24,6 +24,8 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "h-numo_amd"))
 
+from hnumo.roofline import kernel_src_sha16  # noqa: E402
+
 STAGE_KERNELS = ("btp_subcycle_kernel", "btp_stage_kernel")
 
 
@@ -67,7 +69,7 @@ def summarize(tag, cfg):
     out = {"config": cfg, "kernel": kname, "kernel_full": full, "stages_per_dispatch": per,
            "dispatches": len(d), "dispatches_excluded": nall - len(d),
            "dispatch_avg_us": round(statistics.mean(d) / 1e3, 3), "stage_us": round(statistics.mean(d) / 1e3 / per, 4),
-           "source": os.path.relpath(dst, REPO)}
+           "source": os.path.relpath(dst, REPO), "kernel_src_sha16": kernel_src_sha16()}
     sb = stage_bytes_cfg(c)
     out["algorithmic_bytes_per_stage"] = int(sb)
     out["achieved_GBs"] = round(sb / (out["stage_us"] * 1e-6) / 1e9, 1)
