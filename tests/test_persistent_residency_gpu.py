@@ -122,9 +122,10 @@ def test_corrector_abort_is_redone_and_path_recovers(case_factory, monkeypatch):
     """The corrector's persistent launch gives up after the predictor's sub-cycle and its
     baroclinic kernels ran (hnumo_debug_force_abort: launch 0 of the step is the predictor's
     sub-cycle, launch 1 the corrector's).  The step is redone on per-stage launches with the
-    reference's bits; the next step re-probes residency with a trial launch, finds the grid
-    resident and runs persistent again -- the same bits as an engine on per-stage launches from
-    the start."""
+    reference's bits; the next step runs on per-stage launches too (the back-off of one run after
+    a first abort, include/hnumo_engine.h), the one after re-probes residency with a trial launch,
+    finds the grid resident and runs persistent again -- the same bits as an engine on per-stage
+    launches from the start."""
     from hnumo.engine import Engine
     g, case = golden_case("dg25L3_step1", case_factory)
     e = Engine(case)
@@ -139,10 +140,10 @@ def test_corrector_abort_is_redone_and_path_recovers(case_factory, monkeypatch):
     e0 = Engine(case)
     monkeypatch.delenv("HNUMO_PERSISTENT")
     a = [x.copy(order="F") for x in (q, qb, qp)]
-    for _ in range(2):
+    for k in range(3):
         e.ti_rk_bcl(q, qb, qp)
         e0.ti_rk_bcl(*a)
-        assert e.stage_path == "persistent"
+        assert e.stage_path == ("per-stage" if k == 0 else "persistent"), (k, e.persistent_stats)
     for x, y in zip((q, qb, qp), a):
         assert np.array_equal(x, y)
     st = e.persistent_stats
