@@ -2297,11 +2297,11 @@ extern "C" int hnumo_stream_copy_bw(int device, int64_t bytes, int reps, double 
     int ncu = 256;
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device);
     const unsigned grid = (unsigned)std::min<size_t>((size_t)ncu * 16, (n + 255) / 256);
-    double best[3] = {0.0, 0.0, 0.0}, sum[3] = {0.0, 0.0, 0.0};
+    // per variant: one untimed launch, then `reps` launches back to back between two events (the
+    // launch gaps amortised: the rate of a steady copy stream)
+    double rate[3] = {0.0, 0.0, 0.0};
     bool ok = true;
-    for (int r = -3; r < 3 * reps && ok; r++) {  // (three untimed warm-ups; the variants rotate)
-      const int v = (r + 3) % 3;
-      ok = hipEventRecord(e0, st) == hipSuccess;
+    auto launch = [&](int v) {
       if (v == 2)
         hipLaunchKernelGGL(stream_copy_pass_kernel, dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, st,
                            (const copy_v4u *)a, (copy_v4u *)b, n);
@@ -2309,19 +2309,20 @@ extern "C" int hnumo_stream_copy_bw(int device, int64_t bytes, int reps, double 
         hipLaunchKernelGGL(stream_copy_kernel<true>, dim3(grid), dim3(256), 0, st, (const copy_v4u *)a, (copy_v4u *)b, n);
       else
         hipLaunchKernelGGL(stream_copy_kernel<false>, dim3(grid), dim3(256), 0, st, (const copy_v4u *)a, (copy_v4u *)b, n);
+    };
+    for (int v = 0; v < 3 && ok; v++) {
+      launch(v);
+      ok = hipEventRecord(e0, st) == hipSuccess;
+      for (int r = 0; r < reps; r++) launch(v);
       ok = ok && hipEventRecord(e1, st) == hipSuccess && hipEventSynchronize(e1) == hipSuccess;
       float ms = 0.f;
       ok = ok && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms > 0.f;
-      if (ok && r >= 0) {
-        const double g = 2.0 * (double)(n * 16) / (ms * 1e-3) / 1e9;
-        best[v] = std::max(best[v], g);
-        sum[v] += g;
-      }
+      if (ok) rate[v] = 2.0 * (double)(n * 16) * reps / (ms * 1e-3) / 1e9;
     }
     if (ok && hipGetLastError() == hipSuccess) {
-      const int w = (best[1] > best[0]) ? (best[2] > best[1] ? 2 : 1) : (best[2] > best[0] ? 2 : 0);
-      gbs_out2[0] = best[w];
-      gbs_out2[1] = sum[w] / reps;
+      const int w = (rate[1] > rate[0]) ? (rate[2] > rate[1] ? 2 : 1) : (rate[2] > rate[0] ? 2 : 0);
+      gbs_out2[0] = rate[w];
+      gbs_out2[1] = (double)w;
       rc = 0;
     }
   }

@@ -231,8 +231,8 @@ class Engine:
 
     @staticmethod
     def stream_copy_bw(device: int = 0, nbytes: int = 1 << 30, reps: int = 10) -> tuple:
-        """(best, mean) GB/s of a 16-byte stream copy between two buffers of nbytes
-        (read + write counted; hnumo_stream_copy_bw)."""
+        """(GB/s, variant) of the fastest 16-byte stream copy between two buffers of nbytes, reps
+        launches back to back (read + write counted; hnumo_stream_copy_bw)."""
         out = (C.c_double * 2)()
         rc = lib().hnumo_stream_copy_bw(device, nbytes, reps, out)
         if rc:

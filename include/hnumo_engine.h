@@ -293,11 +293,11 @@ int hnumo_debug_stage_profile(hnumo_engine *eng, uint64_t *out, int64_t n);
 int hnumo_step_breakdown(hnumo_engine *eng, int nsteps, char *names, int64_t names_len,
                          double *us_per_step, int max_kernels, int *count);
 
-/* Stream-copy bandwidth of `device` (ABI v8): a 16-byte grid-stride copy kernel between two
- * buffers of `bytes` each, `reps` timed launches per variant (grid-stride default and non-temporal,
- * one-pass non-temporal) after three
- * warm-ups; out2 = {best, mean} of the fastest variant,
- * GB/s counting bytes read + written.  The measured denominator of the roofline.        */
+/* Stream-copy bandwidth of `device` (ABI v8): 16-byte copy kernels between two buffers of
+ * `bytes` each -- grid-stride with default and with non-temporal loads/stores, and a one-pass
+ * non-temporal form -- each run `reps` times back to back between two events after one
+ * untimed launch; out2 = {GB/s of the fastest variant (bytes read + written), its index 0..2}.
+ * The measured denominator of the roofline.                                               */
 int hnumo_stream_copy_bw(int device, int64_t bytes, int reps, double *out2);
 
 #ifdef __cplusplus
