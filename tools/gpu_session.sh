@@ -33,53 +33,53 @@ for step in "$@"; do
   echo "[$(date +%T)] $step"
   case $step in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || fail $step $? $O/pytest_gpu.log
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || fail "$step" $? $O/pytest_gpu.log
       tail -1 $O/pytest_gpu.log ;;
     test:*)
       k=${step#test:}
-      timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "$k" > $O/pytest_k.log 2>&1 || fail $step $? $O/pytest_k.log
+      timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "$k" > $O/pytest_k.log 2>&1 || fail "$step" $? $O/pytest_k.log
       tail -1 $O/pytest_k.log ;;
     smoke)
-      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || fail $step $? $O/smoke.log
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || fail "$step" $? $O/smoke.log
       tail -1 $O/smoke.log ;;
     bench)
-      timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err || fail $step $? $O/bench.err
+      timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err || fail "$step" $? $O/bench.err
       cat $O/bench.json ;;
     benchq)
-      timeout -k 10 600 python bench.py --no-cpu-baseline > $O/benchq.json 2> $O/benchq.err || fail $step $? $O/benchq.err
+      timeout -k 10 600 python bench.py --no-cpu-baseline > $O/benchq.json 2> $O/benchq.err || fail "$step" $? $O/benchq.err
       cat $O/benchq.json ;;
     emu8)
-      timeout -k 10 600 $TR bench.py --emulate 8:1 > $O/emu8.json 2> $O/emu8.err || fail $step $? $O/emu8.err
+      timeout -k 10 600 $TR bench.py --emulate 8:1 > $O/emu8.json 2> $O/emu8.err || fail "$step" $? $O/emu8.err
       cat $O/emu8.json ;;
     emu4lake)
-      timeout -k 10 600 $TR bench.py --emulate 4:1 --config lake200 > $O/emu4lake.json 2> $O/emu4lake.err || fail $step $? $O/emu4lake.err
+      timeout -k 10 600 $TR bench.py --emulate 4:1 --config lake200 > $O/emu4lake.json 2> $O/emu4lake.err || fail "$step" $? $O/emu4lake.err
       cat $O/emu4lake.json ;;
     lake1)
-      timeout -k 10 600 python bench.py --config lake200 --no-cpu-baseline --steps 10 > $O/lake1.json 2> $O/lake1.err || fail $step $? $O/lake1.err
+      timeout -k 10 600 python bench.py --config lake200 --no-cpu-baseline --steps 10 > $O/lake1.json 2> $O/lake1.err || fail "$step" $? $O/lake1.err
       cat $O/lake1.json ;;
     emu4lake2)
-      timeout -k 10 600 $TR bench.py --emulate 4:1 --config lake200 --warmup 1 --steps 2 > $O/emu4lake2.json 2> $O/emu4lake2.err || fail $step $? $O/emu4lake2.err
+      timeout -k 10 600 $TR bench.py --emulate 4:1 --config lake200 --warmup 1 --steps 2 > $O/emu4lake2.json 2> $O/emu4lake2.err || fail "$step" $? $O/emu4lake2.err
       cat $O/emu4lake2.json ;;
     nb56)
-      AB_REPS=2 timeout -k 10 600 python -u tools/ab_env.py dg316L3:stage HNUMO_STAGE_NB=5 HNUMO_STAGE_NB=6 > $O/nb56.log 2>&1 || fail $step $? $O/nb56.log
+      AB_REPS=2 timeout -k 10 600 python -u tools/ab_env.py dg316L3:stage HNUMO_STAGE_NB=5 HNUMO_STAGE_NB=6 > $O/nb56.log 2>&1 || fail "$step" $? $O/nb56.log
       cat $O/nb56.log ;;
     sprof:*)
       c=${step#sprof:}
-      HNUMO_LIB=diag/libhnumo_diag.so timeout -k 10 300 python -u tools/stage_profile.py $c > $O/sprof_$c.txt 2>&1 || fail $step $? $O/sprof_$c.txt
+      HNUMO_LIB=diag/libhnumo_diag.so timeout -k 10 300 python -u tools/stage_profile.py $c > $O/sprof_$c.txt 2>&1 || fail "$step" $? $O/sprof_$c.txt
       cat $O/sprof_$c.txt ;;
     abl:*)
       # abl:<lib>:<cfg>[,<cfg>...]  tools/ab_stage.py with HNUMO_LIB=<lib> (default: the product library)
       x=${step#abl:}; lib=${x%%:*}; cf=${x#*:}
       [ "$lib" = default ] && lib=h-numo_amd/libhnumo_engine.so
-      HNUMO_LIB=$lib timeout -k 10 600 python -u tools/ab_stage.py ${cf//,/ } >> $O/abl.log 2>&1 || fail $step $? $O/abl.log
+      HNUMO_LIB=$lib timeout -k 10 600 python -u tools/ab_stage.py ${cf//,/ } >> $O/abl.log 2>&1 || fail "$step" $? $O/abl.log
       tail -4 $O/abl.log ;;
     emu:*)
       # emu:W:R:cfg:order[:warmup:steps]  bench.py --emulate W:R under torch.distributed.run
       IFS=: read -r _ W R cf od wu ns <<< "$step"
-      timeout -k 10 600 $TR bench.py --emulate $W:$R --config $cf --order $od --warmup ${wu:-3} --steps ${ns:-5} > $O/emu_${cf}_${od}.json 2> $O/emu_${cf}_${od}.err || fail $step $? $O/emu_${cf}_${od}.err
+      timeout -k 10 600 $TR bench.py --emulate $W:$R --config $cf --order $od --warmup ${wu:-3} --steps ${ns:-5} > $O/emu_${cf}_${od}.json 2> $O/emu_${cf}_${od}.err || fail "$step" $? $O/emu_${cf}_${od}.err
       cat $O/emu_${cf}_${od}.json ;;
     rank)
-      timeout -k 10 600 python tools/c4_rank_cost.py > $O/c4_rank_cost.log 2>&1 || fail $step $? $O/c4_rank_cost.log
+      timeout -k 10 600 python tools/c4_rank_cost.py > $O/c4_rank_cost.log 2>&1 || fail "$step" $? $O/c4_rank_cost.log
       tail -1 $O/c4_rank_cost.log ;;
     profiles)
       bash tools/gpu_profiles.sh $TAG || exit 1 ;;
@@ -87,7 +87,7 @@ for step in "$@"; do
       bash tools/gpu_profiles.sh $TAG ${step#prof:} || exit 1 ;;
     ab:*)
       a=${step#ab:}
-      timeout -k 10 900 python tools/ab_stage.py ${a//,/ } > $O/ab.log 2>&1 || fail $step $? $O/ab.log
+      timeout -k 10 900 python tools/ab_stage.py ${a//,/ } > $O/ab.log 2>&1 || fail "$step" $? $O/ab.log
       tail -20 $O/ab.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
