@@ -565,6 +565,9 @@ def main():
             if "value" in base:
                 v = value if not emu else gcase.scalars["nelem"] * 2 * S["N_btp"] * S["kstages"] * 1e3 / ms_per_step
                 out["speedup_vs_base"] = round(v / base["value"], 3)
+                # strong-scaling efficiency of THIS workload (the driver's 1 -> N curve divides by the
+                # N=1 line, which is configs[1], a different mesh)
+                out["efficiency_vs_base"] = round(v / base["value"] / nparts, 3)
     if emu:
         E_g = gcase.scalars["nelem"]
         out["emulation"] = {

@@ -41,5 +41,6 @@ def test_bench_n_gt_1_branch_runs_on_one_gpu():
     em = d["emulation"]
     assert em["world"] == 2 and em["rank"] == 1 and em["processor_faces"] > 0 and em["projection_eu_per_s"] > 0
     assert d["strong_scaling_base"]["value"] > 0 and d["speedup_vs_base"] > 0
+    assert abs(d["efficiency_vs_base"] - d["speedup_vs_base"] / 2) < 1e-3
     for k in ("init_process_group_s", "case_build_s", "engine_create_s", "first_step_s", "halocheck_s"):
         assert k in d["setup_s"], k

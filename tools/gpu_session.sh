@@ -67,6 +67,10 @@ for step in "$@"; do
       c=${step#sprof:}
       HNUMO_LIB=diag/libhnumo_diag.so timeout -k 10 300 python -u tools/stage_profile.py $c > $O/sprof_$c.txt 2>&1 || fail "$step" $? $O/sprof_$c.txt
       cat $O/sprof_$c.txt ;;
+    bclprof:*)
+      c=${step#bclprof:}
+      HNUMO_LIB=diag/libhnumo_diag.so timeout -k 10 300 python -u tools/bcl_profile.py $c > $O/bclprof_$c.txt 2>&1 || fail "$step" $? $O/bclprof_$c.txt
+      cat $O/bclprof_$c.txt ;;
     abl:*)
       # abl:<lib>:<cfg>[,<cfg>...]  tools/ab_stage.py with HNUMO_LIB=<lib> (default: the product library)
       x=${step#abl:}; lib=${x%%:*}; cf=${x#*:}
