@@ -1012,13 +1012,18 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   BCL_MARK(0, 0) BCL_WALL(0, 6)
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
   __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
-  __shared__ double s_q[MAXL][3][P];
   __shared__ double s_qm[5][Q];             // e_x, e_y, n_x, n_y, w
   __shared__ double s_f[MAXL][2][Q];        // udp, vdp per layer
   __shared__ double s_adv[MAXL][P];
   __shared__ double s_fw[4 * NQ], s_fx[MAXL][4 * NQ];  // face weights, layer mass fluxes of the 4 faces
-  __shared__ double s_tb[QS::SIZE];                    // quad-sum term buffers
-  __shared__ double s_qfF[4][MAXL][6 * NGL];           // (qf) the four faces' qf blocks
+  // phase 1's nodal layers and (qf) the four faces' qf blocks, then (phase 2, after the barrier
+  // that ends phase 1) the quad-sum term buffers in the same words: at N=7 the element then fits
+  // three workgroups per CU (all 625 of dg25 in one round)
+  constexpr int U1 = MAXL * 3 * P + 4 * MAXL * 6 * NGL;
+  __shared__ double s_un[U1 > QS::SIZE ? U1 : QS::SIZE];
+  double(*s_q)[3][P] = reinterpret_cast<double(*)[3][P]>(s_un);
+  double(*s_qfF)[MAXL][6 * NGL] = reinterpret_cast<double(*)[MAXL][6 * NGL]>(s_un + MAXL * 3 * P);
+  double *s_tb = s_un;
   __shared__ int s_map[4 * NGL], s_face[4], s_side[4];
   // every load of the phase first (Gather), then the LDS stores: the face ids (scalar loads) and
   // the element-major inputs in one round, the face-indexed ones (qf blocks or fluxes, the face
@@ -1727,10 +1732,13 @@ template <int NGL, int NQ>
 struct MomCfg {
   static constexpr int P = NGL * NGL, Q = NQ * NQ;
   static constexpr int BS = 256;
+  // waves per SIMD the registers are sized for: three workgroups per CU; N=7 (82 KB of LDS, GIV):
+  // two, so at most 256 registers a lane in all
+  static constexpr int MINW = NGL >= 8 ? 2 : 3;
 };
 
 template <int NGL, int NQ>
-__global__ void __launch_bounds__(256, 3)
+__global__ void __launch_bounds__(256, (MomCfg<NGL, NQ>::MINW))
     mom_elem_kernel(DevMesh m, const double *qp_in, const double *qacc, const double *nacc, const double *dpp_graduv,
                     const double *dpprime_visc, const double *momL, const double *momR, const double *lapf,
                     const double *qb, const double *q_in, double *q, double *qp_out, int mode, const double *lapx,
@@ -1758,10 +1766,16 @@ __global__ void __launch_bounds__(256, 3)
   // interpolated dp', u', v', u*dp, v*dp per layer (phases 1-2); then the weak forms' term buffers
   using QS = QSumCfg<NQ, P * 2 * MAXL, 2700>;
   constexpr bool QSUM = P * 2 * MAXL <= BS;  // one weak-form sum per thread (ordered_node_sums)
-  constexpr int IVTB = (QSUM && QS::SIZE > MAXL * 5 * Q) ? QS::SIZE : MAXL * 5 * Q;
+  // GIV (no term buffers, N=7): s_G in the words of s_iv.  Both are [row][Q], so the coupling task
+  // of quad point qd, which reads every s_iv value of column qd before it writes s_G's (the QUIRK
+  // row in registers), is the only one touching that column: 108 -> 82 KB, two workgroups per CU
+  constexpr bool GIV = !QSUM;
+  constexpr int IVTB0 = (QSUM && QS::SIZE > MAXL * 5 * Q) ? QS::SIZE : MAXL * 5 * Q;
+  constexpr int IVTB = (GIV && MAXL * 6 * Q > IVTB0) ? MAXL * 6 * Q : IVTB0;
   __shared__ double s_ivtb[IVTB];
   double(*s_iv)[5][Q] = reinterpret_cast<double(*)[5][Q]>(s_ivtb);
-  __shared__ double s_G[MAXL][6][Q];       // source_x, Hq+uu, uv, source_y, vu, Hq+vv
+  __shared__ double s_Gs[GIV ? 1 : MAXL * 6 * Q];
+  double(*s_G)[6][Q] = reinterpret_cast<double(*)[6][Q]>(GIV ? s_ivtb : s_Gs);  // source_x, Hq+uu, uv, source_y, vu, Hq+vv
   __shared__ double s_qq[MAXL][4][P];      // LDG volume fluxes per layer
   __shared__ double s_r[MAXL][4][P];       // rhs_mom(2) and lap(2) per layer
   __shared__ double s_fw[4 * NQ];          // face quad weights of the 4 faces
@@ -1990,8 +2004,11 @@ __global__ void __launch_bounds__(256, 3)
       const double qb0 = r_qa[0], qb1 = r_qa[1], qb2 = r_qa[2];
       const double so2 = sqrt(r_qa[3]);
       double tuu[MAXL], tvv[MAXL], p_tmp[MAXL + 1], H_tmp[MAXL], u_udp[MAXL], v_vdp[MAXL];
-      double u_vdp0[MAXL], u_vdp1[MAXL], gz0[MAXL + 1], gz1[MAXL + 1];
+      double u_vdp0[MAXL], u_vdp1[MAXL], gz0[MAXL + 1], gz1[MAXL + 1], ppl[MAXL];
       p_tmp[0] = 0.0;
+#pragma unroll
+      for (int k = 0; k < MAXL; k++)
+        if (k < L) ppl[k] = s_iv[L - 1][k][qd];  // (the QUIRK row below, read before s_G is written)
 #pragma unroll
       for (int k = 0; k < MAXL; k++) {
         if (k >= L) break;
@@ -2072,7 +2089,7 @@ __global__ void __launch_bounds__(256, 3)
       for (int k = 0; k < MAXL; k++) {
         if (k >= L) break;
         // QUIRK (mod_create_rhs_mlswe.F90:382): qp(k) = the LAST layer's (dp',u',v') indexed by k
-        const double ppt1 = ppt0 + s_iv[L - 1][k][qd];
+        const double ppt1 = ppt0 + ppl[k];
         double wgt = tuu[k] * oosu;
         const double uu = u_udp[k] + wgt * uu_def;
         const double uv0 = u_vdp0[k] + wgt * uv_def;
