@@ -93,6 +93,7 @@ struct hnumo_engine {
   unsigned long long *stage_prof = nullptr;  // HNUMO_STAGE_PROF=1: per-element phase clocks
   int stage_dbg = 0;                         // HNUMO_STAGE_DBG: diagnostic phase switches (timing only)
   int stage_nb = 0;                          // per-stage kernel arena sizing (StageCfg NB; HNUMO_STAGE_NB)
+  bool bcl_big = false;                      // mass/cons element kernels' small-LDS variant (HNUMO_BCL_BIG)
   // persistent sub-cycle (btp_subcycle_kernel): allowed per summation mode when every element's
   // workgroup fits on the device at once (and HNUMO_PERSISTENT != 0); used on single-rank engines
   bool persistent_ok[2] = {false, false};
@@ -353,9 +354,9 @@ struct Launch {
       hipLaunchKernelGGL((mass_flux_face_kernel<NGL, NQ>), dim3(e->nface), dim3(64), 0, e->stream, e->m, qf, e->facc,
                          e->fmass, e->slmf_face);
     if (!fz) kmark(e, "mass_flux_face");
-    hipLaunchKernelGGL((mass_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(Blk<NGL, NQ>::BSW), 0, e->stream, e->m, qp,
-                       e->qacc, e->fmass, q_in, q, e->slmf, e->dpp, e->neg_flag, fz ? qf : nullptr, e->facc,
-                       e->slmf_face);
+    hipLaunchKernelGGL((e->bcl_big ? mass_elem_kernel<NGL, NQ, true> : mass_elem_kernel<NGL, NQ, false>),
+                       dim3(e->nelem_owned), dim3(Blk<NGL, NQ>::BSW), 0, e->stream, e->m, qp, e->qacc, e->fmass, q_in, q,
+                       e->slmf, e->dpp, e->neg_flag, fz ? qf : nullptr, e->facc, e->slmf_face);
     kmark(e, "mass_elem");
   }
   // (qf: the face traces of qp_out's thickness written by cons_elem itself -- fused extract)
@@ -371,9 +372,9 @@ struct Launch {
         hipLaunchKernelGGL((cons_flux_proc_kernel<NQ>), dim3((e->NS * NQ + 63) / 64), dim3(64), 0, e->stream, e->m,
                          e->cdef, e->d_sface, e->NS, e->fcons);
     }
-    hipLaunchKernelGGL((cons_elem_kernel<NGL, NQ>), dim3(e->nelem_owned), dim3(Blk<NGL, NQ>::BSW), 0, e->stream, e->m, e->dpp,
-                       e->qacc, e->slmf, e->fcons, q, qp_out, finalize_dp, qf, fz ? e->facc : nullptr,
-                       e->slmf_face);
+    hipLaunchKernelGGL((e->bcl_big ? cons_elem_kernel<NGL, NQ, true> : cons_elem_kernel<NGL, NQ, false>),
+                       dim3(e->nelem_owned), dim3(Blk<NGL, NQ>::BSW), 0, e->stream, e->m, e->dpp, e->qacc, e->slmf,
+                       e->fcons, q, qp_out, finalize_dp, qf, fz ? e->facc : nullptr, e->slmf_face);
     kmark(e, "cons_elem");
   }
   // (q_in: the momenta entering the update; mode 1 writes the final qprime, see mom_elem_kernel)
@@ -1342,6 +1343,8 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   // one with 2-row term chunks and 1.501 for round 2's, profiles/r03f)
   eng->stage_nb = eng->nelem_owned >= 2048 ? 5 : 0;
   if (const char *sn = getenv("HNUMO_STAGE_NB")) eng->stage_nb = atoi(sn);
+  eng->bcl_big = eng->nelem_owned >= 2048;
+  if (const char *bb = getenv("HNUMO_BCL_BIG")) eng->bcl_big = bb[0] == '1';
   {
     const char *qv = getenv("HNUMO_QPQ");
     if (par->botfr && !(qv && atoi(qv) == 0)) eng->qpq = dalloc<double>(eng, (size_t)E * 3 * eng->nq * eng->nq);

@@ -229,6 +229,10 @@ struct Blk {
   // mass_elem / cons_elem: 256 threads at least (the quad-point sums, ordered_node_sums)
   static constexpr int BSW = BS < 256 ? 256 : BS;
   using QS = QSumCfg<NQ, P * MAXL, 34 * 1024 / 8>;
+  // BIG (meshes of many rounds, HNUMO_BCL_BIG): one quad row per term chunk, double-buffered --
+  // more barriers per element, but a third of the LDS, so more workgroups per CU
+  template <bool BIG>
+  using QSB = typename std::conditional<BIG, QSumCfg<NQ, P * MAXL, 2 * P * MAXL * (NQ | 1)>, QS>::type;
 };
 
 // sum over the element's nodes of PSIH(n,mm,iq,jq)*x(v, mm*NGL+n), mm outer, n inner (the
@@ -998,7 +1002,7 @@ __global__ void face_unpack_kernel(double *base, const double *buf, const int *s
 // create_layers_volume_mass (mod_create_rhs_mlswe.F90:822-877) + face terms + massinv
 // (:74-76), q(1) += dt*dp_advec and the negativity check (mod_splitting.F90:69-78 /
 // :224-232), then dp' = q(1)/(sum_k q(1)/pb') for the consistency step (:350-353).
-template <int NGL, int NQ>
+template <int NGL, int NQ, bool BIG>
 __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     mass_elem_kernel(DevMesh m, const double *qp, const double *qacc, const double *fmass, const double *q_in,
                      double *q, double *slmf, double *dpp, int *neg_flag, const double *qf, const double *facc,
@@ -1007,7 +1011,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   // (mass_flux_at, in place of mass_flux_face_kernel; each face by both its elements, the same
   // bits), the left element of a face writing its layer sums slmf_face for the consistency step
   constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BSW;
-  using QS = typename Blk<NGL, NQ>::QS;
+  using QS = typename Blk<NGL, NQ>::template QSB<BIG>;
   static_assert(MAXL * P <= BS, "one quad-point sum per thread");
   BCL_MARK(0, 0) BCL_WALL(0, 6)
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
@@ -1186,7 +1190,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
 // create_consistency_volume_mass (mod_create_rhs_mlswe.F90:879-920) + face terms, then
 // q(1) += dt*massinv*dp_advec (mod_splitting.F90:362-364).  finalize_dp (thickness): also
 // qprime(1,:,k) = q(1,:,k)/(sum_k q(1)/pb') (mod_splitting.F90:84-87).
-template <int NGL, int NQ>
+template <int NGL, int NQ, bool BIG>
 __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
     cons_elem_kernel(DevMesh m, const double *dpp, const double *qacc, const double *slmf, const double *fcons,
                      double *q, double *qp_out, int finalize_dp, double *qf, const double *facc,
@@ -1196,7 +1200,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   // qf (finalize_dp, single rank): extract_dprime_df_face of the new thickness fused into the
   // finalize (extract_node_faces), in place of the extract launch after this kernel
   constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BSW;
-  using QS = typename Blk<NGL, NQ>::QS;
+  using QS = typename Blk<NGL, NQ>::template QSB<BIG>;
   static_assert(MAXL * P <= BS, "one quad-point sum per thread");
   BCL_MARK(1, 0) BCL_WALL(1, 6)
   const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;

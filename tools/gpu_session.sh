@@ -14,6 +14,8 @@
 #   emu4lake     bench.py --emulate 4:1 --config lake200 (C5 rank 1 of 4) the same way
 #   nb56         tools/ab_env.py: C4 per-stage kernel, LEAN arena for 5 vs 6 workgroups per CU
 #   sprof:<cfg>  tools/stage_profile.py with the diagnostics build diag/libhnumo_diag.so (phase clocks)
+#   bclprof:<cfg>  tools/bcl_profile.py with the diagnostics build (element kernels' phase clocks)
+#   abbd:<cfg[:stage]>:<KNOB>:<v1>/<v2>  tools/ab_breakdown.py (per-kernel step breakdown per value)
 #   abl:<lib>:<cfgs>  tools/ab_stage.py with HNUMO_LIB=<lib> (A/B of builds)
 #   emu:W:R:cfg:order[:warmup:steps]  bench.py --emulate W:R --config cfg --order order
 #   rank         tools/c4_rank_cost.py (C4/8 rank 1 variants)
@@ -71,6 +73,12 @@ for step in "$@"; do
       c=${step#bclprof:}
       HNUMO_LIB=diag/libhnumo_diag.so timeout -k 10 300 python -u tools/bcl_profile.py $c > $O/bclprof_$c.txt 2>&1 || fail "$step" $? $O/bclprof_$c.txt
       cat $O/bclprof_$c.txt ;;
+    abbd:*)
+      # abbd:<cfg[:stage]>:<KNOB>:<v1>/<v2>[/...]  tools/ab_breakdown.py (per-kernel step breakdown)
+      IFS=: read -r _ cf md kn vs <<< "$step"
+      [ "$md" = stage ] || { vs="$kn"; kn="$md"; md=""; }
+      AB_REPS=${AB_REPS:-2} timeout -k 10 600 python -u tools/ab_breakdown.py $cf${md:+:$md} $kn ${vs//\// } >> $O/abbd.log 2>&1 || fail "$step" $? $O/abbd.log
+      tail -4 $O/abbd.log ;;
     abl:*)
       # abl:<lib>:<cfg>[,<cfg>...]  tools/ab_stage.py with HNUMO_LIB=<lib> (default: the product library)
       x=${step#abl:}; lib=${x%%:*}; cf=${x#*:}
