@@ -823,13 +823,18 @@ static void launch_subcycle(hnumo_engine *e, double *dst, const double *qp, bool
       a.elist = e->d_elB;
       DISPATCH(e, stage(e, a, e->nB, e->stream2, sev ? e->ev_Bs[i & 1] : nullptr));
       if (!sev) (void)hipEventRecord(e->ev_B[i & 1], e->stream2);
-      if (a.write_trace) trace_exchange(e, a.trace_out, e->stream2);
       if (i > 0 && !(e->sched_dbg & 1))
         (void)hipStreamWaitEvent(e->stream, sev ? e->ev_Bs[(i - 1) & 1] : e->ev_B[(i - 1) & 1], 0);
+      const StageArgs aB = a;
       a.elist = e->d_elI;
       a.tcontig = 1;  // (interior elements: trace slots 4e..4e+3, StageArgs::tcontig)
       DISPATCH(e, stage(e, a, e->nI, e->stream, sev ? e->ev_Is : nullptr));
       if (!sev) (void)hipEventRecord(e->ev_I, e->stream);
+      // the transport of B_s's traces, enqueued after I_s (stream2 after B_s as before; the order of
+      // the host calls only): RCCL's enqueue can hold the host until an earlier transport has
+      // finished -- at the end of the interior launch it overlaps -- and I_s must be queued by then,
+      // or every stage waits for the host to queue it (~10 us a stage on the C4/8 rank, r05q)
+      if (aB.write_trace) trace_exchange(e, aB.trace_out, e->stream2);
     }
     (void)hipEventRecord(e->ev_join, e->stream2);
     (void)hipStreamWaitEvent(e->stream, e->ev_join, 0);

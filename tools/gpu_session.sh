@@ -19,6 +19,7 @@
 #   abl:<lib>:<cfgs>  tools/ab_stage.py with HNUMO_LIB=<lib> (A/B of builds)
 #   emu:W:R:cfg:order[:warmup:steps]  bench.py --emulate W:R --config cfg --order order
 #   rank         tools/c4_rank_cost.py (C4/8 rank 1 variants)
+#   rankprof     rocprofv3 kernel trace of tools/c4_rank_cost.py (block, rccl)
 #   profiles     tools/gpu_profiles.sh <tag> (kernel trace + FETCH/WRITE + SQ passes)
 #   prof:<cfg>   tools/gpu_profiles.sh <tag> <cfg>
 #   ab:<args>    tools/ab_stage.py <args, commas for spaces>
@@ -93,6 +94,15 @@ for step in "$@"; do
     rank)
       timeout -k 10 600 python tools/c4_rank_cost.py > $O/c4_rank_cost.log 2>&1 || fail "$step" $? $O/c4_rank_cost.log
       tail -1 $O/c4_rank_cost.log ;;
+    rankenv:*)
+      # rankenv:<VAR>=<value>[,<VAR>=<value>]  tools/c4_rank_cost.py (rccl variant) under one environment setting
+      kv=${step#rankenv:}
+      env ${kv//,/ } timeout -k 10 600 python tools/c4_rank_cost.py --variants rccl --no-projection >> $O/rankenv.log 2>&1 || fail "$step" $? $O/rankenv.log
+      echo "$kv: $(grep '"variant"' $O/rankenv.log | tail -1)" ;;
+    rankprof)
+      # kernel trace of the C4/8 rank (block vs self-neighbour RCCL) for the two-stream timeline
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/rankprof -o rp -- python tools/c4_rank_cost.py --variants block,rccl --steps 2 --no-projection > $O/rankprof.log 2>&1 || fail "$step" $? $O/rankprof.log
+      tail -3 $O/rankprof.log ;;
     profiles)
       bash tools/gpu_profiles.sh $TAG || exit 1 ;;
     prof:*)
