@@ -280,6 +280,16 @@ def _self_neighbour(pc):
     return pc
 
 
+def _claim_stdout():
+    """The JSON line is the only thing on stdout: libraries that print to fd 1 (RCCL's version
+    banner at communicator set-up, the HIP runtime) are sent to stderr; the line goes to a private
+    copy of the original stdout."""
+    sys.stdout.flush()
+    out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -303,6 +313,7 @@ def main():
     ap.add_argument("--summation", default="reference", choices=["reference", "factored"],
                     help="stage summation order (hnumo_set_summation); only 'reference' meets the 1e-10 bar")
     args = ap.parse_args()
+    json_out = _claim_stdout()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -597,7 +608,7 @@ def main():
         ncores = max(1, min(args.cpu_cores, len(os.sched_getaffinity(0))))
         out["cpu_baseline"] = cpu_baseline(build_case(make_config(cfg_name)), args.cpu_steps, ncores)
     if rank == 0:
-        print(json.dumps(out))
+        print(json.dumps(out), file=json_out, flush=True)
     if dist is not None:
         dist.destroy_process_group()
 

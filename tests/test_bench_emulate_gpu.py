@@ -33,8 +33,9 @@ def test_bench_n_gt_1_branch_runs_on_one_gpu():
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
-    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
-    d = json.loads(line)
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1, lines  # the JSON line alone (library banners go to stderr)
+    d = json.loads(lines[0])
     assert d["halo_bitwise"] is True and d["halo_check"]["max_rel_diff"] == 0.0
     assert d["scaling"] == "strong" and d["value"] > 0 and d["ms_per_step"] > 0
     assert "EMULATED" in d["config"]["parallelism"]
