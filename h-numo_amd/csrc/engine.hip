@@ -151,6 +151,7 @@ struct hnumo_engine {
   // botfr != 0; HNUMO_QPQ=0: every stage interpolates, for A/B timing)
   double *qpq = nullptr;      // [E][3][Q]
   double *qsv = nullptr;      // [E][2][P][4] Shu-Osher states of the slim persistent sub-cycle (StageArgs::qsv)
+  int *d_eperm = nullptr;     // persistent sub-cycle: workgroup -> element (SubArgs::eperm), NULL = identity
   // hnumo_step_breakdown: events recorded on the engine stream after every launch of a direct
   // (uncaptured) step, each with the name of the kernel family it closes (kmark)
   struct KMarks {
@@ -243,7 +244,7 @@ struct Launch {
       hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, NB>), dim3(n), dim3(K::BS), 0, st, a);
   }
   static void subcycle(hnumo_engine *e, const StageArgs *stages, int ns) {
-    SubArgs sa{stages, ns, e->epoch, e->sub_done, e->sub_arrive, e->neg_flag, e->dbg_abort_epoch};
+    SubArgs sa{stages, ns, e->epoch, e->sub_done, e->sub_arrive, e->neg_flag, e->dbg_abort_epoch, e->d_eperm};
     if (e->summation == HNUMO_SUM_REFERENCE)
       hipLaunchKernelGGL((btp_subcycle_kernel<NGL, NQ, false>), dim3(e->nelem_owned),
                          dim3(StageCfg<NGL, NQ, false>::BS), e->persist_pad, e->stream, sa);
@@ -275,7 +276,7 @@ struct Launch {
   }
   // the trial launch: the persistent grid with no stages, i.e. the residency rendezvous alone
   static void probe(hnumo_engine *e, int sum) {
-    SubArgs sa{e->d_stages[0], 0, e->epoch, e->sub_done, e->sub_arrive, e->neg_flag, nullptr};
+    SubArgs sa{e->d_stages[0], 0, e->epoch, e->sub_done, e->sub_arrive, e->neg_flag, nullptr, e->d_eperm};
     if (sum == HNUMO_SUM_REFERENCE)
       hipLaunchKernelGGL((btp_subcycle_kernel<NGL, NQ, false>), dim3(e->nelem_owned),
                          dim3(StageCfg<NGL, NQ, false>::BS), e->persist_pad, e->stream, sa);
@@ -1509,6 +1510,28 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
       int ncu = 0;
       HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, eng->device));
       DISPATCH(eng, occupancy(eng, ncu));
+      // (HNUMO_PERSIST_PERM=0: the identity) workgroup b runs on CU b % ncu (the dispatcher's round-robin; blocks b,
+      // b + ncu, b + 2 ncu share a CU), so with E/ncu not whole some CUs hold one element more; the
+      // elements with a physical-boundary face (more work: ghost states, wall fluxes) go to the CUs
+      // holding fewer, the others fill the rest in order.  Same arithmetic per element, same bits
+      // (dg25L3: 16 us less sub-cycle time per step in 3 interleaved pairs, profiles/r05x).
+      const char *pm = getenv("HNUMO_PERSIST_PERM");
+      if (!(pm && pm[0] == '0') && ncu > 0 && E % ncu) {
+        const int nheavy = E % ncu;  // CUs k < nheavy hold one block more
+        std::vector<int> bnd, inr, perm(E);
+        for (int el = 0; el < E; el++) {
+          bool b = false;
+          for (int lf = 0; lf < 4; lf++) b = b || ebc[4 * el + lf] < 0;
+          (b ? bnd : inr).push_back(el);
+        }
+        size_t ib = 0, ii = 0;
+        for (int b = 0; b < E; b++) {
+          const bool light = (b % ncu) >= nheavy;
+          perm[b] = (light && ib < bnd.size()) ? bnd[ib++] : (ii < inr.size() ? inr[ii++] : bnd[ib++]);
+        }
+        eng->d_eperm = dalloc<int>(eng, E);
+        if (eng->d_eperm) HIPCHK(hipMemcpy(eng->d_eperm, perm.data(), E * sizeof(int), hipMemcpyHostToDevice));
+      }
       // the trial launches: what the dispatcher does, not what the estimate says, decides
       for (int sm = 0; sm < 2 && (eng->persist_guard & 2); sm++) {
         if (!eng->persistent_ok[sm] || eng->comm_mode != 0 || eng->nranks != 1) continue;

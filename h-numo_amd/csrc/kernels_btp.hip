@@ -2044,6 +2044,8 @@ struct SubArgs {
   // test hook (hnumo_debug_force_abort): the launch whose epoch equals *abort_epoch gives up as a
   // non-resident one does (NULL: never)
   const unsigned long long *abort_epoch;
+  // workgroup -> element (NULL: the identity; HNUMO_PERSIST_PERM, engine.hip persist_perm)
+  const int *eperm;
 };
 
 // Residency rendezvous of a persistent launch (one thread per workgroup).  The sub-cycle's
@@ -2085,7 +2087,7 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
   using C = StageCfg<NGL, NQ, SF>;
   __shared__ __attribute__((aligned(16))) double s_arena[C::ARENA];
   __shared__ unsigned long long s_prof[HNUMO_DIAG ? 32 : 1];
-  const int e = blockIdx.x, tid = threadIdx.x;
+  const int e = sa.eperm ? __builtin_amdgcn_readfirstlane(sa.eperm[blockIdx.x]) : (int)blockIdx.x, tid = threadIdx.x;
   const unsigned long long ep = *sa.epoch;
   typedef const __attribute__((address_space(4))) StageArgs CStageArgs;
   CStageArgs *tab = (CStageArgs *)sa.stages;
