@@ -1518,6 +1518,9 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
       const char *pm = getenv("HNUMO_PERSIST_PERM");
       if (!(pm && pm[0] == '0') && ncu > 0 && E % ncu) {
         const int nheavy = E % ncu;  // CUs k < nheavy hold one block more
+        // (measured, not kept: also grouping by XCD -- blocks b and b + 8 share one, so group b % 8
+        // took the (b % 8)-th strip of consecutive element ids: 2268 against 2224 us of sub-cycle per
+        // step, profiles/r05z)
         std::vector<int> bnd, inr, perm(E);
         for (int el = 0; el < E; el++) {
           bool b = false;
