@@ -1516,7 +1516,8 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
       // holding fewer, the others fill the rest in order.  Same arithmetic per element, same bits
       // (dg25L3: 16 us less sub-cycle time per step in 3 interleaved pairs, profiles/r05x).
       const char *pm = getenv("HNUMO_PERSIST_PERM");
-      if (!(pm && pm[0] == '0') && ncu > 0 && E % ncu) {
+      if (!(pm && pm[0] == '0') && ncu > 0 && E % ncu && eng->nranks == 1 && !eng->face_halo && eng->comm_mode == 0 &&
+          eng->nelem_owned == E) {
         const int nheavy = E % ncu;  // CUs k < nheavy hold one block more
         // (measured, not kept: also grouping by XCD -- blocks b and b + 8 share one, so group b % 8
         // took the (b % 8)-th strip of consecutive element ids: 2268 against 2224 us of sub-cycle per
@@ -1534,6 +1535,9 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
         }
         eng->d_eperm = dalloc<int>(eng, E);
         if (eng->d_eperm) HIPCHK(hipMemcpy(eng->d_eperm, perm.data(), E * sizeof(int), hipMemcpyHostToDevice));
+        // the element kernels of the step (625 blocks at dg25 too: the same CUs hold one block more)
+        const char *pg = getenv("HNUMO_GLUE_PERM");
+        if (!(pg && pg[0] == '0')) eng->m.eperm = eng->d_eperm;
       }
       // the trial launches: what the dispatcher does, not what the estimate says, decides
       for (int sm = 0; sm < 2 && (eng->persist_guard & 2); sm++) {

@@ -152,6 +152,9 @@ struct DevMesh {
   // the step on per-stage launches.  steps_done counts the steps whose corrector completed.
   const int *runflag;
   unsigned *steps_done;
+  // [nelem] block -> element of the element kernels (the persistent sub-cycle's placement, engine.hip
+  // d_eperm; single-rank engines only; NULL: block b runs element b)
+  const int *eperm;
 };
 
 // device flag word bits (engine.hip flag_error): 1 negative thickness, 2 non-finite state,

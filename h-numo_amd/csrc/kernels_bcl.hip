@@ -132,6 +132,10 @@ struct BasisGather {
 #ifndef HNUMO_MOM_GZS
 #define HNUMO_MOM_GZS 1
 #endif
+// the element of this block (DevMesh::eperm)
+__device__ __forceinline__ int blk_elem(const DevMesh &m) {
+  return m.eperm ? __builtin_amdgcn_readfirstlane(m.eperm[blockIdx.x]) : (int)blockIdx.x;
+}
 #define BCL_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
 
 // Term buffers of ordered_node_sums: chunks of RC quad rows (RC | NQ) for NT chains, two buffers
@@ -477,7 +481,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   // qf_out (not in place: the neighbour reads the face block too), each element writing its side
   constexpr int P = Blk<NGL, NQ>::P, Q = Blk<NGL, NQ>::Q, BS = Blk<NGL, NQ>::BSW;
   static_assert(BS >= 192 && 4 * NQ <= 64 && 4 * NGL <= 64, "face tasks on waves 1 and 2");
-  const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
+  const int e = blk_elem(m), tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
   __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
   __shared__ double s_q[MAXL][3][P];
   __shared__ double s_nm[4][P];
@@ -1014,7 +1018,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   using QS = typename Blk<NGL, NQ>::template QSB<BIG>;
   static_assert(MAXL * P <= BS, "one quad-point sum per thread");
   BCL_MARK(0, 0) BCL_WALL(0, 6)
-  const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
+  const int e = blk_elem(m), tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
   __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
   __shared__ double s_qm[5][Q];             // e_x, e_y, n_x, n_y, w
   __shared__ double s_f[MAXL][2][Q];        // udp, vdp per layer
@@ -1203,7 +1207,7 @@ __global__ void __launch_bounds__((Blk<NGL, NQ>::BSW))
   using QS = typename Blk<NGL, NQ>::template QSB<BIG>;
   static_assert(MAXL * P <= BS, "one quad-point sum per thread");
   BCL_MARK(1, 0) BCL_WALL(1, 6)
-  const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
+  const int e = blk_elem(m), tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
   __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
   __shared__ double s_d[MAXL][P];
   __shared__ double s_qm[5][Q];
@@ -1760,7 +1764,7 @@ __global__ void __launch_bounds__(256, (MomCfg<NGL, NQ>::MINW))
   // (ti_rk_bcl.F90:81-84: thickness from dpp2 = the corrector's own, momenta from evaluate_bcl_v1)
   // and flags a non-finite barotropic state (bit 2) of its element
   constexpr int P = MomCfg<NGL, NQ>::P, Q = MomCfg<NGL, NQ>::Q, BS = MomCfg<NGL, NQ>::BS;
-  const int e = blockIdx.x, tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
+  const int e = blk_elem(m), tid = threadIdx.x, L = m.L, npoin = m.npoin, npq = m.npoin_q, F = m.nface;
   const double g = m.gravity, eps1 = 1.0e-20;
   BCL_MARK(2, 0) BCL_WALL(2, 6)
   __shared__ double s_psiq[NGL * NQ], s_dpsiq[NGL * NQ], s_dpsi[NGL * NGL], s_psi[NGL * NGL];
