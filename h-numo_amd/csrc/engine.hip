@@ -1529,6 +1529,8 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
           (b ? bnd : inr).push_back(el);
         }
         size_t ib = 0, ii = 0;
+        // (measured, not kept: a CU's blocks on consecutive element ids -- neighbours sharing a CU --
+        // 2357 against 2208 us of sub-cycle per step, profiles/r05ac)
         for (int b = 0; b < E; b++) {
           const bool light = (b % ncu) >= nheavy;
           perm[b] = (light && ib < bnd.size()) ? bnd[ib++] : (ii < inr.size() ? inr[ii++] : bnd[ib++]);
