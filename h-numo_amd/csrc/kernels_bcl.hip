@@ -1492,15 +1492,18 @@ __global__ void __launch_bounds__(64)
   const int er = m.fer[f];
   const double g = m.gravity, eps1 = 1.0e-20;
 #define FA(k) s_fa[(k) * NQ + iq]
-  if (tid < NQ) {
-    const int iq = tid;
+  // two lanes per face quad point, sd = 0 (left) and 1 (right): both form the shared upwind
+  // fluxes, each only its own side's layer-overlap pressure H_r and output
+  static_assert(2 * NQ <= 32, "quad lanes below the LDG lanes");
+  if (tid < 2 * NQ) {
+    const int sd = tid / NQ, iq = tid - sd * NQ;
     const double *alpha = m.alpha;
     double nxl = s_fs[0][iq], nyl = s_fs[1][iq];
     double qbl0 = FA(FA_OPEL), qbr0 = FA(FA_OPER);
     double qbl1 = FA(FA_UL), qbr1 = FA(FA_UR);
     double qbl2 = FA(FA_VL), qbr2 = FA(FA_VR);
     double ql[MAXL][3], qr[MAXL][3], udpl[MAXL], udpr[MAXL], vdpl[MAXL], vdpr[MAXL];
-    double udpf[2][MAXL], vdpf[2][MAXL], Hf[2][MAXL];
+    double udpf[2][MAXL], vdpf[2][MAXL];
 #pragma unroll
     for (int k = 0; k < MAXL; k++) {
       if (k >= L) break;
@@ -1580,24 +1583,25 @@ __global__ void __launch_bounds__(64)
       vdpf[0][k] = vdpf[0][k] + ((vu_def * nxl > 0.0) ? fabs(vdpl[k]) * oosl : fabs(vdpr[k]) * oosr) * vu_def;
       vdpf[1][k] = vdpf[1][k] + ((vv_def * nyl > 0.0) ? fabs(vdpl[k]) * oosl : fabs(vdpr[k]) * oosr) * vv_def;
     }
-    // H_r at the face (layer-overlap pressure, :627-707)
-    double pf[2][MAXL + 1], zf[2][MAXL + 1], pep[MAXL + 1], pem[MAXL + 1], zep[MAXL + 1], zem[MAXL + 1];
+    // H_r at the face (layer-overlap pressure, :627-707), side sd: the reference's left and right
+    // formulas are mirror images -- own = this side's layer pressure, other = the overlap sum over
+    // the other side's layers (zo, po) against this side's interfaces (zs); the left side adds
+    // 0.5*(own + other), the right 0.5*(other + own): the same sum
+    double pf[MAXL + 1], zf[MAXL + 1], pep[MAXL + 1], pem[MAXL + 1], zep[MAXL + 1], zem[MAXL + 1], Hf[MAXL];
 #pragma unroll
-    for (int k = 0; k <= MAXL; k++) zf[0][k] = zf[1][k] = pf[0][k] = pf[1][k] = zep[k] = zem[k] = pep[k] = pem[k] = 0.0;
-    double ope_l = sqrt(FA(FA_OPE2L)), ope_r = sqrt(FA(FA_OPE2R));
+    for (int k = 0; k <= MAXL; k++) zf[k] = pf[k] = zep[k] = zem[k] = pep[k] = pem[k] = 0.0;
+    const double ope_s = sqrt(sd ? FA(FA_OPE2R) : FA(FA_OPE2L));
 #pragma unroll
     for (int k = 1; k <= MAXL; k++) {
       if (k > L) break;
-      pf[0][k] = pf[0][k - 1] + ope_l * ql[k - 1][0];
-      pf[1][k] = pf[1][k - 1] + ope_r * qr[k - 1][0];
+      pf[k] = pf[k - 1] + ope_s * (sd ? qr[k - 1][0] : ql[k - 1][0]);
     }
-    double ope_e = sqrt(FA(FA_OPEE2));
-    double zbl = s_fs[2][iq], zbr = s_fs[3][iq];
+    const double ope_e = sqrt(FA(FA_OPEE2));
+    const double zbl = s_fs[2][iq], zbr = s_fs[3][iq];
 #pragma unroll
     for (int k = 1; k <= MAXL; k++)
       if (k == L) {
-        zf[0][k] = zbl;
-        zf[1][k] = zbr;
+        zf[k] = sd ? zbr : zbl;
         zep[k] = zbl;
         zem[k] = zbr;
       }
@@ -1605,8 +1609,7 @@ __global__ void __launch_bounds__(64)
     for (int k = MAXL; k >= 1; k--) {
       if (k > L) continue;
       double aog = alpha[k - 1] / g;
-      zf[0][k - 1] = zf[0][k] + aog * (ope_l * ql[k - 1][0]);
-      zf[1][k - 1] = zf[1][k] + aog * (ope_r * qr[k - 1][0]);
+      zf[k - 1] = zf[k] + aog * (ope_s * (sd ? qr[k - 1][0] : ql[k - 1][0]));
       zep[k - 1] = zep[k] + aog * (ope_e * ql[k - 1][0]);
       zem[k - 1] = zem[k] + aog * (ope_e * qr[k - 1][0]);
     }
@@ -1618,83 +1621,69 @@ __global__ void __launch_bounds__(64)
       pep[k] = pep[k - 1] + ope_e * ql[k - 1][0];
       pem[k] = pem[k - 1] + ope_e * qr[k - 1][0];
     }
+    double zs[MAXL + 1], zo[MAXL + 1], ps[MAXL + 1], po[MAXL + 1];
+#pragma unroll
+    for (int k = 0; k <= MAXL; k++) {
+      zs[k] = sd ? zem[k] : zep[k];
+      zo[k] = sd ? zep[k] : zem[k];
+      ps[k] = sd ? pem[k] : pep[k];
+      po[k] = sd ? pep[k] : pem[k];
+    }
 #pragma unroll
     for (int k = 1; k <= MAXL; k++) {
       if (k > L) break;
-      double Hrp = 0.5 * alpha[k - 1] * (pep[k] * pep[k] - pep[k - 1] * pep[k - 1]);
-      double Hrm = 0.0;
+      double own = 0.5 * alpha[k - 1] * (ps[k] * ps[k] - ps[k - 1] * ps[k - 1]);
+      double other = 0.0;
 #pragma unroll
       for (int kt = 1; kt <= MAXL; kt++) {
         if (kt > L) break;
         double goa = g / alpha[kt - 1];
-        double zt = dmin(zem[kt - 1], zep[k - 1]), zb = dmax(zem[kt], zep[k]);
+        double zt = dmin(zo[kt - 1], zs[k - 1]), zb = dmax(zo[kt], zs[k]);
         if (zt - zb > 0.0) {
-          double pbot = pem[kt] - goa * (zb - zem[kt]);
-          double ptop = pem[kt] - goa * (zt - zem[kt]);
-          Hrm = Hrm + 0.5 * alpha[kt - 1] * (pbot * pbot - ptop * ptop);
+          double pbot = po[kt] - goa * (zb - zo[kt]);
+          double ptop = po[kt] - goa * (zt - zo[kt]);
+          other = other + 0.5 * alpha[kt - 1] * (pbot * pbot - ptop * ptop);
         }
       }
-      Hf[0][k - 1] = 0.5 * (Hrp + Hrm);
-      Hrm = 0.5 * alpha[k - 1] * (pem[k] * pem[k] - pem[k - 1] * pem[k - 1]);
-      Hrp = 0.0;
-#pragma unroll
-      for (int kt = 1; kt <= MAXL; kt++) {
-        if (kt > L) break;
-        double goa = g / alpha[kt - 1];
-        double zt = dmin(zep[kt - 1], zem[k - 1]), zb = dmax(zep[kt], zem[k]);
-        if (zt - zb > 0.0) {
-          double pbot = pep[kt] - goa * (zb - zep[kt]);
-          double ptop = pep[kt] - goa * (zt - zep[kt]);
-          Hrp = Hrp + 0.5 * alpha[kt - 1] * (pbot * pbot - ptop * ptop);
-        }
-      }
-      Hf[1][k - 1] = 0.5 * (Hrp + Hrm);
+      Hf[k - 1] = 0.5 * (own + other);
     }
     if (er == -4) {
 #pragma unroll
       for (int k = 1; k <= MAXL; k++) {
         if (k > L) break;
-        Hf[0][k - 1] = 0.5 * alpha[k - 1] * (pf[0][k] * pf[0][k] - pf[0][k - 1] * pf[0][k - 1]);
-        Hf[1][k - 1] = 0.5 * alpha[k - 1] * (pf[1][k] * pf[1][k] - pf[1][k - 1] * pf[1][k - 1]);
+        Hf[k - 1] = 0.5 * alpha[k - 1] * (pf[k] * pf[k] - pf[k - 1] * pf[k - 1]);
       }
     } else {
 #pragma unroll
       for (int k = 1; k <= MAXL - 1; k++) {
         if (k > L - 1) break;
         double goa = g / alpha[k - 1];
-        double pinc1 = goa * (zf[0][k] - zep[k]);
-        double Hc1 = 0.5 * alpha[k - 1] * ((pf[0][k] + pinc1) * (pf[0][k] + pinc1) - pf[0][k] * pf[0][k]);
-        Hf[0][k - 1] = Hf[0][k - 1] - Hc1;
-        Hf[0][k] = Hf[0][k] + Hc1;
-        double pinc2 = goa * (zf[1][k] - zem[k]);
-        double Hc2 = 0.5 * alpha[k - 1] * ((pf[1][k] + pinc2) * (pf[1][k] + pinc2) - pf[1][k] * pf[1][k]);
-        Hf[1][k - 1] = Hf[1][k - 1] - Hc2;
-        Hf[1][k] = Hf[1][k] + Hc2;
+        double pinc = goa * (zf[k] - zs[k]);
+        double Hc = 0.5 * alpha[k - 1] * ((pf[k] + pinc) * (pf[k] + pinc) - pf[k] * pf[k]);
+        Hf[k - 1] = Hf[k - 1] - Hc;
+        Hf[k] = Hf[k] + Hc;
       }
     }
-    double hfa = FA(FA_H);
-#pragma unroll
-    for (int sd = 0; sd < 2; sd++) {
+    {
       double weight = 1.0, acc = 0.0;
 #pragma unroll
       for (int k = 0; k < MAXL; k++)
-        if (k < L) acc = acc + Hf[sd][k];
-      if (acc > 0.0) weight = hfa / acc;
+        if (k < L) acc = acc + Hf[k];
+      if (acc > 0.0) weight = FA(FA_H) / acc;
 #pragma unroll
       for (int k = 0; k < MAXL; k++)
-        if (k < L) Hf[sd][k] = Hf[sd][k] * weight;
+        if (k < L) Hf[k] = Hf[k] * weight;
     }
+    const int so = sd ? slotR : slotL;
+    if (so >= 0) {
 #pragma unroll
-    for (int k = 0; k < MAXL; k++) {
-      if (k >= L) break;
-      double hlx = nxl * Hf[0][k], hrx = nxl * Hf[1][k], hly = nyl * Hf[0][k], hry = nyl * Hf[1][k];
-      double flux_x = nxl * udpf[0][k] + nyl * udpf[1][k];
-      double flux_y = nxl * vdpf[0][k] + nyl * vdpf[1][k];
-      momL[MSLOT(slotL, k, 0, iq, NQ)] = hlx + flux_x;
-      momL[MSLOT(slotL, k, 1, iq, NQ)] = hly + flux_y;
-      if (slotR >= 0) {
-        momL[MSLOT(slotR, k, 0, iq, NQ)] = hrx + flux_x;
-        momL[MSLOT(slotR, k, 1, iq, NQ)] = hry + flux_y;
+      for (int k = 0; k < MAXL; k++) {
+        if (k >= L) break;
+        double hx = nxl * Hf[k], hy = nyl * Hf[k];
+        double flux_x = nxl * udpf[0][k] + nyl * udpf[1][k];
+        double flux_y = nxl * vdpf[0][k] + nyl * vdpf[1][k];
+        momL[MSLOT(so, k, 0, iq, NQ)] = hx + flux_x;
+        momL[MSLOT(so, k, 1, iq, NQ)] = hy + flux_y;
       }
     }
     BCL_MARK(3, 2)

@@ -16,6 +16,7 @@
 #   sprof:<cfg>  tools/stage_profile.py with the diagnostics build diag/libhnumo_diag.so (phase clocks)
 #   bclprof:<cfg>  tools/bcl_profile.py with the diagnostics build (element kernels' phase clocks)
 #   abbd:<cfg[:stage]>:<KNOB>:<v1>/<v2>  tools/ab_breakdown.py (per-kernel step breakdown per value)
+#   abbdl:<lib>:<cfg>  the same for a build (HNUMO_LIB)
 #   abl:<lib>:<cfgs>  tools/ab_stage.py with HNUMO_LIB=<lib> (A/B of builds)
 #   emu:W:R:cfg:order[:warmup:steps]  bench.py --emulate W:R --config cfg --order order
 #   rank         tools/c4_rank_cost.py (C4/8 rank 1 variants)
@@ -80,6 +81,12 @@ for step in "$@"; do
       [ "$md" = stage ] || { vs="$kn"; kn="$md"; md=""; }
       AB_REPS=${AB_REPS:-2} timeout -k 10 600 python -u tools/ab_breakdown.py $cf${md:+:$md} $kn ${vs//\// } >> $O/abbd.log 2>&1 || fail "$step" $? $O/abbd.log
       tail -4 $O/abbd.log ;;
+    abbdl:*)
+      # abbdl:<lib>:<cfg>  tools/ab_breakdown.py under HNUMO_LIB=<lib> (A/B of builds by the breakdown)
+      x=${step#abbdl:}; lib=${x%%:*}; cf=${x#*:}
+      [ "$lib" = default ] && lib=h-numo_amd/libhnumo_engine.so
+      HNUMO_LIB=$lib AB_REPS=1 timeout -k 10 600 python -u tools/ab_breakdown.py $cf HNUMO_AB_LIB $(basename $lib) >> $O/abbd.log 2>&1 || fail "$step" $? $O/abbd.log
+      tail -1 $O/abbd.log ;;
     abl:*)
       # abl:<lib>:<cfg>[,<cfg>...]  tools/ab_stage.py with HNUMO_LIB=<lib> (default: the product library)
       x=${step#abl:}; lib=${x%%:*}; cf=${x#*:}
