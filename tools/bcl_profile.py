@@ -41,4 +41,15 @@ for k, (nm, ph) in names.items():
             d = cur - prev
             print(f"    {p:16s} mean {d.mean():8.0f}  max {d.max():8.0f}")
             prev = cur
+    if k != 3 and E > 256:
+        # the CUs of blocks b % 256 < E % 256 hold one block more (round-robin dealing, 256 CUs)
+        heavy = (np.arange(E) % 256) < (E % 256)
+        span = w1 - w0
+        print(f"    block span (100 MHz) on CUs holding one more: {span[heavy].mean():.0f}, the others: "
+              f"{span[~heavy].mean():.0f}; start of the last-started block {w0.max() - w0.min()}")
+        marks = [0] + [i + 1 for i, p in enumerate(ph) if p != "-"]  # (phases with a mark of their own)
+        for b in np.argsort(-tot)[:6]:
+            ds = [int(a[b, marks[i + 1]] - a[b, marks[i]]) for i in range(len(marks) - 1)]
+            print(f"    slow block {b:4d} ({'3' if heavy[b] else '2'} on its CU): clocks {tot[b]}, phases {ds}, "
+                  f"wall start +{w0[b] - w0.min()} end +{w1[b] - w0.min()}")
 eng.close()
