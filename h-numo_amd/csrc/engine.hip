@@ -94,6 +94,7 @@ struct hnumo_engine {
   int stage_dbg = 0;                         // HNUMO_STAGE_DBG: diagnostic phase switches (timing only)
   int stage_nb = 0;                          // per-stage kernel arena sizing (StageCfg NB; HNUMO_STAGE_NB)
   bool bcl_big = false;                      // mass/cons element kernels' small-LDS variant (HNUMO_BCL_BIG)
+  bool acc_zero = false;                     // HNUMO_ACC_ZERO=1: zero the time averages before a sub-cycle (A/B)
   // persistent sub-cycle (btp_subcycle_kernel): allowed per summation mode when every element's
   // workgroup fits on the device at once (and HNUMO_PERSISTENT != 0); used on single-rank engines
   bool persistent_ok[2] = {false, false};
@@ -744,6 +745,10 @@ static int stage_table(hnumo_engine *e, const double *qp, std::vector<StageArgs>
       a.rhs_only = 0;
       a.write_trace = !(mstep == NB - 1 && ik == K - 1);
       a.accumulate = !(e->stage_dbg & 32);  // dbg bit 32: no time averages (timing experiments)
+      // the sub-cycle's first stage stores its time-average terms (acc_put), so the slots need no
+      // zeroing before it -- except with the quad-point LDG (method_visc == 1), whose stages leave
+      // the graduvb slots to lapq kernels
+      if (out_args.empty() && a.accumulate && !e->lapq_on && !e->acc_zero) a.accumulate = 2;
       a.prof = e->stage_prof;
       a.dbg = e->stage_dbg;
       const int stage = (int)out_args.size();
@@ -785,7 +790,8 @@ static void launch_subcycle(hnumo_engine *e, double *dst, const double *qp, bool
   const bool pers = use_persistent(e) && tab >= 0;
   // persistent with register averages: the kernel writes them, zeroed and scaled as below
   const bool racc = pers && e->regacc[e->summation] && !(e->stage_dbg & 32);
-  if (!racc) subcycle_prologue(e, e->qb, nullptr, true);
+  // (the first stage stores the time averages unless method_visc == 1: no zeroing, StageArgs::accumulate)
+  if (!racc) subcycle_prologue(e, e->qb, nullptr, e->lapq_on || e->acc_zero);
   if (!pers) exchange_qb(e, e->qbuf[0]);
   if (!pers) DISPATCH(e, grad_trace(e, e->qbuf[0], e->gtrace[0], 0, e->nelem));  // (persistent: its stage 0)
   const int K = e->K, NB = e->p.N_btp;
@@ -1351,6 +1357,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   if (const char *sn = getenv("HNUMO_STAGE_NB")) eng->stage_nb = atoi(sn);
   eng->bcl_big = eng->nelem_owned >= 2048;
   if (const char *bb = getenv("HNUMO_BCL_BIG")) eng->bcl_big = bb[0] == '1';
+  if (const char *az = getenv("HNUMO_ACC_ZERO")) eng->acc_zero = az[0] == '1';
   {
     const char *qv = getenv("HNUMO_QPQ");
     if (par->botfr && !(qv && atoi(qv) == 0)) eng->qpq = dalloc<double>(eng, (size_t)E * 3 * eng->nq * eng->nq);

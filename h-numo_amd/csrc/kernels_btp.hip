@@ -147,6 +147,15 @@ __device__ __forceinline__ void ld_granule(const TraceGranule *p, double &v, uns
   v = __builtin_bit_cast(double, ((unsigned long long)x[1] << 32) | x[0]);
   tag = ((unsigned long long)x[3] << 32) | x[2];
 }
+// a time-average slot of this element: the first stage of a sub-cycle stores 0 + x (the reference's
+// sum starts at zero: the same bits as adding x to a zeroed slot), the later stages add -- so no
+// zeroing pass runs before the sub-cycle (StageArgs::accumulate == 2)
+__device__ __forceinline__ void acc_put(double *p, double x, bool first) {
+  if (first)
+    *p = 0.0 + x;
+  else
+    atomicAdd(p, x);
+}
 struct StageArgs {
   DevMesh m;
   const double *qb_in, *qb0, *qb2, *qprime;  // qb(4,npoin); qprime(3,npoin,L)
@@ -1032,7 +1041,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         for (int k = 0; k < FA_N; k++) pacc[k] = pacc[k] + add[k];
       } else {
 #pragma unroll
-        for (int k = 0; k < FA_N; k++) atomicAdd(&a.facc[FACC_I(k, e * 4 + lf, iq)], add[k]);
+        for (int k = 0; k < FA_N; k++) acc_put(&a.facc[FACC_I(k, e * 4 + lf, iq)], add[k], a.accumulate == 2);
       }
     }
     const double H_kx = nxl * Hf, H_ky = nyl * Hf;
@@ -1134,7 +1143,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           for (int k = 0; k < QA_N; k++) pacc[k] = pacc[k] + add[k];
         } else {
 #pragma unroll
-          for (int k = 0; k < QA_N; k++) atomicAdd(&a.qacc[QACC_I(k, e, q)], add[k]);
+          for (int k = 0; k < QA_N; k++) acc_put(&a.qacc[QACC_I(k, e, q)], add[k], a.accumulate == 2);
         }
       }
       if constexpr (SF) {
@@ -1188,10 +1197,10 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         } else {
           if (!a.lapq)
 #pragma unroll
-            for (int c = 0; c < 4; c++) atomicAdd(&a.nacc[NACC_I(NA_G1 + c, e, p)], g[c]);
-          atomicAdd(&a.nacc[NACC_I(NA_OPE2, e, p)], t1 * t1);
-          atomicAdd(&a.nacc[NACC_I(NA_UB, e, p)], s_u[p]);
-          atomicAdd(&a.nacc[NACC_I(NA_VB, e, p)], s_v[p]);
+            for (int c = 0; c < 4; c++) acc_put(&a.nacc[NACC_I(NA_G1 + c, e, p)], g[c], a.accumulate == 2);
+          acc_put(&a.nacc[NACC_I(NA_OPE2, e, p)], t1 * t1, a.accumulate == 2);
+          acc_put(&a.nacc[NACC_I(NA_UB, e, p)], s_u[p], a.accumulate == 2);
+          acc_put(&a.nacc[NACC_I(NA_VB, e, p)], s_v[p], a.accumulate == 2);
         }
       }
     }
@@ -1256,8 +1265,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           pacc[c] = pacc[c] + gl[c];
           pacc[4 + c] = pacc[4 + c] + gr[c];
         } else {
-          atomicAdd(&a.gfacc[GFACC_I(c, e * 4 + lf, n)], gl[c]);
-          atomicAdd(&a.gfacc[GFACC_I(4 + c, e * 4 + lf, n)], gr[c]);
+          acc_put(&a.gfacc[GFACC_I(c, e * 4 + lf, n)], gl[c], a.accumulate == 2);
+          acc_put(&a.gfacc[GFACC_I(4 + c, e * 4 + lf, n)], gr[c], a.accumulate == 2);
         }
       }
     }
