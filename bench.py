@@ -154,6 +154,7 @@ def single_gpu_line(cfg: str, workload: str, steps: int = 3, case=None, device: 
     k_ms = eng.time_stage_kernel(1)
     path = eng.stage_path
     stats = eng.persistent_stats
+    env = eng.overrides
     bd = step_breakdown(eng, case, 1) if breakdown else None
     from hnumo.roofline import HBM_PEAK_GBS, stage_bytes
     eng.close()
@@ -162,7 +163,8 @@ def single_gpu_line(cfg: str, workload: str, steps: int = 3, case=None, device: 
            "value": round(element_updates_per_step(case) * steps / t, 1), "unit": "element-updates/s",
            "steps": steps, "ms_per_step": round(1e3 * t / steps, 3),
            "stage_kernel_us": round(k_ms * 1e3, 2), "stage_kernel_frac": round(ach / HBM_PEAK_GBS, 4),
-           "algorithmic_bytes_per_stage": int(stage_bytes(case)), "persistent_fallbacks": stats["aborts"]}
+           "algorithmic_bytes_per_stage": int(stage_bytes(case)), "persistent_fallbacks": stats["aborts"],
+           "engine_env": env}
     out.update(_profiled(cfg, "btp_subcycle_kernel" if path == "persistent" else "btp_stage_kernel", k_ms))
     if bd:
         out.update(bd)
@@ -440,6 +442,10 @@ def main():
     barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
+    # the timed run's own persistent-path counters and stage path, read before any diagnostic step
+    # below (step_breakdown, the halo check) can add aborts or re-probes of its own
+    timed_stats = eng.persistent_stats
+    timed_path = eng.stage_path
     eu_local = element_updates_per_step(case) * steps
     if dist is not None:
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
@@ -450,7 +456,7 @@ def main():
         eu_total = float(n.item())
     else:
         eu_total = float(eu_local)
-    path = eng.stage_path
+    path = timed_path
     kname = "btp_subcycle_kernel" if path == "persistent" else "btp_stage_kernel"
     k_src = "graph event nodes around the corrector sub-cycle"
     if not (k_ms and k_ms > 0):
@@ -541,7 +547,7 @@ def main():
         "metric": "DG element-updates/sec (all layers, per RK stage)",
         "value": round(value, 1), "unit": "element-updates/s", "n_gpus": world, "steps": steps,
         "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-        "scaling": scaling, "vs_baseline": None, "dtype": "f64",
+        "scaling": "emulated" if emu else scaling, "vs_baseline": None, "dtype": "f64",
         "data": f"synthetic (analytic {base_cfg['test_case']} IC)",
         "config": {"workload": wl + f", N={S['ngl'] - 1}, {S['nlayers']} layers, "
                                f"N_btp={S['N_btp']}, kstages={S['kstages']}",
@@ -556,7 +562,10 @@ def main():
         out["halo_check"] = halo_check
     # the persistent path's in-launch residency check: launches that gave up (and were redone on
     # per-stage launches), trial re-probes, and re-probes that found the grid resident again
-    out["persistent"] = eng.persistent_stats
+    out["persistent"] = timed_stats
+    # every HNUMO_* environment setting the engine read (hnumo_overrides; experiment knobs are
+    # honoured only with HNUMO_EXPERIMENTS=1): empty on a clean box
+    out["engine_env"] = eng.overrides
     eng.close()
     if multi and not weak and not args.no_base:
         # the strong-scaling base: the whole mesh on rank 0's GPU alone, timed in this run, so the
@@ -580,6 +589,8 @@ def main():
                 # N=1 line, which is configs[1], a different mesh)
                 out["efficiency_vs_base"] = round(v / base["value"] / nparts, 3)
     if emu:
+        # value is ONE rank block's rate on one GPU, not a measured N-GPU (or whole-mesh) rate
+        out["emulated"] = True
         E_g = gcase.scalars["nelem"]
         out["emulation"] = {
             "world": nparts, "rank": prank, "order": order,

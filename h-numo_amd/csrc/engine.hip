@@ -55,6 +55,8 @@ struct hnumo_engine {
   bool own_stream = true;
   std::string err;
   std::string comm_err;  // first halo-transport failure (sticky until reported)
+  // environment settings this engine read at create, honoured or ignored (hnumo_overrides)
+  std::string overrides;
   hipStream_t stream = nullptr;
   DevMesh m{};
   hnumo_params p{};
@@ -86,6 +88,7 @@ struct hnumo_engine {
   // events recorded inside the captured step around the corrector sub-cycle's stage kernels
   hipEvent_t evk0 = nullptr, evk1 = nullptr;
   bool capturing = false, kernel_events = false, no_graph = false;
+  int graph_env = -1;                        // HNUMO_GRAPH at create: 0 direct launches, 1 capture (RCCL too), -1 unset
   bool no_fuse = false;                      // HNUMO_FUSE=0: face kernels and extract launches (A/B)
   int sched_dbg = 0;                         // HNUMO_SCHED_DBG (timing experiments only, wrong results):
                                              // 1 the interior launch skips its wait for the boundary one
@@ -187,6 +190,26 @@ static T *dalloc(hnumo_engine *eng, size_t n) {
   (void)hipMemset(ptr, 0, (n ? n : 1) * sizeof(T));
   eng->allocs.push_back(ptr);
   return (T *)ptr;
+}
+
+// Environment settings read at engine creation.  Two kinds:
+//  * public (documented in include/hnumo_engine.h): HNUMO_PERSISTENT=0, HNUMO_GRAPH=0|1 (same
+//    bits, another launch schedule) and HNUMO_SUMMATION=reference|factored (any other value is an
+//    error, not a silent switch);
+//  * experiment knobs (A/B timing and the equivalence tests of old behaviour, tests/
+//    test_placement_gpu.py): honoured ONLY when HNUMO_EXPERIMENTS=1 is set as well, ignored
+//    otherwise.
+// Every variable found is recorded in eng->overrides ("NAME=value" honoured, "NAME=value
+// (ignored)" not), which hnumo_overrides returns and bench.py puts in its line, so a stray
+// variable on a benchmark box can never change the measured path unseen.
+static const char *env_knob(hnumo_engine *eng, const char *name, bool experiment = true) {
+  const char *v = getenv(name);
+  if (!v) return nullptr;
+  const char *x = experiment ? getenv("HNUMO_EXPERIMENTS") : nullptr;
+  const bool on = !experiment || (x && x[0] == '1' && x[1] == 0);
+  if (!eng->overrides.empty()) eng->overrides += ';';
+  eng->overrides += std::string(name) + "=" + v + (on ? "" : " (ignored: HNUMO_EXPERIMENTS!=1)");
+  return on ? v : nullptr;
 }
 
 static void face_exchange_qf(hnumo_engine *e, double *qf, int nc);
@@ -930,6 +953,14 @@ extern "C" {
 
 int hnumo_abi_version(void) { return HNUMO_ABI_VERSION; }
 
+int hnumo_overrides(const hnumo_engine *eng, char *out, int64_t len) {
+  if (!eng || !out || len <= 0) return HNUMO_ERR_INVALID;
+  const size_t n = std::min((size_t)len - 1, eng->overrides.size());
+  std::memcpy(out, eng->overrides.data(), n);
+  out[n] = 0;
+  return eng->overrides.size() < (size_t)len ? HNUMO_OK : HNUMO_ERR_INVALID;
+}
+
 const char *hnumo_last_error(const hnumo_engine *eng) { return eng ? eng->err.c_str() : "null engine"; }
 
 void hnumo_engine_destroy(hnumo_engine *eng) {
@@ -1340,29 +1371,36 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
   }
   eng->rhs = dalloc<double>(eng, 3 * npoin);
   eng->neg_flag = dalloc<int>(eng, 1);
-  if (const char *sm = getenv("HNUMO_SUMMATION"))
-    eng->summation = (sm[0] == 'r' || sm[0] == '0') ? HNUMO_SUM_REFERENCE : HNUMO_SUM_FACTORED;
+  if (const char *ge = env_knob(eng, "HNUMO_GRAPH", false)) eng->graph_env = ge[0] == '0' ? 0 : ge[0] == '1' ? 1 : -1;
+  if (const char *sm = env_knob(eng, "HNUMO_SUMMATION", false)) {
+    if (!strcmp(sm, "reference"))
+      eng->summation = HNUMO_SUM_REFERENCE;
+    else if (!strcmp(sm, "factored"))
+      eng->summation = HNUMO_SUM_FACTORED;
+    else
+      return fail(eng, HNUMO_ERR_INVALID, std::string("HNUMO_SUMMATION=") + sm + ": only 'reference' or 'factored'");
+  }
   if (HNUMO_DIAG)  // (diagnostics builds only; see engine_internal.h)
-    if (const char *sd = getenv("HNUMO_STAGE_DBG")) eng->stage_dbg = atoi(sd);
-  if (const char *fz = getenv("HNUMO_FUSE")) eng->no_fuse = fz[0] == '0';
+    if (const char *sd = env_knob(eng, "HNUMO_STAGE_DBG")) eng->stage_dbg = atoi(sd);
+  if (const char *fz = env_knob(eng, "HNUMO_FUSE")) eng->no_fuse = fz[0] == '0';
   // (bit 1 drops a required stream dependency -- wrong results, timing only: diagnostics builds)
   if (HNUMO_DIAG)
-    if (const char *sd = getenv("HNUMO_SCHED_DBG")) eng->sched_dbg = atoi(sd);
+    if (const char *sd = env_knob(eng, "HNUMO_SCHED_DBG")) eng->sched_dbg = atoi(sd);
   // per-stage kernel arena: on meshes that take several residency rounds per stage, the arena
   // sized for 4 workgroups per CU (1-row term chunks) -- 1.566 -> 1.517 ms per stage at C4
   // (tools/ab_env.py, round 2); small meshes keep the 3-per-CU arena
   // large meshes: the LEAN 5-per-CU arena (C4: 1.331 ms per stage against 1.409 for the 4-per-CU
   // one with 2-row term chunks and 1.501 for round 2's, profiles/r03f)
   eng->stage_nb = eng->nelem_owned >= 2048 ? 5 : 0;
-  if (const char *sn = getenv("HNUMO_STAGE_NB")) eng->stage_nb = atoi(sn);
+  if (const char *sn = env_knob(eng, "HNUMO_STAGE_NB")) eng->stage_nb = atoi(sn);
   eng->bcl_big = eng->nelem_owned >= 2048;
-  if (const char *bb = getenv("HNUMO_BCL_BIG")) eng->bcl_big = bb[0] == '1';
-  if (const char *az = getenv("HNUMO_ACC_ZERO")) eng->acc_zero = az[0] == '1';
+  if (const char *bb = env_knob(eng, "HNUMO_BCL_BIG")) eng->bcl_big = bb[0] == '1';
+  if (const char *az = env_knob(eng, "HNUMO_ACC_ZERO")) eng->acc_zero = az[0] == '1';
   {
-    const char *qv = getenv("HNUMO_QPQ");
+    const char *qv = env_knob(eng, "HNUMO_QPQ");
     if (par->botfr && !(qv && atoi(qv) == 0)) eng->qpq = dalloc<double>(eng, (size_t)E * 3 * eng->nq * eng->nq);
   }
-  if (const char *sp = HNUMO_DIAG ? getenv("HNUMO_STAGE_PROF") : nullptr)
+  if (const char *sp = HNUMO_DIAG ? env_knob(eng, "HNUMO_STAGE_PROF") : nullptr)
     if (sp[0] == '1') eng->stage_prof = dalloc<unsigned long long>(eng, (size_t)eng->nelem * 32);
   if (eng->face_halo) {
     eng->rank = halo->rank;
@@ -1497,22 +1535,12 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
     eng->dbg_abort_epoch = dalloc<unsigned long long>(eng, 1);
     if (eng->dbg_abort_epoch) HIPCHK(hipMemset(eng->dbg_abort_epoch, 0xff, sizeof(unsigned long long)));  // never
     for (int b = 0; b < 2; b++) eng->gtr[b] = dalloc<TraceGranule>(eng, (size_t)E * 32 * ngl);
-    const double *qps[2] = {eng->qp, eng->qp2};
-    for (int v = 0; v < 2; v++) {
-      std::vector<StageArgs> st;
-      (void)stage_table(eng, qps[v], st);
-      st.front().qb_in = eng->qb;                        // the step-start state (launch_subcycle)
-      st.front().self_trace = 1;                         // stage 0 publishes its input traces
-      st.back().qb_out = v == 0 ? eng->qbp : eng->qb;    // predictor / corrector result
-      eng->d_stages[v] = dalloc<StageArgs>(eng, st.size());
-      if (eng->alloc_failed) return fail(eng, HNUMO_ERR_DEVICE, "hipMalloc failed (stage tables)");
-      HIPCHK(hipMemcpy(eng->d_stages[v], st.data(), st.size() * sizeof(StageArgs), hipMemcpyHostToDevice));
-    }
-    const char *pe = getenv("HNUMO_PERSISTENT");
-    if (!(pe && pe[0] == '0')) {
-      if (const char *pp = getenv("HNUMO_PERSIST_LDS_PAD")) eng->persist_pad = std::max(0, atoi(pp));
+    const char *pe = env_knob(eng, "HNUMO_PERSISTENT", false);
+    const bool persist_on = !(pe && pe[0] == '0');
+    if (persist_on) {
+      if (const char *pp = env_knob(eng, "HNUMO_PERSIST_LDS_PAD")) eng->persist_pad = std::max(0, atoi(pp));
       // HNUMO_PERSIST_GUARD: 0 none (the in-launch rendezvous alone), 'estimate', 'trial', 1 both
-      if (const char *pg = getenv("HNUMO_PERSIST_GUARD"))
+      if (const char *pg = env_knob(eng, "HNUMO_PERSIST_GUARD"))
         eng->persist_guard = pg[0] == '0' ? 0 : pg[0] == 'e' ? 1 : pg[0] == 't' ? 2 : 3;
       int ncu = 0;
       HIPCHK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, eng->device));
@@ -1522,7 +1550,7 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
       // elements with a physical-boundary face (more work: ghost states, wall fluxes) go to the CUs
       // holding fewer, the others fill the rest in order.  Same arithmetic per element, same bits
       // (dg25L3: 16 us less sub-cycle time per step in 3 interleaved pairs, profiles/r05x).
-      const char *pm = getenv("HNUMO_PERSIST_PERM");
+      const char *pm = env_knob(eng, "HNUMO_PERSIST_PERM");
       if (!(pm && pm[0] == '0') && ncu > 0 && E % ncu && eng->nranks == 1 && !eng->face_halo && eng->comm_mode == 0 &&
           eng->nelem_owned == E) {
         const int nheavy = E % ncu;  // CUs k < nheavy hold one block more
@@ -1545,9 +1573,24 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
         eng->d_eperm = dalloc<int>(eng, E);
         if (eng->d_eperm) HIPCHK(hipMemcpy(eng->d_eperm, perm.data(), E * sizeof(int), hipMemcpyHostToDevice));
         // the element kernels of the step (625 blocks at dg25 too: the same CUs hold one block more)
-        const char *pg = getenv("HNUMO_GLUE_PERM");
+        const char *pg = env_knob(eng, "HNUMO_GLUE_PERM");
         if (!(pg && pg[0] == '0')) eng->m.eperm = eng->d_eperm;
       }
+    }
+    // the stage tables copy eng->m: built after the placement above, so every DevMesh copy (these,
+    // the per-stage tables of stage_table at run time) carries the same eperm
+    const double *qps[2] = {eng->qp, eng->qp2};
+    for (int v = 0; v < 2; v++) {
+      std::vector<StageArgs> st;
+      (void)stage_table(eng, qps[v], st);
+      st.front().qb_in = eng->qb;                        // the step-start state (launch_subcycle)
+      st.front().self_trace = 1;                         // stage 0 publishes its input traces
+      st.back().qb_out = v == 0 ? eng->qbp : eng->qb;    // predictor / corrector result
+      eng->d_stages[v] = dalloc<StageArgs>(eng, st.size());
+      if (eng->alloc_failed) return fail(eng, HNUMO_ERR_DEVICE, "hipMalloc failed (stage tables)");
+      HIPCHK(hipMemcpy(eng->d_stages[v], st.data(), st.size() * sizeof(StageArgs), hipMemcpyHostToDevice));
+    }
+    if (persist_on) {
       // the trial launches: what the dispatcher does, not what the estimate says, decides
       for (int sm = 0; sm < 2 && (eng->persist_guard & 2); sm++) {
         if (!eng->persistent_ok[sm] || eng->comm_mode != 0 || eng->nranks != 1) continue;
@@ -1598,8 +1641,7 @@ static int ensure_graph(hnumo_engine *eng) {
   // into a graph cannot be exercised on a one-GPU box, and at the multi-GPU sizes (~1e4
   // elements per GPU, ~0.2 ms per stage) the host issues a stage's launches faster than the
   // GPU runs them
-  const char *ge = getenv("HNUMO_GRAPH");
-  if (eng->comm_mode == 1 || (ge && ge[0] == '0') || (eng->comm_mode == 2 && !(ge && ge[0] == '1'))) {
+  if (eng->comm_mode == 1 || eng->graph_env == 0 || (eng->comm_mode == 2 && eng->graph_env != 1)) {
     eng->no_graph = true;
     return 0;
   }
@@ -2221,19 +2263,20 @@ int hnumo_group_ti_rk_bcl(hnumo_engine **engines, int n, double **q_df, double *
 // Per-kernel breakdown of a step: `nsteps` direct (uncaptured) steps of the resident device state
 // with an event after every launch on the engine stream; the span between two marks is charged to
 // the kernel family of the later one.  Single-stream engines (one rank) only.
-int hnumo_step_breakdown(hnumo_engine *eng, int nsteps, char *names, int64_t names_len, double *us_per_step,
-                         int max_kernels, int *count) {
-  if (!eng || nsteps < 1 || !names || names_len < 1 || !us_per_step || max_kernels < 1 || !count)
-    return HNUMO_ERR_INVALID;
+// (retry: the per-stage repeat of the steps a persistent launch that gave up left undone, as in
+// run_steps: it neither re-probes nor counts as a run of the back-off wait)
+static int step_breakdown(hnumo_engine *eng, int nsteps, char *names, int64_t names_len, double *us_per_step,
+                          int max_kernels, int *count, bool retry) {
   if (eng->comm_mode != 0 || eng->nranks != 1 || eng->face_halo)
     return fail(eng, HNUMO_ERR_INVALID, "step breakdown: single-rank engines only");
   if (!eng->resident || !eng->uploaded)
     return fail(eng, HNUMO_ERR_INVALID, "step breakdown: needs a resident, uploaded state (hnumo_set_resident)");
   HIPCHK(hipSetDevice(eng->device));
-  int rc = maybe_reprobe(eng);
+  int rc = retry ? 0 : maybe_reprobe(eng);
   if (rc) return rc;
   hnumo_engine::KMarks km;
   HIPCHK(hipMemsetAsync(eng->neg_flag, 0, sizeof(int), eng->stream));
+  HIPCHK(hipMemsetAsync(eng->steps_done, 0, sizeof(unsigned), eng->stream));
   eng->km = &km;
   kmark(eng, "start");
   for (int s = 0; s < nsteps; s++) launch_step(eng);
@@ -2241,15 +2284,20 @@ int hnumo_step_breakdown(hnumo_engine *eng, int nsteps, char *names, int64_t nam
   auto release = [&]() {
     for (hipEvent_t ev : km.ev) (void)hipEventDestroy(ev);
   };
-  if (hipStreamSynchronize(eng->stream) != hipSuccess || hipMemcpy(eng->h_neg, eng->neg_flag, sizeof(int),
-                                                                    hipMemcpyDeviceToHost) != hipSuccess) {
+  if (hipStreamSynchronize(eng->stream) != hipSuccess ||
+      hipMemcpy(eng->h_neg, eng->neg_flag, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(eng->h_steps, eng->steps_done, sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess) {
     release();
     return fail(eng, HNUMO_ERR_DEVICE, "step breakdown: HIP error");
   }
   if ((*eng->h_neg & RUN_ABORT) && use_persistent(eng)) {
+    // the steps completed before the abort stand (their errors are reported); the rest are redone
+    // and timed on per-stage launches, so the state advances by exactly nsteps
     release();
+    const int done = (int)*eng->h_steps;
+    if ((rc = flag_error(eng, *eng->h_neg & ~RUN_ABORT))) return rc;
     persistent_abort(eng);
-    return hnumo_step_breakdown(eng, nsteps, names, names_len, us_per_step, max_kernels, count);
+    return step_breakdown(eng, nsteps - done, names, names_len, us_per_step, max_kernels, count, true);
   }
   if ((rc = flag_error(eng, *eng->h_neg))) {
     release();
@@ -2282,6 +2330,13 @@ int hnumo_step_breakdown(hnumo_engine *eng, int nsteps, char *names, int64_t nam
   std::memcpy(names, joined.c_str(), joined.size() + 1);
   *count = nk;
   return 0;
+}
+
+int hnumo_step_breakdown(hnumo_engine *eng, int nsteps, char *names, int64_t names_len, double *us_per_step,
+                         int max_kernels, int *count) {
+  if (!eng || nsteps < 1 || !names || names_len < 1 || !us_per_step || max_kernels < 1 || !count)
+    return HNUMO_ERR_INVALID;
+  return step_breakdown(eng, nsteps, names, names_len, us_per_step, max_kernels, count, false);
 }
 
 }  // extern "C"

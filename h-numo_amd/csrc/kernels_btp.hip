@@ -30,80 +30,20 @@
 //       next stage, written straight into the neighbours' trace slots.
 #include "engine_internal.h"
 
-// Reference-order volume integral without term buffers ("on the fly", OTF) from this NGL on:
-// one thread per (component v, node p) computes its terms T(v,p,q) itself, in quad order, as
-// it sums them.  Same terms, same order, same bits as the chunked term buffers; no [3P][Q]
-// LDS staging (46 KB at N=7) and one D phase instead of NCH+1 -- at N=7 the chunked arena
-// allows one workgroup per CU.
-#ifndef HNUMO_OTF_MIN_NGL
-#define HNUMO_OTF_MIN_NGL 8
-#endif
-// The slim OTF arena (StageCfg::SLIM); 0 keeps the round-1 layout for A/B measurement.
-#ifndef HNUMO_SLIM
-#define HNUMO_SLIM 1
-#endif
-#ifndef HNUMO_SLIM_LATE
-#define HNUMO_SLIM_LATE 1
-#endif
-#ifndef HNUMO_OTF_PAIR
-#define HNUMO_OTF_PAIR 1
-#endif
-// Interleaved basis in LDS (PDI): psiq(n, iq) and dpsiq(n, iq) adjacent, read together with one
-// ds_read_b128 where the pair is needed (the volume terms) instead of two rows NGL*NQ apart
-#ifndef HNUMO_PDI
-#define HNUMO_PDI 1
-#endif
-// N=7 volume sums of the persistent kernel: all three components of a node on one thread (TRIPLE,
-// sharing hi, dhdx, dhdy), their face lifts on three waves after the barrier
-#ifndef HNUMO_I4
-#define HNUMO_I4 1
-#endif
-#ifndef HNUMO_QPM
-#define HNUMO_QPM 1
-#endif
-// E (EW0 == 0): the new state's grad(u_bar) on four waves, one component each (nodal_grad, the
-// same terms and order as nodal_grad4's), after a barrier, instead of on the E1 wave alone
-#ifndef HNUMO_EGRAD4
-#define HNUMO_EGRAD4 1
-#endif
-#ifndef HNUMO_OTF_TRIPLE
-#define HNUMO_OTF_TRIPLE 1
-#endif
-#ifndef HNUMO_OPAIR_PERSIST
-#define HNUMO_OPAIR_PERSIST 1
-#endif
-#ifndef HNUMO_OTF_UNROLL
-#define HNUMO_OTF_UNROLL 3
-#endif
-// Chunked D phases (StageCfg::VSUM): term tasks split in two node halves, and one summing thread
-// per (component, node) for the whole volume integral (its partial sum in a register)
-#ifndef HNUMO_VSUM
-#define HNUMO_VSUM 1
-#endif
-// The lean per-stage arenas of large meshes (StageCfg::LEAN); 0 keeps the round-2 layout for A/B.
-#ifndef HNUMO_LEAN
-#define HNUMO_LEAN 1
-#endif
-// Wave priorities by role (stage_body, s_setprio; 0: off).  On a CU holding three elements the
-// elements' waves compete for the SIMDs; the waves whose chains a phase waits for -- the volume
-// sums, the last D phase, E -- issue ahead of the ones with slack (the term tasks, which finish
-// behind the sums anyway): PRIO_S for the summing waves in D, PRIO_E for the last D phase and E,
-// 0 for the term tasks, 1 elsewhere
-#ifndef HNUMO_PRIO
-#define HNUMO_PRIO 1
-#endif
-#ifndef HNUMO_PRIO_S
-#define HNUMO_PRIO_S 2
-#endif
-#ifndef HNUMO_PRIO_E
-#define HNUMO_PRIO_E 3
-#endif
-#ifndef HNUMO_PRIO_L
-#define HNUMO_PRIO_L HNUMO_PRIO_E
-#endif
-#ifndef HNUMO_PRIO_B
-#define HNUMO_PRIO_B 1
-#endif
+// Design constants (the alternatives each replaced were measured and removed):
+// OTF_MIN_NGL: from this NGL on the reference-order volume integral runs without term buffers
+//   ("on the fly", OTF): one thread per (component v, node p) computes its terms T(v,p,q) itself, in
+//   quad order, as it sums them -- same terms, same order, same bits as the chunked term buffers,
+//   without their [3P][Q] LDS staging (46 KB at N=7), so the persistent N=7 arena fits 3 per CU;
+// OTF_UNROLL: unroll of the on-the-fly sums' inner quad loop;
+// PRIO_*: wave priorities by role (stage_body, s_setprio).  On a CU holding three elements the
+//   elements' waves compete for the SIMDs; the waves whose chains a phase waits for -- the volume
+//   sums, the last D phase, E -- issue ahead of the ones with slack (the term tasks, which finish
+//   behind the sums anyway): PRIO_S for the summing waves in D, PRIO_E for the last D phase and E,
+//   0 for the term tasks, PRIO_B elsewhere.
+constexpr int OTF_MIN_NGL = 8;
+#define OTF_UNROLL 3
+constexpr int PRIO_B = 1, PRIO_S = 2, PRIO_E = 3;
 // Diagnostics (HNUMO_DIAG builds only, engine_internal.h; timing experiments, most break the
 // physics): StageArgs::dbg phase switches -- 1 the face lifts of the volume sums, 2 the Laplacian,
 // 4 the volume sums, 16 the persistent trace waits, 32 the time averages (engine), 64 the term
@@ -264,7 +204,8 @@ struct StageCfg {
   static constexpr int ECO = eco_stride(Q, P);              // ecoef record per element (4Q + 5P, even)
   static constexpr int NB = 2 * NGL * NQ + NGL * NGL;       // psiq, dpsiq, dpsi (+ a zero slot)
   static_assert(Q <= BS, "one quad-point task per thread");
-  static constexpr bool OTF = !SF && NGL >= HNUMO_OTF_MIN_NGL;
+  static constexpr bool OTF = !SF && NGL >= OTF_MIN_NGL;
+  // SLIM, SLATE, OPAIR and QPM name four aspects of the one OTF arena (all on together with OTF):
   // SLIM (OTF): an arena small enough for 3 workgroups per CU, so the persistent sub-cycle holds
   // all 625 elements of dg25 at N=7 at once.  The last wave (EW), idle beside the on-the-fly
   // volume sums of waves 0..2, runs the LDG volume fluxes, LDG face fluxes and the Laplacian
@@ -272,16 +213,16 @@ struct StageCfg {
   // pbprime, the nodal coefficients, the Laplacian -- lives in that wave's registers (loaded
   // from global memory while waves 0..2 sum) instead of LDS; the new state overwrites the
   // stage input in place; the bottom-layer qprime (A2 only) overlays the nodal gradients.
-  static constexpr bool SLIM = OTF && HNUMO_SLIM;
+  static constexpr bool SLIM = OTF;
   // SLATE (SLIM): the face fluxes also run on the last wave in D, so the neighbour traces are
   // needed (persistent: polled) only there, behind the element's own interpolation, quad-point
   // physics and most of its volume sums -- the neighbours' stage-to-stage skew hides behind them;
   // the volume sums' face lifts follow a barrier
-  static constexpr bool SLATE = SLIM && HNUMO_SLIM_LATE;
-  // OPAIR (SLATE): a node's component-1 and -2 volume sums on one thread (see otf_sum12).  Used by
-  // the per-stage kernel only (stage_body's PERSIST = false): at dg25N7L3 it took the per-stage
-  // launch from 65.0 to 57.0 us, but the persistent sub-cycle from 56.4 to 63.6 us
-  static constexpr bool OPAIR = SLATE && HNUMO_OTF_PAIR;
+  static constexpr bool SLATE = SLIM;
+  // OPAIR (SLATE): a node's component-1 and -2 volume sums on one thread (see otf_sum12) in the
+  // per-stage kernel (dg25N7L3: 65.0 -> 57.0 us per launch); the persistent sub-cycle instead sums
+  // all three components of a node on one thread (otf_sum012, TRIPLE)
+  static constexpr bool OPAIR = SLATE;
   static constexpr int EW = BS / 64 - 1;
   // LEAN (the per-stage kernel's arenas for large meshes, NBK != 0): less fixed LDS so that more
   // workgroups fit a CU or more quad rows fit a term chunk -- E1 on the last wave (the volume-sum
@@ -289,7 +230,7 @@ struct StageCfg {
   // during D) instead of LDS; the right-hand side and the Laplacian in the term buffer that is dead
   // in the last D phase, the new state in the other one (dead after D), the face-quad traces of
   // FPRE in term buffer 0 (A2 -> B; D0 writes it first)
-  static constexpr bool LEAN = HNUMO_LEAN && NBK != 0 && !SF && !OTF;
+  static constexpr bool LEAN = NBK != 0 && !SF && !OTF;
   // G16: 16-byte LDS-DMA for the element's records (glds_copy).  Not in the slim N=7 arena: there
   // it measured slower (dg25N7L3 persistent 50.2 -> 53.0 us per stage, while dg25L3 persistent
   // 13.0 -> 12.7 and C4 1.322 -> 1.296 ms; profiles/r03h)
@@ -304,7 +245,7 @@ struct StageCfg {
   // A2's interpolations in slots 0..3 and the bottom layer's in 4..6 until B overwrites them -- so the
   // on-the-fly sums read a quad point's 8 values as four ds_read_b128 from one address; w moves out of
   // s_qk, which keeps the metric pairs alone (16-byte aligned)
-  static constexpr bool QPM = SLIM && HNUMO_QPM;
+  static constexpr bool QPM = SLIM;
   static constexpr int QKR = QPM ? 4 : QE_KEEP;  // s_qk rows
   static constexpr int al2(int x) { return (x + 1) & ~1; }
   static constexpr int O_BASIS = 0, O_EREC = ev(O_BASIS + NB + 1), O_QB = ev(O_EREC + ERSD), O_Q0 = O_QB + 4 * P,
@@ -323,7 +264,7 @@ struct StageCfg {
                        O_QN = O_LAP + ((SLIM || LEAN) ? 0 : 2 * P), O_Y = O_W,
                        W_END0 = O_QN + ((SLIM || LEAN) ? 0 : 4 * P),
                        QN_END_W = W_END0 - O_W,
-                       W_END = (SLIM && !SLATE && O_W + 32 * NQ > W_END0) ? O_W + 32 * NQ : W_END0,
+                       W_END = W_END0,
                        O_BIN = ev((SF && O_Y + NYV * NGL * NQ > W_END) ? O_Y + NYV * NGL * NQ : W_END);
   // B inputs: the bottom-layer qprime, face statics, neighbour traces, face coefficients,
   // reloaded every stage (the persistent kernel: re-fetched behind E1) and overlaid by term
@@ -359,7 +300,7 @@ struct StageCfg {
   // FPRE (exact): A2 also interpolates each face's own-side traces and, on physical
   // boundaries, the ghost-side traces to the face quad points, into s_fi [8][4*NQ] (in the
   // W region, dead from A to D0), so B's face fluxes interpolate only the neighbour traces
-  static constexpr bool FPRE = !SF && !SLATE && (SLIM || LEAN || 4 * NQ * 8 <= QN_END_W);
+  static constexpr bool FPRE = !SF && !SLATE && (LEAN || 4 * NQ * 8 <= QN_END_W);
   static constexpr int WTMAX = QC * NGL;  // term tasks of a full chunk
   // VSUM (exact, chunked D): a chunk's term tasks split in two node halves on threads
   // [0, 2*WTMAX) (the longest lane forms ceil(NGL/2) nodes' terms instead of NGL), and the 3P
@@ -367,7 +308,7 @@ struct StageCfg {
   // phase, the partial sum in a register (instead of 3 chains per thread through s_rhs); qq and
   // the LDG face fluxes (D0, no sums yet) after the terms
   static constexpr int OVS = BS - 3 * P;
-  static constexpr bool VSUM = HNUMO_VSUM && !SF && !OTF && 2 * WTMAX <= OVS &&
+  static constexpr bool VSUM = !SF && !OTF && 2 * WTMAX <= OVS &&
                                2 * WTMAX + P <= BS && OL >= 2 * WTMAX + P && OL + 4 * NGL <= BS;
   // NSPLIT: node groups of the term tasks (VSUM: two node halves), task t = (group t / WTMAX,
   // task t % WTMAX) on thread t.  (Measured, not kept: one group in the LEAN arenas, thirds, and the
@@ -494,18 +435,14 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   double *const S = s_arena;
   // basis: psiq [NGL][NQ], dpsiq [NGL][NQ] (PDI: interleaved [NGL][NQ][2]), dpsi [NGL][NGL] + a zero slot
   const double *s_psiq = S + C::O_BASIS, *s_dpsiq = s_psiq + NGL * NQ, *s_dpsi = s_dpsiq + NGL * NQ;
-  constexpr bool PDI = HNUMO_PDI;
-  auto PSQ = [&](int x) -> double { return PDI ? s_psiq[2 * x] : s_psiq[x]; };
-  auto DPSQ = [&](int x) -> double { return PDI ? s_psiq[2 * x + 1] : s_dpsiq[x]; };
+  // (interleaved, m.basis_pd: psiq(n, iq) and dpsiq(n, iq) adjacent, read together with one
+  // ds_read_b128 where the pair is needed -- the volume terms)
+  auto PSQ = [&](int x) -> double { return s_psiq[2 * x]; };
+  auto DPSQ = [&](int x) -> double { return s_psiq[2 * x + 1]; };
   auto PDQ = [&](int x, double &pv, double &dv) {
-    if constexpr (PDI) {
-      const double2 w = reinterpret_cast<const double2 *>(s_psiq)[x];
-      pv = w.x;
-      dv = w.y;
-    } else {
-      pv = s_psiq[x];
-      dv = s_dpsiq[x];
-    }
+    const double2 w = reinterpret_cast<const double2 *>(s_psiq)[x];
+    pv = w.x;
+    dv = w.y;
   };
   const int *s_er = reinterpret_cast<const int *>(S + C::O_EREC);
   const int *s_side = s_er + EREC_SIDE, *s_bc = s_er + EREC_BC;
@@ -556,7 +493,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     if (tid == 0) s_prof[20] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // XCC_ID
   }
   STAGE_MARK(0);
-  if (HNUMO_PRIO) __builtin_amdgcn_s_setprio(HNUMO_PRIO_B);
+  __builtin_amdgcn_s_setprio(PRIO_B);
   if (PROF && tid == 0) s_prof[22] = 0;
   const bool use_q0 = !a.rhs_only && a.a1 != 0.0, use_q2 = !a.rhs_only && a.a3 != 0.0;
   const int qpm = (SF || !m.botfr || !a.qpq) ? 0 : a.qpq_mode;  // see StageArgs::qpq
@@ -565,7 +502,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     const bool tsl = !PERSIST && m.etsrc && !a.tcontig;
     const int4 ts = tsl ? slot_ids4(m.etsrc + 4 * e) : make_int4(0, 0, 0, 0);
     if (!PERSIST || first) {
-      glds_copy<BS, C::G16>(PDI ? m.basis_pd : m.basis, S + C::O_BASIS, 2 * C::NB, tid, rot);
+      glds_copy<BS, C::G16>(m.basis_pd, S + C::O_BASIS, 2 * C::NB, tid, rot);
       glds_copy<BS, C::G16>(m.erec + (size_t)e * C::ERS, S + C::O_EREC, C::ERS, tid, rot);
       glds_copy<BS, C::G16>(m.qstatE + (size_t)e * qe_stride(Q) + (QPM ? Q : 0), s_qk, 2 * C::QKR * Q, tid, rot);
       if constexpr (!C::SLIM) glds_copy<BS, C::G16>(a.ecoef + (size_t)e * C::ECO + 4 * Q, s_nc, 2 * 5 * P, tid, rot);
@@ -767,7 +704,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     const bool full = !PERSIST || first;
     // I4 (more quad points than half the block): one task per quad point forms all four of
     // (dp, dpp, udp, vdp) -- one pass instead of two -- and the bottom layer's three another
-    constexpr bool I4 = !SF && HNUMO_I4 && 2 * Q > BS;
+    constexpr bool I4 = !SF && 2 * Q > BS;
     const int ng = (m.botfr && qpm != 2) ? 3 : 2;
     constexpr int TPG = SF ? NQ * NGL : Q;  // tasks per group
     const int nint = (I4 ? ng - 1 : ng) * TPG;
@@ -1391,42 +1328,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     LDS_BARRIER();
     STAGE_MARK(7);
   } else if constexpr (C::OTF) {
-    // D (OTF): thread (v, p) sums rhs(v,p) = sum_q T(v,p,q) in quad order, computing each term
+    // D (OTF): rhs(v,p) = sum_q T(v,p,q) summed in quad order by one thread, each term computed
     // as it goes (create_rhs_btp_volume_qdf, mod_rhs_btp.F90:194-206):
     //   T(0) = wq*(dhdx*udp + dhdy*vdp), T(1) = wq*(hi*scx + dhdx*A + quv*dhdy),
     //   T(2) = wq*(hi*scy + dhdx*quv + dhdy*B)
-    // written uniformly as T = wq*((hi*s1 + dhdx*s2) + s3*dhdy) with s1 = 0 for v = 0: the
-    // extra (hi*0) adds a signed zero, which leaves any non-zero partial sum unchanged, and a
-    // zero term can only differ in the sign of zero -- added to a sum that starts at +0 it
-    // changes nothing (round-to-nearest never produces -0 from +0 + x).  Then the face
-    // projections; qq and the LDG face fluxes run beside; the Laplacian after the barrier.
-    // (quad-point values by role: QO(k, q), k = 0..6 = udp, vdp, scx, A, quv, scy, B; QW, QK -- see QPM)
-    auto otf_sum = [&](int t) {
-      const int v = t / P, p = t % P, i = p % NGL, j = p / NGL;
-      const int r1 = v == 2 ? 5 : 2, r2 = v == 0 ? 0 : (v == 1 ? 3 : 4), r3 = v == 0 ? 1 : (v == 1 ? 4 : 6);
-      const bool z1 = v == 0;
-      const int bi = i * NQ, bj = j * NQ;
-      double acc = 0.0;
-#pragma unroll 1
-      for (int jq = 0; jq < NQ; jq++) {
-        double pj, dpj;
-        PDQ(bj + jq, pj, dpj);
-        const int q0 = jq * NQ;
-#pragma unroll HNUMO_OTF_UNROLL
-        for (int iq = 0; iq < NQ; iq++) {
-          const int q = q0 + iq;
-          double pi, dpi;
-          PDQ(bi + iq, pi, dpi);
-          const double hi = pi * pj, h_e = dpi * pj, h_n = pi * dpj;
-          const double dhdx = h_e * QK(QE_EX, q) + h_n * QK(QE_NX, q);
-          const double dhdy = h_e * QK(QE_EY, q) + h_n * QK(QE_NY, q);
-          const double s1 = z1 ? 0.0 : QO(r1, q);
-          acc = acc + QW(q) * ((hi * s1 + dhdx * QO(r2, q)) + QO(r3, q) * dhdy);
-        }
-      }
-      return acc;
-    };
-    auto otf_task = [&](int t, bool) { s_rhs[t] = face_proj(t / P, t % P, otf_sum(t)); };
+    // Then the face projections; qq and the LDG face fluxes run beside; the Laplacian after the
+    // barrier.  (quad-point values by role: QO(k, q), k = 0..6 = udp, vdp, scx, A, quv, scy, B; QW,
+    // QK -- see QPM)
     // OPAIR: node p's component-0 sum on one thread (without the zero hi*s1 term: the
     // reference's own wq*(dhdx*udp + dhdy*vdp)), its component-1 and -2 sums together on
     // another, sharing hi, dhdx, dhdy -- 36 instead of 48 f64 operations per (p, q), the same
@@ -1440,7 +1348,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         double pj, dpj;
         PDQ(bj + jq, pj, dpj);
         const int q0 = jq * NQ;
-#pragma unroll HNUMO_OTF_UNROLL
+#pragma unroll OTF_UNROLL
         for (int iq = 0; iq < NQ; iq++) {
           const int q = q0 + iq;
           double pi, dpi;
@@ -1462,7 +1370,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         double pj, dpj;
         PDQ(bj + jq, pj, dpj);
         const int q0 = jq * NQ;
-#pragma unroll HNUMO_OTF_UNROLL
+#pragma unroll OTF_UNROLL
         for (int iq = 0; iq < NQ; iq++) {
           const int q = q0 + iq;
           double pi, dpi;
@@ -1489,7 +1397,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         double pj, dpj;
         PDQ(bj + jq, pj, dpj);
         const int q0 = jq * NQ;
-#pragma unroll HNUMO_OTF_UNROLL
+#pragma unroll OTF_UNROLL
         for (int iq = 0; iq < NQ; iq++) {
           const int q = q0 + iq;
           double pi, dpi;
@@ -1507,14 +1415,14 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       acc1 = a1;
       acc2 = a2;
     };
-    if constexpr (C::SLIM) {
+    {
       // waves 0..EW-1: the volume sums; the last wave: its register loads, qq, the LDG face
       // fluxes and the Laplacian (it alone writes and reads qq and the face fluxes: a wave-local
       // LDS wait, no barrier)
-      double acc_r = 0.0, acc_r2 = 0.0;  // SLATE: this thread's volume sum(s), lifted after the barrier
-      if (HNUMO_PRIO) SETPRIO_IF(tid < C::EW * 64, HNUMO_PRIO_S, HNUMO_PRIO_B);  // the volume sums ahead
+      double acc_r = 0.0, acc_r2 = 0.0;  // this thread's volume sum(s), lifted after the barrier
+      SETPRIO_IF(tid < C::EW * 64, PRIO_S, PRIO_B);  // the volume sums ahead
       if (tid < C::EW * 64) {
-        if constexpr (HNUMO_OTF_TRIPLE && PERSIST && C::SLATE) {
+        if constexpr (PERSIST) {  // (TRIPLE: the three sums of a node on one thread)
           if (tid < P) {
             double a1_, a2_;
             otf_sum012(tid, acc_r, a1_, a2_);
@@ -1522,21 +1430,16 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
             s_rhs[2 * P + tid] = a2_;
           }
           if (PROF && tid == 0) s_prof[28] = clock64();
-        } else if constexpr (C::OPAIR && (!PERSIST || HNUMO_OPAIR_PERSIST)) {
+        } else {  // (OPAIR: component 0 on wave 0, components 1 and 2 together on wave 1)
           if (tid < P)
             acc_r = otf_sum0(tid);
           else if (tid >= 64 && tid < 64 + P)
             otf_sum12(tid - 64, acc_r, acc_r2);
           if (PROF && tid == 0) s_prof[28] = clock64();
-        } else if constexpr (C::SLATE) {
-          if (tid < 3 * P) acc_r = otf_sum(tid);
-          if (PROF && tid == 0) s_prof[28] = clock64();
-        } else {
-          for (int t = tid; t < 3 * P; t += C::EW * 64) otf_task(t, true);
         }
       } else {
         const int p = tid - C::EW * 64;
-        // the E1 lane's values (see StageCfg::SLIM), loaded now or, SLATE, after the Laplacian
+        // the E1 lane's values (see StageCfg::SLIM), loaded after the Laplacian
         auto load_e1 = [&]() {
           if (p < P) {
             const double *q0s = PERSIST ? a.qsv + (size_t)e * 8 * P : a.qb0 + (size_t)e * 4 * P;
@@ -1550,7 +1453,6 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
             r_pb = m.nstatE[((size_t)e * NE_N + NE_PB) * P + p];
           }
         };
-        if constexpr (!C::SLATE) load_e1();
         if (p < P) {
           const double *nco = a.ecoef + (size_t)e * C::ECO + 4 * Q + p;
           double nc[5];
@@ -1560,56 +1462,43 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
 #pragma unroll
           for (int c = 0; c < 4; c++) s_qq[c * P + p] = nc[NC_PV] * s_grad[c * P + p] + nc[NC_D1 + c];
         }
-        if constexpr (C::SLATE) {
-          // the neighbour traces (persistent: checked now), then the face fluxes
-          issue_granules_wave();
-          poll_wave();
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          for (int t = p; t < 4 * NQ; t += 64) face_task(t);
-          asm volatile("" ::: "memory");
-        }
+        // the neighbour traces (persistent: checked now), then the face fluxes (SLATE)
+        issue_granules_wave();
+        poll_wave();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int t = p; t < 4 * NQ; t += 64) face_task(t);
+        asm volatile("" ::: "memory");
         if (p < 4 * NGL) ldg_task(p, false);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (p < P && !DBG(2)) {
           r_lap[0] = lap_val(0, p);
           r_lap[1] = lap_val(1, p);
         }
-        if constexpr (C::SLATE) load_e1();
+        load_e1();
         if (PROF && p == 0) s_prof[23] = clock64();  // (the last wave's D work done)
       }
-      if constexpr (C::SLATE) {
+      {
         LDS_BARRIER();  // the face fluxes are in
         STAGE_MARK(6);
-        if constexpr (HNUMO_OTF_TRIPLE && PERSIST && C::SLATE) {
+        if constexpr (PERSIST) {
           if (tid < P) {
             s_rhs[tid] = face_proj(0, tid, acc_r);
           } else if ((tid & 63) < P && tid < 3 * 64) {
             const int v = tid >> 6, p = tid & 63;
             s_rhs[v * P + p] = face_proj(v, p, s_rhs[v * P + p]);
           }
-        } else if constexpr (C::OPAIR && (!PERSIST || HNUMO_OPAIR_PERSIST)) {
+        } else {
           if (tid < P) {
             s_rhs[tid] = face_proj(0, tid, acc_r);
           } else if (tid >= 64 && tid < 64 + P) {
             s_rhs[P + tid - 64] = face_proj(1, tid - 64, acc_r);
             s_rhs[2 * P + tid - 64] = face_proj(2, tid - 64, acc_r2);
           }
-        } else if (tid < 3 * P) {
-          s_rhs[tid] = face_proj(tid / P, tid % P, acc_r);
         }
       }
       LDS_BARRIER();
-      STAGE_MARK(C::SLATE ? 7 : 6);
-      if (HNUMO_PRIO) SETPRIO_IF(tid >= C::EW * 64, HNUMO_PRIO_E, HNUMO_PRIO_B);  // E1 runs on the last wave
-    } else {
-      for_tasks<BS>(tid, 0, 3 * P, otf_task);
-      for_tasks<BS>(tid, 3 * P, P, [&](int t, bool) { qq_task(t); });
-      for_tasks<BS>(tid, 4 * P, 4 * NGL, ldg_task);
-      LDS_BARRIER();
-      STAGE_MARK(6);
-      for_tasks<BS>(tid, 0, 2 * P, [&](int t, bool) { lap_task(t / P, t % P); });
-      LDS_BARRIER();
       STAGE_MARK(7);
+      SETPRIO_IF(tid >= C::EW * 64, PRIO_E, PRIO_B);  // E1 runs on the last wave
     }
   } else {
     // D0 .. D_NCH: weak-form terms T(v,p,q) of quad-row chunk k computed in parallel into
@@ -1832,13 +1721,11 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       }
     }
     // the term-task waves behind everything else, the summing waves ahead
-    if (HNUMO_PRIO)
-      SETPRIO_IF(VSUM ? tid >= C::OVS - (C::OVS & 63) : (OSUM == BS - 64 && tid >= OSUM),
-                 HNUMO_PRIO_S, 0);
+    SETPRIO_IF(VSUM ? tid >= C::OVS - (C::OVS & 63) : (OSUM == BS - 64 && tid >= OSUM), PRIO_S, 0);
 #pragma unroll
     for (int k = 0; k <= NCH; k++) {
       asm volatile("" ::: "memory");  // keep LDS reads inside their phase (no hoisting)
-      if (HNUMO_PRIO && k == NCH) __builtin_amdgcn_s_setprio(HNUMO_PRIO_L);
+      if (k == NCH) __builtin_amdgcn_s_setprio(PRIO_E);
       const int WT = (k < NCH) ? ((k == NCH - 1) ? (Q - k * QC) : QC) * NGL : 0;  // term tasks
       if constexpr (VSUM) {
         // first node halves on [0, WT), second halves on [WTMAX, WTMAX + WT)
@@ -1880,7 +1767,6 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   }
 
   // ------------------------------------------------------------- E1: update + wall fix
-  if (HNUMO_PRIO && !C::OTF && HNUMO_PRIO_L != HNUMO_PRIO_E) __builtin_amdgcn_s_setprio(HNUMO_PRIO_E);
   // (SLIM: on the last wave, with its registers; otherwise wave 0)
   constexpr int EW0 = (C::SLIM || C::LEAN) ? C::EW * 64 : 0;
   static_assert(P <= 64, "E1 and the nodal gradients run on one wave");
@@ -1932,7 +1818,9 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     s_v[p] = qn[3] / qn[0];
   }
   if (a.rhs_only) return;
-  if (a.write_trace && HNUMO_EGRAD4 && EW0 == 0 && BS == 256) {
+  if (a.write_trace && EW0 == 0 && BS == 256) {
+    // the new state's grad(u_bar) on four waves, one component each (nodal_grad: the same terms
+    // and order as nodal_grad4's), after a barrier, instead of on the E1 wave alone
     LDS_BARRIER();  // u_bar, v_bar of every node
     if ((tid & 63) < P) {
       const int c = tid >> 6, p = tid & 63, i = p % NGL, j = p / NGL;
@@ -1976,7 +1864,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         a.trace_out[slot] = val;
     }
   }
-  if (HNUMO_PRIO) __builtin_amdgcn_s_setprio(HNUMO_PRIO_B);
+  __builtin_amdgcn_s_setprio(PRIO_B);
   if constexpr (REGACC) {
     // the sub-cycle's last stage: each accumulating thread writes its time averages once, scaled
     // as btp_finalize_kernel scales the atomically summed ones (mod_rk_mlswe.F90:124-149); the

@@ -64,6 +64,7 @@ def lib():
         L.hnumo_debug_force_abort.argtypes = [vp, C.c_int]
         L.hnumo_step_breakdown.argtypes = [vp, C.c_int, C.c_char_p, C.c_int64, dp, C.c_int, C.POINTER(C.c_int)]
         L.hnumo_stream_copy_bw.argtypes = [C.c_int, C.c_int64, C.c_int, dp]
+        L.hnumo_overrides.argtypes = [vp, C.c_char_p, C.c_int64]
         _lib = L
     return _lib
 
@@ -188,6 +189,14 @@ class Engine:
         self._check(lib().hnumo_persistent_stats(self.h, out))
         v = list(out)
         return {"aborts": v[0], "reprobes": v[1], "recovered": v[2], "wait": v[3]}
+
+    @property
+    def overrides(self) -> list:
+        """The HNUMO_* environment settings this engine read at create (hnumo_overrides):
+        "NAME=value", with " (ignored: HNUMO_EXPERIMENTS!=1)" for experiment knobs not honoured."""
+        buf = C.create_string_buffer(4096)
+        self._check(lib().hnumo_overrides(self.h, buf, len(buf)))
+        return [x for x in buf.value.decode().split(";") if x]
 
     def debug_force_abort(self, k: int):
         """Test hook: the k-th persistent sub-cycle launch from now (0 = the next) gives up as a

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define HNUMO_ABI_VERSION 8
+#define HNUMO_ABI_VERSION 9
 
 enum {
   HNUMO_OK = 0,
@@ -226,7 +226,8 @@ int hnumo_sync(hnumo_engine *eng, double *q_df, double *qb_df, double *qprime_df
  * but the momentum RHS is a difference of terms ~1e7 times larger, so reordering moves
  * it by up to ~1e-6 relative and the state by ~1e-7 relative after a few steps: outside
  * the 1e-10 parity bar, hence opt-in.  Environment override at create:
- * HNUMO_SUMMATION=reference|factored.  hnumo_get_summation returns the mode.          */
+ * HNUMO_SUMMATION=reference|factored (any other value: create fails with code 4).
+ * hnumo_get_summation returns the mode.                                               */
 #define HNUMO_SUM_REFERENCE 0
 #define HNUMO_SUM_FACTORED 1
 int hnumo_set_summation(hnumo_engine *eng, int mode);
@@ -292,6 +293,14 @@ int hnumo_debug_stage_profile(hnumo_engine *eng, uint64_t *out, int64_t n);
  * per step in us_per_step[0..count).  The state advances by nsteps steps.               */
 int hnumo_step_breakdown(hnumo_engine *eng, int nsteps, char *names, int64_t names_len,
                          double *us_per_step, int max_kernels, int *count);
+
+/* Environment settings the engine read at create (ABI v9), ';'-joined "NAME=value" (with
+ * " (ignored: HNUMO_EXPERIMENTS!=1)" appended where not honoured); "" when none.  Public
+ * settings: HNUMO_PERSISTENT=0, HNUMO_GRAPH=0|1 (launch schedule, same bits) and
+ * HNUMO_SUMMATION.  Every other HNUMO_* knob is an A/B experiment switch honoured only
+ * with HNUMO_EXPERIMENTS=1.  Returns 4 if `len` bytes (incl. the terminator) were too few
+ * (the text is cut).                                                                   */
+int hnumo_overrides(const hnumo_engine *eng, char *out, int64_t len);
 
 /* Stream-copy bandwidth of `device` (ABI v8): 16-byte copy kernels between two buffers of
  * `bytes` each -- grid-stride with default and with non-temporal loads/stores, and a one-pass

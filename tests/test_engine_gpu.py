@@ -358,9 +358,12 @@ def test_stage_arenas_match_reference_golden(nb, case_factory, monkeypatch):
     case = case_factory(str(g["config"]), **overrides_of(g))
     monkeypatch.setenv("HNUMO_PERSISTENT", "0")
     monkeypatch.setenv("HNUMO_STAGE_NB", nb)
+    monkeypatch.setenv("HNUMO_EXPERIMENTS", "1")
     e = Engine(case)
     monkeypatch.delenv("HNUMO_PERSISTENT")
     monkeypatch.delenv("HNUMO_STAGE_NB")
+    monkeypatch.delenv("HNUMO_EXPERIMENTS")
+    assert e.overrides == ["HNUMO_STAGE_NB=" + nb, "HNUMO_PERSISTENT=0"]
     assert e.stage_path == "per-stage"
     q, qb, qp = e.state()
     e.ti_rk_bcl(q, qb, qp)

@@ -34,6 +34,7 @@ def test_face_halo_every_stage_arena_matches_reference_mpi(nb, monkeypatch):
     other arena forced on a large mesh (HNUMO_STAGE_NB; the default there is the 5-per-CU LEAN
     arena), C5 at its stated size (10,000 elements per rank) still equals the reference under
     mpiexec bit for bit on every rank."""
+    monkeypatch.setenv("HNUMO_EXPERIMENTS", "1")
     monkeypatch.setenv("HNUMO_STAGE_NB", nb)
     _face_halo_run("lake200_mpi4m_step1")
 

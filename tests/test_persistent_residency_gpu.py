@@ -32,6 +32,7 @@ def assert_golden(g, q, qb, qp):
 
 def make_engine(case, monkeypatch, guard):
     from hnumo.engine import Engine
+    monkeypatch.setenv("HNUMO_EXPERIMENTS", "1")
     monkeypatch.setenv("HNUMO_PERSIST_LDS_PAD", str(PAD))
     monkeypatch.setenv("HNUMO_PERSIST_GUARD", guard)
     try:
@@ -39,6 +40,7 @@ def make_engine(case, monkeypatch, guard):
     finally:
         monkeypatch.delenv("HNUMO_PERSIST_LDS_PAD")
         monkeypatch.delenv("HNUMO_PERSIST_GUARD")
+        monkeypatch.delenv("HNUMO_EXPERIMENTS")
 
 
 def test_default_engine_is_persistent_and_resident(case_factory):
@@ -173,3 +175,33 @@ def test_predict_on_resident_engine_reuploads(case_factory):
         assert np.array_equal(x, y)
     e.close()
     e1.close()
+
+
+def test_step_breakdown_abort_advances_exactly_nsteps(case_factory, monkeypatch):
+    """hnumo_step_breakdown whose second step's corrector launch gives up (launch 3 from now):
+    the first step stands, only the second is redone on per-stage launches, so the state advances
+    by exactly the 2 steps asked -- the same bits as 3 steps of an engine on per-stage launches
+    (1 ti_rk_bcl + the breakdown's 2), and the retry does not spend the back-off wait."""
+    from hnumo.engine import Engine
+    _, case = golden_case("dg25L3_step1", case_factory)
+    e = Engine(case)
+    assert e.stage_path == "persistent"
+    e.set_resident(True)
+    a = e.state()
+    e.ti_rk_bcl(*a)
+    e.debug_force_abort(3)
+    bd = e.step_breakdown(2)
+    assert bd and all(v >= 0 for v in bd.values()), bd
+    st = e.persistent_stats
+    assert st["aborts"] == 1 and st["reprobes"] == 0 and st["wait"] == 1, st
+    e.sync(*a)
+    monkeypatch.setenv("HNUMO_PERSISTENT", "0")
+    e0 = Engine(case)
+    monkeypatch.delenv("HNUMO_PERSISTENT")
+    b = e0.state()
+    for _ in range(3):
+        e0.ti_rk_bcl(*b)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    e.close()
+    e0.close()

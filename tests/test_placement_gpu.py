@@ -12,11 +12,13 @@ pytestmark = pytest.mark.gpu
 
 def _run(case, monkeypatch, env):
     from hnumo.engine import Engine
+    env = dict(env, HNUMO_EXPERIMENTS="1") if env else env   # experiment knobs need the gate
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     e = Engine(case)
     for k in env:
         monkeypatch.delenv(k)
+    assert len(e.overrides) == max(0, len(env) - 1) and not any("ignored" in x for x in e.overrides)
     st = e.state()
     for _ in range(2):
         e.ti_rk_bcl(*st)
@@ -54,3 +56,24 @@ def test_first_stage_store_and_large_mesh_kernels_keep_the_bits(cfg, kw, case_fa
     old = _run(case, monkeypatch, {"HNUMO_ACC_ZERO": "1", "HNUMO_BCL_BIG": "0"})
     assert new[2] == old[2]
     _same(new, old)
+
+
+def test_stray_experiment_knob_is_ignored_and_reported(case_factory, monkeypatch):
+    """An experiment knob without HNUMO_EXPERIMENTS=1 changes nothing (a stray variable on a
+    benchmark box) and is reported by hnumo_overrides; HNUMO_SUMMATION takes only its two words."""
+    from hnumo.engine import Engine, EngineError
+    case = case_factory("dg25L3")
+    monkeypatch.setenv("HNUMO_PERSIST_LDS_PAD", "30000")   # honoured, this would drop persistence
+    e = Engine(case)
+    assert e.stage_path == "persistent"
+    assert e.overrides == ["HNUMO_PERSIST_LDS_PAD=30000 (ignored: HNUMO_EXPERIMENTS!=1)"]
+    e.close()
+    monkeypatch.delenv("HNUMO_PERSIST_LDS_PAD")
+    monkeypatch.setenv("HNUMO_SUMMATION", "fast")
+    with pytest.raises(EngineError) as ex:
+        Engine(case)
+    assert ex.value.code == 4
+    monkeypatch.setenv("HNUMO_SUMMATION", "reference")
+    e = Engine(case)
+    assert e.overrides == ["HNUMO_SUMMATION=reference"] and e.summation == "reference"
+    e.close()

@@ -13,6 +13,7 @@ cfg, _, mode = sys.argv[1].partition(":")
 if mode == "stage":
     os.environ["HNUMO_PERSISTENT"] = "0"
 from hnumo.engine import Engine  # noqa: E402
+os.environ["HNUMO_EXPERIMENTS"] = "1"   # the engine honours HNUMO_* experiment knobs only with this
 
 knob, values = sys.argv[2], sys.argv[3:]
 case = build_case(make_config(cfg), dense=False)

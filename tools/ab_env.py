@@ -14,6 +14,7 @@ from hnumo.roofline import stage_bytes  # noqa: E402
 cfg, _, mode = sys.argv[1].partition(":")
 os.environ["HNUMO_PERSISTENT"] = "0" if mode == "stage" else "1"
 from hnumo.engine import Engine  # noqa: E402
+os.environ["HNUMO_EXPERIMENTS"] = "1"   # the engine honours HNUMO_* experiment knobs only with this
 
 case = build_case(make_config(cfg), dense=False)
 reps = int(os.environ.get("AB_REPS", "1"))

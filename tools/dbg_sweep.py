@@ -7,6 +7,7 @@ import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "h-numo_amd"))
 from hnumo.case import build_case, make_config  # noqa: E402
+os.environ["HNUMO_EXPERIMENTS"] = "1"   # the engine honours HNUMO_* experiment knobs only with this
 
 cfg = sys.argv[1]
 case = build_case(make_config(cfg), dense=False)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Roofline evidence for the three single-GPU BASELINE configs (dg25L3 = configs[1], dg25N7L3 = C3,
 # dg316L3 = C4): per config one rocprofv3 --kernel-trace --stats run of bench.py, the FETCH_SIZE and
-# WRITE_SIZE passes, and (C3, C4) two SQ instruction-mix passes; each pass its own run.
+# WRITE_SIZE passes, and two SQ instruction-mix passes; each pass its own run.
 # Usage (via gpurun): bash tools/gpu_profiles.sh <tag> [configs...]
 # Then, here: python tools/profile_summary.py <tag>
 set -o pipefail
@@ -26,7 +26,7 @@ for cfg in $CFGS; do
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $c -d $O/pmc_${c}_$cfg -o run --output-format csv -- $B --steps 2 --warmup 1 > $O/pmc_${c}_$cfg.log 2>&1 || { echo "pmc $c $cfg failed"; tail -20 $O/pmc_${c}_$cfg.log; exit 1; }
   done
-  if [ "$cfg" != "dg25L3" ]; then
+  if true; then
     i=1
     for set in "$SQ1" "$SQ2"; do
       timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $set -d $O/pmc_sq${i}_$cfg -o run --output-format csv -- $B --steps 2 --warmup 1 > $O/pmc_sq${i}_$cfg.log 2>&1 || { echo "pmc sq$i $cfg failed"; tail -20 $O/pmc_sq${i}_$cfg.log; exit 1; }

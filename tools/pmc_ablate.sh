@@ -19,7 +19,7 @@ for lib in $LIBS; do
   tag=$(basename $lib .so)
   for dbg in ${DBGS:-0 64 4 1 2 32 68}; do
     if [ "$lib" = default ]; then L=""; else L=$lib; fi
-    HNUMO_LIB=$L HNUMO_STAGE_DBG=$dbg timeout -s KILL 180 rocprofv3 --kernel-trace --pmc $SQ -d $OUT/${tag}_d$dbg -o run --output-format csv -- python3 tools/stage_only.py $CFG 1 > $OUT/${tag}_d$dbg.log 2>&1 || { echo "pass $tag dbg $dbg failed"; tail -5 $OUT/${tag}_d$dbg.log; exit 1; }
+    HNUMO_LIB=$L HNUMO_EXPERIMENTS=1 HNUMO_STAGE_DBG=$dbg timeout -s KILL 180 rocprofv3 --kernel-trace --pmc $SQ -d $OUT/${tag}_d$dbg -o run --output-format csv -- python3 tools/stage_only.py $CFG 1 > $OUT/${tag}_d$dbg.log 2>&1 || { echo "pass $tag dbg $dbg failed"; tail -5 $OUT/${tag}_d$dbg.log; exit 1; }
   done
 done
 python3 - "$OUT" "$CFG" <<'PY'

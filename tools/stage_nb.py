@@ -6,6 +6,7 @@ import time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "h-numo_amd"))
 from hnumo.case import build_case, make_config  # noqa: E402
 from hnumo.roofline import stage_bytes  # noqa: E402
+os.environ["HNUMO_EXPERIMENTS"] = "1"   # the engine honours HNUMO_* experiment knobs only with this
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "dg316L3"
 nbs = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "4"]

@@ -7,6 +7,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 import numpy as np  # noqa: E402
 from hnumo.case import build_case, make_config  # noqa: E402
 from hnumo.engine import Engine  # noqa: E402
+os.environ["HNUMO_EXPERIMENTS"] = "1"   # the engine honours HNUMO_* experiment knobs only with this
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "dg25L3"
 case = build_case(make_config(cfg), dense=False)
