@@ -92,15 +92,16 @@ contains
             h_proc(1:num_nbh) = nbh_proc(1:num_nbh)                ! 1-based ranks, as p4est fills them
             h_num(1:num_nbh) = num_send_recv(1:num_nbh)
             h_list(1:sum(num_send_recv(1:num_nbh))) = nbh_send_recv(1:sum(num_send_recv(1:num_nbh)))
+            halo%rank = irank; halo%nranks = numproc; halo%num_nbh = num_nbh
+            halo%nbh_proc = c_loc(h_proc); halo%num_send_recv = c_loc(h_num); halo%nbh_send_recv = c_loc(h_list)
+            halo%nelem_owned = nelem
+            call dump_halo(halo)
             if (irank == 0) then
                 rc = hnumo_rccl_unique_id(comm_id)
                 if (rc /= HNUMO_OK) stop 'hnumo_bridge: hnumo_rccl_unique_id failed'
             end if
             call mpi_bcast(comm_id, 128, MPI_CHARACTER, 0, MPI_COMM_WORLD, ierr)
-            halo%rank = irank; halo%nranks = numproc; halo%num_nbh = num_nbh
-            halo%nbh_proc = c_loc(h_proc); halo%num_send_recv = c_loc(h_num); halo%nbh_send_recv = c_loc(h_list)
             halo%comm_id = c_loc(comm_id)
-            halo%nelem_owned = nelem
             halo_p = c_loc(halo)
         end if
         face8 = face(1:8, 1:nface)
@@ -152,6 +153,34 @@ contains
             if (resident) rc = hnumo_set_resident(engine, 1_c_int)
         end if
     end subroutine hnumo_bridge_init
+
+    ! Verification hook (tests/test_fortran_abi.py): with HNUMO_BRIDGE_HALO_DUMP=<path> in the
+    ! environment, write the processor-face descriptor exactly as hnumo_engine_create will read it
+    ! -- through the descriptor's own pointers -- to <path>.<rank> before the first device call:
+    ! int32 rank, nranks, num_nbh, nelem_owned, sum(num_send_recv), then nbh_proc(num_nbh),
+    ! num_send_recv(num_nbh), nbh_send_recv(sum).  Nothing is written without the variable.
+    subroutine dump_halo(h)
+        use iso_c_binding, only: c_f_pointer
+        type(hnumo_halo_desc), intent(in) :: h
+        character(len=1024) :: path
+        character(len=16) :: rs
+        integer :: n, stat, u
+        integer(c_int32_t), pointer :: proc(:), num(:), lst(:)
+        call get_environment_variable('HNUMO_BRIDGE_HALO_DUMP', path, status=stat)
+        if (stat /= 0 .or. len_trim(path) == 0) return
+        n = 0
+        if (h%num_nbh > 0) then
+            call c_f_pointer(h%nbh_proc, proc, [h%num_nbh])
+            call c_f_pointer(h%num_send_recv, num, [h%num_nbh])
+            n = sum(num)
+            call c_f_pointer(h%nbh_send_recv, lst, [max(n, 1)])
+        end if
+        write(rs, '(I0)') h%rank
+        open(newunit=u, file=trim(path) // '.' // trim(rs), access='stream', form='unformatted', status='replace')
+        write(u) h%rank, h%nranks, h%num_nbh, h%nelem_owned, int(n, c_int32_t)
+        if (h%num_nbh > 0) write(u) proc, num, lst(1:n)
+        close(u)
+    end subroutine dump_halo
 
     ! drop-in for ti_rk_bcl (ti_rk_bcl.F90:9-19): same arguments, same layouts
     subroutine hnumo_bridge_ti_rk_bcl(q_df, qb_df, qprime_df)

@@ -88,3 +88,68 @@ def test_bridge_multirank_branch_compiles_links_and_runs_to_the_device():
         r = subprocess.run([O.MPIEXEC, "-launcher", "fork", "-n", "2", O.DROPIN_DRIVER, fin, fout], cwd=d,
                            capture_output=True, text=True, timeout=300)
     assert "hnumo_bridge: hnumo_rccl_unique_id failed" in r.stdout + r.stderr, (r.stdout[-1000:], r.stderr[-1000:])
+
+
+def _bridge_halo_dump(parts, d):
+    """Run oracle/_ref/dropin_driver under mpiexec on `parts` with HNUMO_BRIDGE_HALO_DUMP set: each
+    rank's bridge writes the hnumo_halo_desc it built from mod_parallel, then (no GPU here) stops at
+    its first device call.  Returns the per-rank dumps."""
+    import numpy as np
+    import oracle as O
+    from hnumo import bundle as B
+    fin, fout, dump = os.path.join(d, "bundle.bin"), os.path.join(d, "out.bin"), os.path.join(d, "halo")
+    for r, pc in enumerate(parts):
+        B.write_bundle(f"{fin}.{r}", pc, "step", 1, metrics=True)
+    env = dict(os.environ, HNUMO_BRIDGE_HALO_DUMP=dump)
+    subprocess.run([O.MPIEXEC, "-launcher", "fork", "-n", str(len(parts)), O.DROPIN_DRIVER, fin, fout], cwd=d,
+                   capture_output=True, text=True, timeout=300, env=env)
+    out = []
+    for r in range(len(parts)):
+        a = np.fromfile(f"{dump}.{r}", dtype="<i4")
+        rank, nranks, nn, nown, n = (int(x) for x in a[:5])
+        rest = a[5:]
+        assert rest.size == 2 * nn + n
+        out.append({"rank": rank, "nranks": nranks, "num_nbh": nn, "nelem_owned": nown,
+                    "nbh_proc": rest[:nn], "num_send_recv": rest[nn:2 * nn], "nbh_send_recv": rest[2 * nn:]})
+    return out
+
+
+@pytest.mark.ref
+@pytest.mark.parametrize("cfg,kw,nranks,order", [("lake10", {}, 4, "morton"),
+                                                  ("dg25L3", {"nelx": 8, "nely": 8}, 8, "block")])
+def test_bridge_multirank_descriptor_equals_engine_lists(cfg, kw, nranks, order):
+    """The Fortran bridge's multi-rank branch (hnumo_bridge.F90) builds hnumo_halo_desc from
+    mod_parallel (num_nbh, nbh_proc 1-based, num_send_recv, nbh_send_recv; mod_parallel.F90:106-171
+    as p4est.c:1343-1412 fills them).  Run under mpiexec on a Morton lake (4 ranks) and a 4x2-block
+    double gyre (8 ranks), every rank's descriptor, read back through its own pointers, equals
+    hnumo.facepart.halo_lists and the Python host's HaloDesc -- the lists the engine is tested with
+    (tests/test_facehalo_gpu.py) -- field by field, including the 1-based nbh_proc."""
+    import numpy as np
+    import oracle as O
+    from hnumo.abi import Halo
+    from hnumo.case import build_case, make_config
+    from hnumo.facepart import face_partition, halo_lists
+    if not os.path.exists(O.DROPIN_DRIVER):
+        pytest.skip("dropin_driver not built")
+    case = build_case(make_config(cfg, **kw))
+    parts = [face_partition(case, nranks, r, order) for r in range(nranks)]
+    with tempfile.TemporaryDirectory() as d:
+        dumps = _bridge_halo_dump(parts, d)
+    for r, (pc, got) in enumerate(zip(parts, dumps)):
+        proc, num, lst, _ = halo_lists(pc)
+        assert (got["rank"], got["nranks"], got["nelem_owned"]) == (r, nranks, pc.scalars["nelem"])
+        assert got["num_nbh"] == proc.size and got["num_nbh"] > 0
+        assert np.array_equal(got["nbh_proc"], proc) and np.array_equal(got["num_send_recv"], num)
+        assert np.array_equal(got["nbh_send_recv"], lst)
+        assert set(got["nbh_proc"]) <= set(range(1, nranks + 1)) and r + 1 not in set(got["nbh_proc"])
+        h = Halo(pc)
+        assert (h.desc.rank, h.desc.nranks, h.desc.num_nbh, h.desc.nelem_owned) == \
+            (got["rank"], got["nranks"], got["num_nbh"], got["nelem_owned"])
+        for k in ("nbh_proc", "num_send_recv", "nbh_send_recv"):
+            assert np.array_equal(h.keep[k], got[k]), (r, k)
+    # every shared face is listed by both of its ranks, the same number of times
+    pairs = {}
+    for r, got in enumerate(dumps):
+        for p, n in zip(got["nbh_proc"], got["num_send_recv"]):
+            pairs[(r, int(p) - 1)] = int(n)
+    assert all(pairs[(b, a)] == n for (a, b), n in pairs.items())
