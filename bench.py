@@ -21,8 +21,11 @@ Workloads (BASELINE.json configs):
   --config lake200 at N>1 -- configs[4] (C5), the lake at rest on 200x200 elements, 2 layers, on
                    a Morton processor-face partition (the C5 reference fixture's).
   --emulate W:R -- the N>1 code path on ONE GPU (torch.distributed.run --nproc-per-node 1): rank R
-                   of the W-rank partition as its own neighbour (the self-neighbour contract:
-                   its processor faces listed under itself), with the real run's nccl process
+                   of the W-rank partition as its own neighbour (the self-neighbour contract,
+                   hnumo/facepart.py self_neighbour: its per-neighbour processor-face lists kept,
+                   each addressed to itself -- one RCCL send/recv pair per real neighbour at the
+                   real offsets and sizes -- and the processor faces' side-2 statics mirrored
+                   from side 1 so the mirror is well balanced), with the real run's nccl process
                    group, id broadcast, RCCL engine, two-stream schedule, timed loop, halo check
                    and strong-scaling base -- the per-GPU cost of a W-GPU run and the setup time
                    of every phase, measured where no W-GPU node is available.
@@ -269,19 +272,6 @@ def _limiter(frac: float, dram_frac: float | None, E: int) -> str:
     return f"not HBM: DRAM traffic at {dram_frac:.1%} of peak while the algorithmic bytes run at {frac:.1%}; {why}"
 
 
-def _self_neighbour(pc):
-    """The self-neighbour contract (tests/test_rccl_self_gpu.py): every processor face of the rank
-    listed under the rank itself, as ONE list, in a one-rank communicator -- the same streams,
-    element split, launches, events and RCCL group calls per stage as the real rank, each message
-    going to itself instead of over xGMI."""
-    import numpy as np
-    from hnumo.facepart import FaceNeighbour
-    pc.nranks, pc.rank = 1, 0
-    faces = [n.faces for n in pc.fneighbours]
-    pc.fneighbours = [FaceNeighbour(0, np.concatenate(faces))] if faces else []
-    return pc
-
-
 def _claim_stdout():
     """The JSON line is the only thing on stdout: libraries that print to fd 1 (RCCL's version
     banner at communicator set-up, the HIP runtime) are sent to stderr; the line goes to a private
@@ -305,6 +295,13 @@ def main():
                     help="N>1 processor-face partition: block (default; C4's 4x2 blocks) or morton (default for lake200)")
     ap.add_argument("--emulate", default=None, metavar="W:R",
                     help="one GPU: rank R of a W-rank run as its own neighbour (see the module docstring)")
+    ap.add_argument("--emulate-lists", default="peers", choices=["peers", "one"],
+                    help="--emulate: keep the rank's per-neighbour processor-face lists (peers: one RCCL send/recv "
+                         "pair per real neighbour, the real run's message shape) or merge them into one list")
+    ap.add_argument("--emulate-halo", default=None, choices=["mirror", "frozen"],
+                    help="--emulate: what the rank's processor faces receive -- its own traces (mirror; default "
+                         "except lake configs) or the first message of each exchange site again (frozen: the "
+                         "at-rest neighbour of an at-rest lake; hnumo_debug_frozen_halo)")
     ap.add_argument("--cpu-steps", type=int, default=8)
     ap.add_argument("--cpu-cores", type=int, default=16,
                     help="MPI ranks (= host cores) of the reference CPU baseline (the GPU box's share is 16)")
@@ -351,6 +348,7 @@ def main():
     weak = multi and args.weak
     cfg_name = args.config or ("dg316L3" if multi and not weak else "dg25L3")
     order = args.order or ("morton" if cfg_name.startswith("lake") else "block")
+    emu_halo = args.emulate_halo or ("frozen" if cfg_name.startswith("lake") else "mirror")
     steps = args.steps if args.steps is not None else (20 if not multi or weak else 5)
     base_cfg = make_config(cfg_name)
     eng, parallelism, scaling = None, "single", "weak"
@@ -378,7 +376,8 @@ def main():
                 from hnumo.facepart import face_partition
                 case = face_partition(gcase, nparts, prank, order)
                 if emu:
-                    case = _self_neighbour(case)
+                    from hnumo.facepart import self_neighbour
+                    case = self_neighbour(case, per_peer=args.emulate_lists == "peers")
             else:
                 if emu:
                     raise ValueError("--emulate needs the processor-face halo")
@@ -386,6 +385,8 @@ def main():
             setup["partition_s"] = round(time.perf_counter() - t0, 2)
             t0 = time.perf_counter()
             eng = Engine(case, device=local_rank, comm_id=obj[0], summation=args.summation)
+            if emu and emu_halo == "frozen":
+                eng.debug_frozen_halo(True)
             setup["engine_create_s"] = round(time.perf_counter() - t0, 2)
             eng.set_resident(True)
             q, qb, qp = eng.state()
@@ -416,7 +417,8 @@ def main():
                 parallelism = (f"domain decomposition: {nparts} Morton (Z-order) pieces of the "
                                f"{gcfg['nelx']}x{gcfg['nely']} elements, {how}")
             if emu:
-                parallelism = f"EMULATED on one GPU: rank {prank} of [{parallelism}] as its own neighbour"
+                parallelism = (f"EMULATED on one GPU: rank {prank} of [{parallelism}] as its own neighbour "
+                               f"({args.emulate_lists} lists, {emu_halo} halo)")
             live_halo = True
     if eng is None:
         if case is None:
@@ -478,7 +480,7 @@ def main():
             # the self-neighbour partition's own local-exchange-group step is what the RCCL run must
             # equal; the real run's check (all W partitions as a local group) is built and stepped
             # too, to time it, but not compared (a real rank's neighbours are other ranks)
-            _, ref = HC.reference_faces_cases([case], 0, local_rank)
+            _, ref = HC.reference_faces_cases([case], 0, local_rank, frozen=emu_halo == "frozen")
             ref = HC.owned(case, ref)
             t1 = time.perf_counter()
             HC.reference_faces(gcase, nparts, prank, order, local_rank)
@@ -593,7 +595,8 @@ def main():
         out["emulated"] = True
         E_g = gcase.scalars["nelem"]
         out["emulation"] = {
-            "world": nparts, "rank": prank, "order": order,
+            "world": nparts, "rank": prank, "order": order, "lists": args.emulate_lists, "halo": emu_halo,
+            "messages_per_exchange": len(case.fneighbours),
             "rank_elements": S["nelem"], "processor_faces": int(sum(n.faces.size for n in case.fneighbours)),
             "projection_eu_per_s": round(E_g * 2 * S["N_btp"] * S["kstages"] * 1e3 / ms_per_step, 1),
             "note": f"this GPU ran rank {prank}'s block at {ms_per_step:.3f} ms per step with every exchange going to "

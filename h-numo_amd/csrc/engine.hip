@@ -140,6 +140,18 @@ struct hnumo_engine {
   int *d_elB = nullptr, *d_elI = nullptr;    // elements with / without a processor face
   int nB = 0, nI = 0;
   double *cdef = nullptr;                    // consistency deficits [L][side][2][F*NQ]
+  // hnumo_debug_frozen_halo (self-neighbour emulation only): each exchange site's first message,
+  // kept and sent again by every later exchange of the site (halo_src); site = the trace buffer
+  // for the stage traces, the position in the step's sequence of baroclinic exchanges for the rest
+  // (one array may carry different quantities at different points of the step)
+  bool emu_frozen = false;
+  int xseq = 0;                              // baroclinic exchanges so far in this step (their site)
+  struct Frozen {
+    const void *key;
+    size_t n;
+    double *buf;
+  };
+  std::vector<Frozen> frozen;
   hipStream_t stream2 = nullptr;             // boundary elements + trace transport (two-stream schedule)
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_I = nullptr, ev_B[2] = {nullptr, nullptr};
   hipEvent_t ev_Is = nullptr, ev_Bs[2] = {nullptr, nullptr};  // kernel stop events of the same hand-offs
@@ -564,7 +576,10 @@ static void exchange_dpp(hnumo_engine *e) { exchange(e, e->dpp, 1, e->L, (size_t
 // ------------------------------------------------------------------ processor-face exchanges
 // The peer engine of a local group holding rank r.
 static hnumo_engine *group_peer(hnumo_engine *e, int r) { return e->group->eng[r]; }
-static const hnumo_engine::FNbr *peer_entry(hnumo_engine *peer, int rank) {
+// the peer's entry for my list `mine`: the peer's one entry for my rank, or -- a self-neighbour
+// engine, whose lists may all name itself -- the same list
+static const hnumo_engine::FNbr *peer_entry(hnumo_engine *peer, int rank, const hnumo_engine::FNbr *mine) {
+  if (peer->rank == rank) return mine;
   for (auto &n : peer->fnb)
     if (n.rank == rank) return &n;
   return nullptr;
@@ -572,6 +587,37 @@ static const hnumo_engine::FNbr *peer_entry(hnumo_engine *peer, int rank) {
 
 // (a rank without shared faces still takes part in a local group's barriers)
 static bool face_tx_skip(const hnumo_engine *e) { return !e->face_halo || (e->NS == 0 && e->comm_mode != 1); }
+
+// The source of a halo message of `n` doubles at `live` (exchange site `key`, stream st): live, or
+// with hnumo_debug_frozen_halo the copy of the site's first message.  The frozen halo is an
+// emulation device (bench.py --emulate of an at-rest case): a self-neighbour rank
+// otherwise receives its own processor faces' traces, a zero-jump (extrapolation) boundary whose
+// faces lose the upwind dissipation -- stable for the double gyre at CFL ~0.03, not for the lake
+// at CFL ~1, which runs away within two steps.  Frozen, each processor face keeps receiving the
+// first message, at the initial condition the same values the real neighbour sends (a continuous
+// state's traces are equal from both sides: the first RHS is bit-identical to the whole mesh's,
+// tools/mirror_rhs.py) -- an at-rest neighbour for a lake at rest.  Same messages, sizes, sources
+// in HBM and transport calls; only their content stops following the rank's own state.
+static const double *halo_src(hnumo_engine *e, const void *key, const double *live, size_t n, hipStream_t st) {
+  if (!e->emu_frozen || n == 0) return live;
+  for (const auto &f : e->frozen)
+    if (f.key == key && f.n == n) return f.buf;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (e->capturing || (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)) {
+    e->comm_err = "frozen halo: an exchange site's first message inside a graph capture (use direct launches)";
+    return live;
+  }
+  // (not dalloc: its zero fill is a null-stream memset, unordered with this non-blocking stream's copy)
+  double *d = nullptr;
+  if (hipMalloc(&d, n * sizeof(double)) != hipSuccess) d = nullptr;
+  if (d) e->allocs.push_back(d);
+  if (!d || hipMemcpyAsync(d, live, n * sizeof(double), hipMemcpyDeviceToDevice, st) != hipSuccess) {
+    e->comm_err = "frozen halo: snapshot of a message failed";
+    return live;
+  }
+  e->frozen.push_back({key, n, d});
+  return d;
+}
 
 // before packing bx_sbuf: in a local group my previous message must have been read by every peer
 static void face_tx_begin(hnumo_engine *e) {
@@ -582,10 +628,11 @@ static void face_tx_begin(hnumo_engine *e) {
 // the packed messages bx_sbuf (`per` doubles per shared face, slots in nbh_send_recv order) into
 // the neighbours' bx_rbuf slots of the same faces, on the engine stream
 static void face_tx(hnumo_engine *e, size_t per) {
+  const double *src = halo_src(e, (const void *)(uintptr_t)(1 + e->xseq++), e->bx_sbuf, per * e->NS, e->stream);
   if (e->comm_mode == 2) {
     nccl_check(e, ncclGroupStart(), "ncclGroupStart");
     for (auto &n : e->fnb) {
-      nccl_check(e, ncclSend(e->bx_sbuf + per * n.off, per * n.n, ncclDouble, n.rank, e->comm, e->stream), "ncclSend");
+      nccl_check(e, ncclSend(src + per * n.off, per * n.n, ncclDouble, n.rank, e->comm, e->stream), "ncclSend");
       nccl_check(e, ncclRecv(e->bx_rbuf + per * n.off, per * n.n, ncclDouble, n.rank, e->comm, e->stream), "ncclRecv");
     }
     nccl_check(e, ncclGroupEnd(), "ncclGroupEnd");
@@ -594,13 +641,13 @@ static void face_tx(hnumo_engine *e, size_t per) {
     if (!e->group->barrier()) return;
     for (auto &n : e->fnb) {
       hnumo_engine *peer = group_peer(e, n.rank);
-      const hnumo_engine::FNbr *pn = peer_entry(peer, e->rank);
+      const hnumo_engine::FNbr *pn = peer_entry(peer, e->rank, &n);
       if (!pn || pn->n != n.n) {
         e->comm_err = "local group: neighbour lists of two ranks disagree";
         continue;
       }
       (void)hipStreamWaitEvent(e->stream, peer->ev_bpacked, 0);
-      if (hipMemcpyAsync(e->bx_rbuf + per * n.off, peer->bx_sbuf + per * pn->off, per * n.n * sizeof(double),
+      if (hipMemcpyAsync(e->bx_rbuf + per * n.off, (peer == e ? src : peer->bx_sbuf) + per * pn->off, per * n.n * sizeof(double),
                          hipMemcpyDeviceToDevice, e->stream) != hipSuccess)
         e->comm_err = "local group: hipMemcpyAsync of a face message failed";
     }
@@ -667,10 +714,11 @@ static void face_exchange_cdef(hnumo_engine *e) {
 static void trace_exchange(hnumo_engine *e, double *tb, hipStream_t st) {
   if (!e->face_halo || (e->NS == 0 && e->comm_mode != 1)) return;
   const size_t slot = 8 * (size_t)e->ngl, s0 = 4 * (size_t)e->nelem, r0 = s0 + e->NS;
+  const double *src = halo_src(e, tb, tb + s0 * slot, slot * e->NS, st);  // = the send slots
   if (e->comm_mode == 2) {
     nccl_check(e, ncclGroupStart(), "ncclGroupStart");
     for (auto &n : e->fnb) {
-      nccl_check(e, ncclSend(tb + (s0 + n.off) * slot, slot * n.n, ncclDouble, n.rank, e->comm, st), "ncclSend");
+      nccl_check(e, ncclSend(src + n.off * slot, slot * n.n, ncclDouble, n.rank, e->comm, st), "ncclSend");
       nccl_check(e, ncclRecv(tb + (r0 + n.off) * slot, slot * n.n, ncclDouble, n.rank, e->comm, st), "ncclRecv");
     }
     nccl_check(e, ncclGroupEnd(), "ncclGroupEnd");
@@ -683,13 +731,13 @@ static void trace_exchange(hnumo_engine *e, double *tb, hipStream_t st) {
   if (!e->group->barrier()) return;
   for (auto &n : e->fnb) {
     hnumo_engine *peer = group_peer(e, n.rank);
-    const hnumo_engine::FNbr *pn = peer_entry(peer, e->rank);
+    const hnumo_engine::FNbr *pn = peer_entry(peer, e->rank, &n);
     if (!pn || pn->n != n.n) {
       e->comm_err = "local group: neighbour lists of two ranks disagree";
       continue;
     }
     (void)hipStreamWaitEvent(st, peer->ev_tsent, 0);
-    if (hipMemcpyAsync(tb + (r0 + n.off) * slot, peer->gtrace[bi] + (4 * (size_t)peer->nelem + pn->off) * slot,
+    if (hipMemcpyAsync(tb + (r0 + n.off) * slot, (peer == e ? src + pn->off * slot : peer->gtrace[bi] + (4 * (size_t)peer->nelem + pn->off) * slot),
                        slot * n.n * sizeof(double), hipMemcpyDeviceToDevice, st) != hipSuccess)
       e->comm_err = "local group: hipMemcpyAsync of a trace message failed";
   }
@@ -901,6 +949,7 @@ static void launch_subcycle(hnumo_engine *e, double *dst, const double *qp, bool
 // the prediction half of ti_rk_bcl (ti_rk_bcl.F90:43-57) on device state (e->q, e->qb, e->qp):
 // results in e->q2 (q_df2), e->qbp (qb after the sub-cycle), e->qp2 (qprime_df2)
 static void launch_predict(hnumo_engine *e) {
+  e->xseq = 0;  // (every step starts here: its baroclinic exchanges' sites, see halo_src)
   launch_bcl_coeffs(e, e->qp, e->qf);
   launch_subcycle(e, e->qbp, e->qp);
   // (q_df2 = q_df, qprime_df2 = qprime_df, qprime_face2 = qprime_face (ti_rk_bcl.F90:53-55) without
@@ -1043,9 +1092,14 @@ int hnumo_engine_create(const hnumo_mesh_desc *mesh, const hnumo_static_desc *st
         if (nb.rank < 0 || nb.rank >= halo->nranks || (nb.rank == halo->rank && halo->nranks > 1))
           return fail(eng, HNUMO_ERR_INVALID, "nbh_proc: bad neighbour rank (1-based ranks expected)");
         // mod_parallel lists each neighbour process once (p4est.c:1343-1360); the transports pair a
-        // rank's message with the peer's one entry for it
-        for (const auto &pn : eng->fnb)
-          if (pn.rank == nb.rank) return fail(eng, HNUMO_ERR_INVALID, "nbh_proc: a neighbour rank is listed twice");
+        // rank's message with the peer's one entry for it.  The one exception is the self-neighbour
+        // contract (nranks == 1): a W-rank partition's rank emulated on one GPU may keep its real
+        // per-neighbour lists, every one addressed to itself -- one ncclSend/ncclRecv pair per list
+        // inside the group (RCCL matches same-peer operations in issue order), each list's message
+        // at its own offset and size, as on the W-GPU run
+        if (halo->nranks > 1)
+          for (const auto &pn : eng->fnb)
+            if (pn.rank == nb.rank) return fail(eng, HNUMO_ERR_INVALID, "nbh_proc: a neighbour rank is listed twice");
         if (nb.n < 0) return fail(eng, HNUMO_ERR_INVALID, "num_send_recv < 0");
         for (int i = 0; i < nb.n; i++) {
           const int f = halo->nbh_send_recv[o + i] - 1;
@@ -1856,6 +1910,16 @@ int hnumo_persistent_stats(hnumo_engine *eng, int32_t *out4) {
                         eng->persist_suspended ? eng->persist_wait : -1};
   std::memcpy(out4, v, sizeof(v));
   return 0;
+}
+
+int hnumo_debug_frozen_halo(hnumo_engine *eng, int on) {
+  if (!eng) return HNUMO_ERR_INVALID;
+  if (!eng->face_halo || eng->nranks != 1) {
+    eng->err = "the frozen halo is for self-neighbour engines (one-rank processor-face halo) only";
+    return HNUMO_ERR_INVALID;
+  }
+  eng->emu_frozen = on != 0;
+  return HNUMO_OK;
 }
 
 int hnumo_debug_force_abort(hnumo_engine *eng, int k) {

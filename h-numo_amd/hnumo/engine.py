@@ -62,6 +62,7 @@ def lib():
         L.hnumo_persistent_info.argtypes = [vp, C.POINTER(C.c_int32)]
         L.hnumo_persistent_stats.argtypes = [vp, C.POINTER(C.c_int32)]
         L.hnumo_debug_force_abort.argtypes = [vp, C.c_int]
+        L.hnumo_debug_frozen_halo.argtypes = [vp, C.c_int]
         L.hnumo_step_breakdown.argtypes = [vp, C.c_int, C.c_char_p, C.c_int64, dp, C.c_int, C.POINTER(C.c_int)]
         L.hnumo_stream_copy_bw.argtypes = [C.c_int, C.c_int64, C.c_int, dp]
         L.hnumo_overrides.argtypes = [vp, C.c_char_p, C.c_int64]
@@ -202,6 +203,12 @@ class Engine:
         """Test hook: the k-th persistent sub-cycle launch from now (0 = the next) gives up as a
         launch whose workgroups are not co-resident does (hnumo_debug_force_abort)."""
         self._check(lib().hnumo_debug_force_abort(self.h, int(k)))
+
+    def debug_frozen_halo(self, on: bool = True):
+        """Emulation hook (self-neighbour engines only, bench.py --emulate): every halo exchange
+        site sends its first message again and again -- an at-rest neighbour for an at-rest case
+        (hnumo_debug_frozen_halo).  Set before the first step."""
+        self._check(lib().hnumo_debug_frozen_halo(self.h, int(on)))
 
     def set_resident(self, on: bool):
         self._check(lib().hnumo_set_resident(self.h, int(on)))

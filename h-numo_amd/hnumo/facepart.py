@@ -202,6 +202,43 @@ def halo_lists(pc: FaceRankCase):
     return nbh_proc, num, lst, np.ones(lst.size, dtype=np.int32)
 
 
+def self_neighbour(pc: FaceRankCase, per_peer: bool = True, mirror_statics: bool = True) -> FaceRankCase:
+    """Rank `pc.rank` of a W-rank partition as its own neighbour, in a one-rank communicator (the
+    self-neighbour contract of hnumo_engine_create; bench.py --emulate): one GPU runs the rank's
+    launches, streams, events and RCCL group calls per stage with every message going to itself.
+
+    per_peer: keep the real per-neighbour lists, each addressed to rank 0 (itself) -- the real
+        run's message shape: one ncclSend/ncclRecv pair per neighbour, at its own offset and size
+        (send_receive_bound.F90:860-880); False: all processor faces as ONE list.
+    mirror_statics: a processor face receives its OWN side-1 traces as side 2, so its side-2
+        statics become side 1's too (pbprime_face, pbprime_df_face, zbot_face, and the edge
+        wave-speed coefficients of compute_reference_edge_variables, mod_initial_mlswe.F90:355-401,
+        with c_- = c_+) -- the mirror is then a well-balanced neighbour: a lake at rest stays at
+        rest (against the real neighbour's bathymetry statics it did not: profiles/r05c).  The
+        work per face is unchanged.  Modifies and returns pc."""
+    pc.nranks, pc.rank = 1, 0
+    nb = pc.fneighbours
+    if per_peer:
+        pc.fneighbours = [FaceNeighbour(0, n.faces) for n in nb]
+    else:
+        pc.fneighbours = [FaceNeighbour(0, np.concatenate([n.faces for n in nb]))] if nb else []
+    if mirror_statics and nb:
+        f = np.concatenate([n.faces for n in nb])
+        B = pc.arrays
+        for k in ("pbprime_face", "pbprime_df_face", "zbot_face"):
+            B[k][1][:, f] = B[k][0][:, f]
+        alpha = np.asarray(B["alpha"])
+        c = np.sqrt(alpha[pc.scalars["nlayers"] - 1] * B["pbprime_face"][0][:, f])
+        ok = c > 0.0
+        den = np.where(ok, c + c, 1.0)
+        z = np.zeros_like(c)
+        for k in ("coeff_pbpert_L", "coeff_pbpert_R", "coeff_mass_pbub_L", "coeff_mass_pbub_R"):
+            B[k][:, f] = np.where(ok, c / den, z)
+        B["coeff_pbub_LR"][:, f] = np.where(ok, 1.0 / den, z)
+        B["coeff_mass_pbpert_LR"][:, f] = np.where(ok, c * c / den, z)
+    return pc
+
+
 def gather_faces_state(parts, name, global_case):
     """Reassemble a nodal state array (ncomp, npoin[, L]) from every rank's elements."""
     A = np.asarray(global_case.arrays[name])

@@ -60,12 +60,15 @@ def reference_faces(gcase, nranks, rank, order, device):
     return reference_faces_cases(parts, rank, device)
 
 
-def reference_faces_cases(parts, rank, device):
+def reference_faces_cases(parts, rank, device, frozen=False):
     """reference_faces for given partition cases (ranks 0..n-1 of one partition; a single
-    self-neighbour case for bench.py --emulate)."""
+    self-neighbour case for bench.py --emulate, frozen: with its frozen halo)."""
     from .engine import Engine, group_ti_rk_bcl, local_group
     engines = [Engine(p, device=device) for p in parts]
     try:
+        if frozen:
+            for e in engines:
+                e.debug_frozen_halo(True)
         local_group(engines)
         states = [e.state() for e in engines]
         group_ti_rk_bcl(engines, states)

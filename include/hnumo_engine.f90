@@ -17,7 +17,7 @@ module hnumo_engine_c
         HNUMO_ERR_NONFINITE = 2, HNUMO_ERR_DEVICE = 3, HNUMO_ERR_INVALID = 4
     integer(c_int32_t), parameter, public :: HNUMO_SHEAR_CORRECTOR_REFERENCE = 0, &
         HNUMO_SHEAR_CORRECTOR_PREDICTED = 1
-    integer(c_int), parameter, public :: HNUMO_ABI_EXPECTED = 9   ! must equal hnumo_abi_version()
+    integer(c_int), parameter, public :: HNUMO_ABI_EXPECTED = 10   ! must equal hnumo_abi_version()
     integer(c_int), parameter, public :: HNUMO_SUM_REFERENCE = 0, HNUMO_SUM_FACTORED = 1
 
     ! = hnumo_mesh_desc (mod_grid, mod_face, mod_basis, mod_metrics; optional dense tables)

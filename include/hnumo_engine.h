@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define HNUMO_ABI_VERSION 9
+#define HNUMO_ABI_VERSION 10
 
 enum {
   HNUMO_OK = 0,
@@ -260,6 +260,14 @@ int hnumo_persistent_stats(hnumo_engine *eng, int32_t *out4);
 /* Test hook (ABI v7): the k-th persistent sub-cycle launch from now (0 = the next) gives
  * up exactly as a launch whose workgroups are not all resident does.                  */
 int hnumo_debug_force_abort(hnumo_engine *eng, int k);
+
+/* Emulation hook (ABI v10; self-neighbour engines only: a one-rank communicator whose
+ * processor faces are listed under the rank itself, bench.py --emulate): on = 1 freezes the
+ * halo -- every exchange site sends the message it sent first, again and again (same sizes,
+ * offsets and transport calls), so each processor face keeps the at-rest neighbour of an at-rest
+ * case instead of its own traces.  Set before the first step.  Returns 4 on any
+ * other engine.                                                                          */
+int hnumo_debug_frozen_halo(hnumo_engine *eng, int on);
 
 /* RCCL unique id (128 bytes) for hnumo_halo_desc.comm_id: generated by one rank and
  * broadcast by the host (MPI / torch.distributed) before hnumo_engine_create.        */

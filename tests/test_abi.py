@@ -30,7 +30,7 @@ def test_library_exports_all_symbols():
     for name in declared():
         assert hasattr(lib, name), name
     lib.hnumo_abi_version.restype = ctypes.c_int
-    assert lib.hnumo_abi_version() == 9
+    assert lib.hnumo_abi_version() == 10
 
 
 def test_descriptor_struct_matches_header():

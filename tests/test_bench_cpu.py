@@ -22,21 +22,53 @@ def test_lake200_is_the_c5_fixture_configuration():
 
 
 def test_self_neighbour_lists_every_processor_face_once_under_rank_0():
-    import bench
+    """facepart.self_neighbour (bench.py --emulate): per_peer keeps the real rank's per-neighbour
+    lists (C4/8 rank 1 of the 4x2 blocks: neighbours 0, 2, 5), each addressed to rank 0 itself, in
+    the same order and sizes; one-list mode merges them.  Every processor face is listed once."""
     from hnumo.case import build_case, make_config
-    from hnumo.facepart import face_partition
+    from hnumo.facepart import face_partition, halo_lists, self_neighbour
     g = build_case(make_config("dg8L3q"), dense=False)
-    pc = face_partition(g, 4, 1, "block")
+    pc = face_partition(g, 8, 1, "block")
+    assert [n.rank for n in pc.fneighbours] == [0, 2, 5]
+    sizes = [n.faces.size for n in pc.fneighbours]
     faces = np.concatenate([n.faces for n in pc.fneighbours])
-    sn = bench._self_neighbour(pc)
+    sn = self_neighbour(face_partition(g, 8, 1, "block"))
     assert sn.nranks == 1 and sn.rank == 0
-    assert len(sn.fneighbours) == 1 and sn.fneighbours[0].rank == 0
-    assert np.array_equal(sn.fneighbours[0].faces, faces)
+    assert [n.rank for n in sn.fneighbours] == [0, 0, 0] and [n.faces.size for n in sn.fneighbours] == sizes
+    nbh_proc, num, lst, _ = halo_lists(sn)
+    assert nbh_proc.tolist() == [1, 1, 1] and num.tolist() == sizes and np.array_equal(lst - 1, faces)
+    one = self_neighbour(face_partition(g, 8, 1, "block"), per_peer=False)
+    assert len(one.fneighbours) == 1 and np.array_equal(one.fneighbours[0].faces, faces)
     assert len(np.unique(faces)) == faces.size
+
+
+def test_self_neighbour_mirrors_the_processor_faces_statics():
+    """The mirror's side 2 is side 1 (the face receives its own traces): side-2 bathymetry statics
+    copied from side 1 and the edge coefficients of mod_initial_mlswe.F90:355-401 with c_- = c_+ --
+    on every processor face and nowhere else."""
+    from hnumo.case import build_case, make_config
+    from hnumo.facepart import face_partition, self_neighbour
+    g = build_case(make_config("lake10"), dense=False)
+    pc = face_partition(g, 4, 1, "morton")
+    ref = {k: np.array(v) for k, v in pc.arrays.items() if k.startswith(("pbprime", "zbot_face", "coeff_"))}
+    f = np.concatenate([n.faces for n in pc.fneighbours])
+    other = np.setdiff1d(np.arange(pc.scalars["nface"]), f)
+    sn = self_neighbour(pc)
+    A = sn.arrays
+    for k in ("pbprime_face", "pbprime_df_face", "zbot_face"):
+        assert np.array_equal(A[k][1][:, f], A[k][0][:, f])
+        assert np.array_equal(A[k][:, :, other], ref[k][:, :, other])
+    assert not np.array_equal(ref["pbprime_face"][1][:, f], ref["pbprime_face"][0][:, f])  # (the lake's bathymetry)
+    for a, b in (("coeff_pbpert_L", "coeff_pbpert_R"), ("coeff_mass_pbub_L", "coeff_mass_pbub_R")):
+        assert np.array_equal(A[a][:, f], A[b][:, f])
+    wet = A["pbprime_face"][0][:, f] > 0
+    assert np.all(A["coeff_pbpert_L"][:, f][wet] == 0.5)
+    for k in ("coeff_pbpert_L", "coeff_pbub_LR", "coeff_mass_pbpert_LR"):
+        assert np.array_equal(A[k][:, other], ref[k][:, other])
 
 
 def test_bench_cli_lists_the_emulation_and_baseline_switches():
     out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--help"], capture_output=True, text=True,
                          check=True).stdout
-    for flag in ("--emulate", "--order", "--no-base", "--no-c4-cpu"):
+    for flag in ("--emulate", "--emulate-lists", "--order", "--no-base", "--no-c4-cpu"):
         assert flag in out

@@ -37,7 +37,7 @@ def test_bench_n_gt_1_branch_runs_on_one_gpu():
     assert len(lines) == 1, lines  # the JSON line alone (library banners go to stderr)
     d = json.loads(lines[0])
     assert d["halo_bitwise"] is True and d["halo_check"]["max_rel_diff"] == 0.0
-    assert d["scaling"] == "strong" and d["value"] > 0 and d["ms_per_step"] > 0
+    assert d["scaling"] == "emulated" and d["emulated"] is True and d["value"] > 0 and d["ms_per_step"] > 0
     assert "EMULATED" in d["config"]["parallelism"]
     em = d["emulation"]
     assert em["world"] == 2 and em["rank"] == 1 and em["processor_faces"] > 0 and em["projection_eu_per_s"] > 0
