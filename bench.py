@@ -13,7 +13,8 @@ Workloads (BASELINE.json configs):
   N=1   dg25L3  -- configs[1], the double gyre at 25x25 elements, N=4, 3 layers (the metric's
                    1-GPU configuration); the line also carries "c4_single_gpu", the C4 mesh
                    below on this one GPU (the strong-scaling base of the N>1 lines), and
-                   "c3_single_gpu", configs[2] (dg25N7L3: N=7, 3 layers, 25x25 elements).
+                   "c3_single_gpu", configs[2] (dg25N7L3: N=7, 3 layers, 25x25 elements), and
+                   "c5_single_gpu", configs[4]'s mesh (lake200: the lake at rest, 2 layers) on this GPU.
   N>1   dg316L3 -- configs[3] (C4), the double gyre at 316x316 = 99,856 elements, N=4,
                    3 layers, dt=40 s, dt_btp=2 s, split over the N GPUs (strong scaling:
                    rank grid 2x1, 2x2, 4x2 of 158x316 / 158x158 / 79x158 element blocks).
@@ -210,28 +211,32 @@ def stream_copy(device: int = 0) -> dict | None:
                    f"back to back per variant, the fastest ({kind}); this GPU, this run"}
 
 
-def c4_cpu_baseline(gcase, cores: int) -> dict | None:
+def c4_cpu_baseline(gcase, cores: int, repeats: int = 3) -> dict | None:
     """The reference Fortran on the C4 workload itself: ONE baroclinic step of the 316x316 mesh under
     `mpiexec -n cores` on a Morton processor-face partition (its own MPI halo), each rank reading
-    the dense tables of its own elements (facepart.add_dense_tables)."""
+    the dense tables of its own elements (facepart.add_dense_tables); `repeats` runs, the median
+    reported with the spread (the host cores are shared)."""
     from hnumo.facepart import add_dense_tables, face_partition
     from hnumo.roofline import element_updates_per_step
     try:
         t0 = time.perf_counter()
         parts = [add_dense_tables(face_partition(gcase, cores, r, "morton")) for r in range(cores)]
-        t = _run_reference(parts, 1, cores)
+        runs = [t for t in (_run_reference(parts, 1, cores) for _ in range(repeats)) if t]
         wall = time.perf_counter() - t0
     except Exception as exc:  # pragma: no cover - diagnostic only
         print(f"[bench] C4 reference baseline failed: {exc}", file=sys.stderr)
         return None
-    if not t:
+    if not runs:
         return None
     eu = element_updates_per_step(gcase)
+    t = sorted(runs)[len(runs) // 2]
+    rates = sorted(eu / x for x in runs)
     return {"value": round(eu / t, 1), "unit": "element-updates/s", "cores": cores, "kind": "reference",
             "sample": f"dg316L3 (C4, {gcase.scalars['nelem']} elements), 1 baroclinic step of the reference Fortran "
                       f"(amdflang -O2) under mpiexec -n {cores} (Morton processor-face partition, its own MPI "
-                      f"halo), one rank per core: {t:.2f} s (MPI_Wtime, max over ranks; {wall:.0f} s with the "
-                      "per-rank dense tables and bundles)"}
+                      f"halo), one rank per core: {t:.2f} s (MPI_Wtime, max over ranks; median of {len(runs)} runs; "
+                      f"{wall:.0f} s in all with the per-rank dense tables and bundles)",
+            "spread": {"runs": len(runs), "min": round(rates[0], 1), "max": round(rates[-1], 1)}}
 
 
 def _profiled(cfg: str, kname: str, k_ms: float) -> dict:
@@ -307,7 +312,7 @@ def main():
                     help="MPI ranks (= host cores) of the reference CPU baseline (the GPU box's share is 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c4-cpu", action="store_true", help="N=1: skip the reference C4 step on the host cores")
-    ap.add_argument("--no-c4", action="store_true", help="N=1: skip the c4_single_gpu / c3_single_gpu figures")
+    ap.add_argument("--no-c4", action="store_true", help="N=1: skip the c4/c3/c5_single_gpu figures")
     ap.add_argument("--no-base", action="store_true", help="N>1: skip the strong-scaling base (whole mesh on rank 0's GPU)")
     ap.add_argument("--summation", default="reference", choices=["reference", "factored"],
                     help="stage summation order (hnumo_set_summation); only 'reference' meets the 1e-10 bar")
@@ -606,7 +611,9 @@ def main():
         out["setup_s"] = setup
     if rank == 0 and not multi and not args.no_c4 and args.config is None:
         for key, cfg, wl, n in [("c4_single_gpu", "dg316L3", "dg316L3 (C4: 316x316 elements, N=4, 3 layers)", 3),
-                                ("c3_single_gpu", "dg25N7L3", "dg25N7L3 (C3: 25x25 elements, N=7, 3 layers)", 5)]:
+                                ("c3_single_gpu", "dg25N7L3", "dg25N7L3 (C3: 25x25 elements, N=7, 3 layers)", 5),
+                                ("c5_single_gpu", "lake200", "lake200 (C5: the lake at rest, 200x200 elements, "
+                                                             "N=4, 2 layers, wetting/drying BC path)", 3)]:
             try:
                 c = build_case(make_config(cfg), dense=False)
                 out[key] = single_gpu_line(cfg, wl, n, case=c)
