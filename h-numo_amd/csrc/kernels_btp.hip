@@ -241,7 +241,7 @@ struct StageCfg {
   // (the regions LDS-DMA writes start on 16 bytes: ev; not the slim arena, which keeps the dword
   // copies -- see G16)
   static constexpr int ev(int x) { return SLIM ? x : (x + 1) & ~1; }
-  // QPM (SLIM): the quad-point values quad-point-major, s_qv [Q][8] = (w, the 7 integrand factors) --
+  // QPM (SLIM): the quad-point values by quad point, s_qv [4][Q][2] = pairs of (w, the 7 integrand factors) --
   // A2's interpolations in slots 0..3 and the bottom layer's in 4..6 until B overwrites them -- so the
   // on-the-fly sums read a quad point's 8 values as four ds_read_b128 from one address; w moves out of
   // s_qk, which keeps the metric pairs alone (16-byte aligned)
@@ -460,10 +460,16 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   // (dp, dpp, udp, vdp), the bottom layer's c = 0..2, B's outputs k = 0..6, the weight w, and the
   // metric pairs (QE_EX, QE_NX, QE_EY, QE_NY)
   constexpr bool QPM = C::QPM;
-  auto QI = [&](int c, int q) -> double & { return QPM ? s_qv[q * 8 + c] : s_qv[c * Q + q]; };
-  auto QP = [&](int c, int q) -> double & { return QPM ? s_qv[q * 8 + 4 + c] : s_pq[c * Q + q]; };
-  auto QO = [&](int k, int q) -> double & { return QPM ? s_qv[q * 8 + 1 + k] : s_qv[k * Q + q]; };
-  auto QW = [&](int q) -> double { return QPM ? s_qv[q * 8] : s_qk[qe_pos(QE_W, q, Q)]; };
+  // (QPM: slot sl of quad point q in pair-major order [4][Q][2] -- pair sl/2 of every quad point in one
+  // row: a writer lane q stores a 16-byte pair 16 B past its neighbour's, conflict-free, where the
+  // record-per-quad-point order [Q][8] put the 16 lanes of a ds_write_b64 group 64 B apart on two bank
+  // pairs, 8-way (C3: ~1,100 conflict cycles an element-stage); the on-the-fly sums still read the
+  // four pairs of a quad point with one address and four immediate offsets)
+  auto QSL = [&](int sl, int q) -> double & { return s_qv[((sl >> 1) * Q + q) * 2 + (sl & 1)]; };
+  auto QI = [&](int c, int q) -> double & { return QPM ? QSL(c, q) : s_qv[c * Q + q]; };
+  auto QP = [&](int c, int q) -> double & { return QPM ? QSL(4 + c, q) : s_pq[c * Q + q]; };
+  auto QO = [&](int k, int q) -> double & { return QPM ? QSL(1 + k, q) : s_qv[k * Q + q]; };
+  auto QW = [&](int q) -> double { return QPM ? QSL(0, q) : s_qk[qe_pos(QE_W, q, Q)]; };
   auto QK = [&](int c, int q) -> double { return s_qk[qe_pos(c, q, Q) - (QPM ? Q : 0)]; };
   double *s_y = S + C::O_Y;        // SF: [NYV][NGL][NQ] interpolation partials
   double *s_grad = S + C::O_GR, *s_qq = S + C::O_QQ;  // [4][P]
@@ -1099,7 +1105,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         s_qv[6 * Q + q] = wq * (nx * A + ny * quv);
         s_qv[7 * Q + q] = wq * (nx * quv + ny * B);
       } else {
-        if (QPM) s_qv[q * 8] = r_wq;
+        if (QPM) QSL(0, q) = r_wq;
         QO(0, q) = udp;
         QO(1, q) = vdp;
         QO(2, q) = sc_x;
