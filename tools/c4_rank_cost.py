@@ -5,9 +5,9 @@ One rank of the 8-GPU run holds a 79x158 block (12,482 elements) of the 316x316 
 runs its boundary elements on a second stream, ships their traces over RCCL and runs its
 interior elements beside it (csrc/engine.hip launch_subcycle).  RCCL refuses two ranks on one
 device, so the rank is run here as a self-neighbour engine (tests/test_rccl_self_gpu.py): a
-one-rank communicator whose processor faces are listed under itself -- the same streams, events,
-element split, launches and RCCL group calls per stage as the real rank, with each message going
-to itself instead of over xGMI.  Compared with:
+one-rank communicator whose per-neighbour processor-face lists are addressed to itself -- the same
+streams, events, element split, launches and RCCL group calls (one send/recv pair per neighbour)
+per stage as the real rank, with each message going to itself instead of over xGMI.  Compared with:
   block     the same 79x158 elements as a single-rank engine (walls instead of processor faces,
             one stream, graph-captured step): the per-GPU work without any halo machinery;
   local     the self-neighbour partition through the local exchange group (device copies);
@@ -63,6 +63,7 @@ def main():
     ap.add_argument("--rank", type=int, default=1, help="rank of the 4x2 partition (1: three neighbours)")
     ap.add_argument("--variants", default="block,local,rccl,rccl_g")
     ap.add_argument("--no-projection", action="store_true")
+    ap.add_argument("--one-list", action="store_true")
     args = ap.parse_args()
     from hnumo.case import build_case, make_config
     from hnumo.engine import Engine, local_group
@@ -70,12 +71,10 @@ def main():
     g = build_case(make_config("dg316L3"), dense=False)
     pc = face_partition(g, 8, args.rank, "block")
     nbrs = [(n.rank, int(n.faces.size)) for n in pc.fneighbours]
-    # the self-neighbour contract: every processor face listed under the rank itself, as ONE list
-    # (mod_parallel lists each neighbour once; the engine rejects a rank listed twice)
-    import numpy as np
-    from hnumo.facepart import FaceNeighbour
-    pc.nranks, pc.rank = 1, 0
-    pc.fneighbours = [FaceNeighbour(0, np.concatenate([n.faces for n in pc.fneighbours]))]
+    # the self-neighbour contract: the rank's per-neighbour processor-face lists, each addressed to
+    # the rank itself (facepart.self_neighbour; --one-list: all faces as one list, rounds 3-5)
+    from hnumo.facepart import self_neighbour
+    pc = self_neighbour(pc, per_peer=not args.one_list)
     E = pc.scalars["nelem"]
     S = g.scalars
     stages = 2 * S["N_btp"] * S["kstages"]
