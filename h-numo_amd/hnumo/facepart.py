@@ -213,9 +213,10 @@ def self_neighbour(pc: FaceRankCase, per_peer: bool = True, mirror_statics: bool
     mirror_statics: a processor face receives its OWN side-1 traces as side 2, so its side-2
         statics become side 1's too (pbprime_face, pbprime_df_face, zbot_face, and the edge
         wave-speed coefficients of compute_reference_edge_variables, mod_initial_mlswe.F90:355-401,
-        with c_- = c_+) -- the mirror is then a well-balanced neighbour: a lake at rest stays at
-        rest (against the real neighbour's bathymetry statics it did not: profiles/r05c).  The
-        work per face is unchanged.  Modifies and returns pc."""
+        with c_- = c_+): the mirror is one consistent neighbour.  For the shipped configurations this
+        changes no bit (their bathymetry is continuous, both sides already agree); what keeps an
+        emulated lake at rest is the frozen halo (Engine.debug_frozen_halo).  The work
+        per face is unchanged.  Modifies and returns pc."""
     pc.nranks, pc.rank = 1, 0
     nb = pc.fneighbours
     if per_peer:

@@ -50,15 +50,19 @@ def test_self_neighbour_mirrors_the_processor_faces_statics():
     from hnumo.facepart import face_partition, self_neighbour
     g = build_case(make_config("lake10"), dense=False)
     pc = face_partition(g, 4, 1, "morton")
-    ref = {k: np.array(v) for k, v in pc.arrays.items() if k.startswith(("pbprime", "zbot_face", "coeff_"))}
     f = np.concatenate([n.faces for n in pc.fneighbours])
+    # (the lake's bathymetry is continuous, so its two sides agree already: make side 2 differ, as a
+    # discontinuous bathymetry would)
+    for k in ("pbprime_face", "pbprime_df_face", "zbot_face"):
+        pc.arrays[k][1][:, f] = 1.01 * pc.arrays[k][1][:, f] + 1.0
+    ref = {k: np.array(v) for k, v in pc.arrays.items() if k.startswith(("pbprime", "zbot_face", "coeff_"))}
     other = np.setdiff1d(np.arange(pc.scalars["nface"]), f)
     sn = self_neighbour(pc)
     A = sn.arrays
     for k in ("pbprime_face", "pbprime_df_face", "zbot_face"):
         assert np.array_equal(A[k][1][:, f], A[k][0][:, f])
+        assert not np.array_equal(A[k][1][:, f], ref[k][1][:, f])
         assert np.array_equal(A[k][:, :, other], ref[k][:, :, other])
-    assert not np.array_equal(ref["pbprime_face"][1][:, f], ref["pbprime_face"][0][:, f])  # (the lake's bathymetry)
     for a, b in (("coeff_pbpert_L", "coeff_pbpert_R"), ("coeff_mass_pbub_L", "coeff_mass_pbub_R")):
         assert np.array_equal(A[a][:, f], A[b][:, f])
     wet = A["pbprime_face"][0][:, f] > 0
