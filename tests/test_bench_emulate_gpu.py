@@ -45,3 +45,22 @@ def test_bench_n_gt_1_branch_runs_on_one_gpu():
     assert abs(d["efficiency_vs_base"] - d["speedup_vs_base"] / 2) < 1e-3
     for k in ("init_process_group_s", "case_build_s", "engine_create_s", "first_step_s", "halocheck_s"):
         assert k in d["setup_s"], k
+
+
+def test_bench_emulates_a_morton_lake_rank_with_its_frozen_halo():
+    """C5's own shape through bench.py (missing 2): rank 1 of the lake on a 4-rank
+    Morton partition keeps its three per-neighbour lists (three RCCL send/recv pairs to itself per
+    exchange) and, the lake at rest, the frozen halo; the line carries a bitwise halo check against
+    the same self-neighbour partition as a local exchange group, and the state stays finite."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(REPO, "bench.py"), "--emulate", "4:1", "--config", "lake10", "--steps", "2",
+           "--warmup", "1", "--no-base"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.strip()][0])
+    assert d["halo_bitwise"] is True and d["emulated"] is True and d["value"] > 0
+    em = d["emulation"]
+    assert em["order"] == "morton" and em["halo"] == "frozen" and em["lists"] == "peers"
+    assert em["messages_per_exchange"] == 3

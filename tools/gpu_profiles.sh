@@ -16,7 +16,7 @@ SQ1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VALU_ADD_F64 SQ_
 SQ2="SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES"
 for cfg in $CFGS; do
   case $cfg in
-    dg316L3) S=3; W=1 ;;
+    dg316L3|lake200) S=3; W=1 ;;
     dg25N7L3) S=10; W=2 ;;
     *) S=20; W=3 ;;
   esac

@@ -2,7 +2,7 @@
 profiles/roofline_pmc.json (read by bench.py: roofline.traffic and the rocprof kernel duration of
 every single-GPU line).
 
-Per config (dg25L3, dg25N7L3, dg316L3):
+Per config (dg25L3, dg25N7L3, dg316L3, lake200):
   kernel_stats_<cfg>.csv  rocprofv3 --stats of the bench run
   <cfg> entry             dominant stage kernel: mean dispatch duration from the kernel trace
                           (the persistent sub-cycle's stage-less residency trial launch at engine
@@ -103,7 +103,7 @@ def main():
     tag = sys.argv[1]
     path = os.path.join(REPO, "profiles", "roofline_pmc.json")
     allr = json.load(open(path)) if os.path.exists(path) else {}
-    for cfg in ("dg25L3", "dg25N7L3", "dg316L3"):
+    for cfg in ("dg25L3", "dg25N7L3", "dg316L3", "lake200"):
         o = summarize(tag, cfg)
         if o:
             allr[cfg] = o
