@@ -273,11 +273,22 @@ struct Launch {
   }
   template <int NB>
   static void launch_nb(int n, hipStream_t st, hipEvent_t stop, const StageArgs &a) {
+    // (the time-average mode as a template argument: stage_body ACCF)
+    if (a.accumulate == 2)
+      launch_nb_acc<NB, 1>(n, st, stop, a);
+    else if (a.accumulate == 1)
+      launch_nb_acc<NB, 2>(n, st, stop, a);
+    else
+      launch_nb_acc<NB, 0>(n, st, stop, a);
+  }
+  template <int NB, int ACCF>
+  static void launch_nb_acc(int n, hipStream_t st, hipEvent_t stop, const StageArgs &a) {
     using K = StageCfg<NGL, NQ, false, NB>;
     if (stop)
-      hipExtLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, NB>), dim3(n), dim3(K::BS), 0, st, nullptr, stop, 0, a);
+      hipExtLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, NB, ACCF>), dim3(n), dim3(K::BS), 0, st, nullptr, stop, 0,
+                            a);
     else
-      hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, NB>), dim3(n), dim3(K::BS), 0, st, a);
+      hipLaunchKernelGGL((btp_stage_kernel<NGL, NQ, false, NB, ACCF>), dim3(n), dim3(K::BS), 0, st, a);
   }
   static void subcycle(hnumo_engine *e, const StageArgs *stages, int ns) {
     SubArgs sa{stages, ns, e->epoch, e->sub_done, e->sub_arrive, e->neg_flag, e->dbg_abort_epoch, e->d_eperm};

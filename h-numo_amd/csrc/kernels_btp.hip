@@ -422,10 +422,17 @@ __device__ __forceinline__ void for_tasks(int tid, int o, int n, F &&f) {
 // first stage on; the data other workgroups (or this one, earlier in the launch) wrote --
 // the state buffers and the neighbour traces -- move with sc1 (L2-coherent, write-through)
 // register loads and stores (MI355X_MICROARCH.md, inter-workgroup visibility).
-template <int NGL, int NQ, bool SF, bool PERSIST, class ARGS, int NB = 0>
+// ACCF: the stage's time-average mode fixed at compile time (per-stage launches of the LEAN arenas:
+// 1 the first stage of a sub-cycle, which stores 0 + x; 2 the later ones, which add), instead of a
+// branch on StageArgs::accumulate at every one of the ~35 accumulator sites; 0: read at run time.
+// (C4 1264-1273 -> 1249-1255 us per stage, lake200 516 -> 508, same bits: profiles/r06/ab_accf.log.
+// The scratch-loaded bottom-layer qprime of the later stages fixed the same way measured slower,
+// 1252 -> 1261-1264 us, and is not kept.)
+template <int NGL, int NQ, bool SF, bool PERSIST, class ARGS, int NB = 0, int ACCF = 0>
 __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsigned long long *s_prof,
                                            bool first, const int e, const int tid, unsigned long long ep = 0,
                                            double *pacc = nullptr) {
+  const int accm = ACCF == 1 ? 2 : (ACCF == 2 ? 1 : a.accumulate);
   using C = StageCfg<NGL, NQ, SF, NB>;
   // persistent: the time averages accumulate in pacc (this thread's registers, see REGACC)
   constexpr bool REGACC = PERSIST && C::REGACC;
@@ -888,7 +895,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   auto face_task = [&](int t) {
     const int lf = t / NQ, iq = t % NQ;
     const int side = s_side[lf], er = s_bc[lf];
-    const bool keep = a.accumulate && s_acc[lf];
+    const bool keep = accm && s_acc[lf];
     const double *ef = s_ef + lf * C::FBLK, *efn = ef + EF_N * NQ;
     const double *ec = s_ec + lf * C::EFC;
     const double *tr = s_tr + lf * 8 * NGL;
@@ -984,7 +991,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         for (int k = 0; k < FA_N; k++) pacc[k] = pacc[k] + add[k];
       } else {
 #pragma unroll
-        for (int k = 0; k < FA_N; k++) acc_put(&a.facc[FACC_I(k, e * 4 + lf, iq)], add[k], a.accumulate == 2);
+        for (int k = 0; k < FA_N; k++) acc_put(&a.facc[FACC_I(k, e * 4 + lf, iq)], add[k], accm == 2);
       }
     }
     const double H_kx = nxl * Hf, H_ky = nyl * Hf;
@@ -1076,7 +1083,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
       const double qu = ub * udp + ope * pre[NST + QC_QUU];
       const double quv = ub * vdp + ope * pre[NST + QC_QUV];
       const double qv = vb * vdp + ope * pre[NST + QC_QVV];
-      if (a.accumulate) {  // time averages (mod_rk_mlswe.F90:107-113)
+      if (accm) {  // time averages (mod_rk_mlswe.F90:107-113)
         double add[QA_N];
         add[QA_H] = Hq; add[QA_QU] = qu; add[QA_QV] = qv; add[QA_QUV] = quv;
         add[QA_TBU] = tb_u; add[QA_TBV] = tb_v; add[QA_OPE] = ope; add[QA_OPE2] = ope * ope;
@@ -1086,7 +1093,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           for (int k = 0; k < QA_N; k++) pacc[k] = pacc[k] + add[k];
         } else {
 #pragma unroll
-          for (int k = 0; k < QA_N; k++) acc_put(&a.qacc[QACC_I(k, e, q)], add[k], a.accumulate == 2);
+          for (int k = 0; k < QA_N; k++) acc_put(&a.qacc[QACC_I(k, e, q)], add[k], accm == 2);
         }
       }
       if constexpr (SF) {
@@ -1129,7 +1136,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
 #pragma unroll
         for (int c = 0; c < 4; c++) s_grad[c * P + p] = g[c];
       }
-      if (a.accumulate) {
+      if (accm) {
         const double t1 = 1.0 + s_qb[p * 4 + 1] * s_ns[NE_OOP * P + p];
         if constexpr (REGACC) {  // (persistent: never the method_visc == 1 branch)
 #pragma unroll
@@ -1140,10 +1147,10 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
         } else {
           if (!a.lapq)
 #pragma unroll
-            for (int c = 0; c < 4; c++) acc_put(&a.nacc[NACC_I(NA_G1 + c, e, p)], g[c], a.accumulate == 2);
-          acc_put(&a.nacc[NACC_I(NA_OPE2, e, p)], t1 * t1, a.accumulate == 2);
-          acc_put(&a.nacc[NACC_I(NA_UB, e, p)], s_u[p], a.accumulate == 2);
-          acc_put(&a.nacc[NACC_I(NA_VB, e, p)], s_v[p], a.accumulate == 2);
+            for (int c = 0; c < 4; c++) acc_put(&a.nacc[NACC_I(NA_G1 + c, e, p)], g[c], accm == 2);
+          acc_put(&a.nacc[NACC_I(NA_OPE2, e, p)], t1 * t1, accm == 2);
+          acc_put(&a.nacc[NACC_I(NA_UB, e, p)], s_u[p], accm == 2);
+          acc_put(&a.nacc[NACC_I(NA_VB, e, p)], s_v[p], accm == 2);
         }
       }
     }
@@ -1172,7 +1179,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   auto ldg_task = [&](int t, bool first) {
     const int lf = t / NGL, n = t % NGL;
     const int side = s_side[lf], er = s_bc[lf];
-    const bool keep = a.accumulate && s_acc[lf] && !a.lapq;
+    const bool keep = accm && s_acc[lf] && !a.lapq;
     const int p = s_map[lf * NGL + n];
     const double *efn = s_ef + lf * C::FBLK + EF_N * NQ;
     const double *B = s_ec + lf * C::EFC + 4 * NQ;  // btp_graduv_dpp_face(c) at [c][NGL]
@@ -1208,8 +1215,8 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
           pacc[c] = pacc[c] + gl[c];
           pacc[4 + c] = pacc[4 + c] + gr[c];
         } else {
-          acc_put(&a.gfacc[GFACC_I(c, e * 4 + lf, n)], gl[c], a.accumulate == 2);
-          acc_put(&a.gfacc[GFACC_I(4 + c, e * 4 + lf, n)], gr[c], a.accumulate == 2);
+          acc_put(&a.gfacc[GFACC_I(c, e * 4 + lf, n)], gl[c], accm == 2);
+          acc_put(&a.gfacc[GFACC_I(4 + c, e * 4 + lf, n)], gr[c], accm == 2);
         }
       }
     }
@@ -1875,7 +1882,7 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
     // the sub-cycle's last stage: each accumulating thread writes its time averages once, scaled
     // as btp_finalize_kernel scales the atomically summed ones (mod_rk_mlswe.F90:124-149); the
     // face slots of faces another element keeps get zeros, as the zeroed atomic buffers did
-    if (!a.write_trace && a.accumulate) {
+    if (!a.write_trace && accm) {
       const double ni = a.n_inv;
       if (tid < Q) {
 #pragma unroll
@@ -1918,13 +1925,13 @@ __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsig
   }
 }
 
-template <int NGL, int NQ, bool SF, int NB = 0>
+template <int NGL, int NQ, bool SF, int NB = 0, int ACCF = 0>
 __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF, NB>::BS), (StageCfg<NGL, NQ, SF, NB>::MINW))
     btp_stage_kernel(StageArgs a) {
   __shared__ __attribute__((aligned(16))) double s_arena[StageCfg<NGL, NQ, SF, NB>::ARENA];
   __shared__ unsigned long long s_prof[HNUMO_DIAG ? 32 : 1];
-  stage_body<NGL, NQ, SF, false, StageArgs, NB>(a, s_arena, s_prof, true,
-                                                a.elist ? a.elist[blockIdx.x] : (int)blockIdx.x, threadIdx.x);
+  stage_body<NGL, NQ, SF, false, StageArgs, NB, ACCF>(a, s_arena, s_prof, true,
+                                                      a.elist ? a.elist[blockIdx.x] : (int)blockIdx.x, threadIdx.x);
 }
 
 // The whole barotropic sub-cycle (N_btp x kstages stages, ti_barotropic_ssprk_mlswe
