@@ -428,11 +428,14 @@ __device__ __forceinline__ void for_tasks(int tid, int o, int n, F &&f) {
 // (C4 1264-1273 -> 1249-1255 us per stage, lake200 516 -> 508, same bits: profiles/r06/ab_accf.log.
 // The scratch-loaded bottom-layer qprime of the later stages fixed the same way measured slower,
 // 1252 -> 1261-1264 us, and is not kept.)
-template <int NGL, int NQ, bool SF, bool PERSIST, class ARGS, int NB = 0, int ACCF = 0>
+// FST: whether this is a sub-cycle's first stage fixed at compile time (1 first, 2 a later one; 0:
+// the argument first_rt decides).
+template <int NGL, int NQ, bool SF, bool PERSIST, class ARGS, int NB = 0, int ACCF = 0, int FST = 0>
 __device__ __forceinline__ void stage_body(const ARGS &a, double *s_arena, unsigned long long *s_prof,
-                                           bool first, const int e, const int tid, unsigned long long ep = 0,
+                                           bool first_rt, const int e, const int tid, unsigned long long ep = 0,
                                            double *pacc = nullptr) {
   const int accm = ACCF == 1 ? 2 : (ACCF == 2 ? 1 : a.accumulate);
+  const bool first = FST == 0 ? first_rt : FST == 1;
   using C = StageCfg<NGL, NQ, SF, NB>;
   // persistent: the time averages accumulate in pacc (this thread's registers, see REGACC)
   constexpr bool REGACC = PERSIST && C::REGACC;
@@ -2016,15 +2019,24 @@ __global__ void __launch_bounds__((StageCfg<NGL, NQ, SF>::BS), (StageCfg<NGL, NQ
   double pacc[16];  // this thread's time averages (StageCfg::REGACC)
 #pragma unroll
   for (int k = 0; k < 16; k++) pacc[k] = 0.0;
+  // the first stage peeled off the stage loop, so that neither copy of the body branches on it (two
+  // inlined bodies; C3 35.8 -> 34.8-35.4 us per stage, dg25L3 unchanged, same bits:
+  // profiles/r06/ab_pfirst.log)
+  if (NS > 0) {
+    int tid_s = tid, e_s = e;
+    asm volatile("" : "+v"(tid_s), "+s"(e_s));
+    tid_s &= C::BS - 1;
+    stage_body<NGL, NQ, SF, true, CStageArgs, 0, 0, 1>(tab[0], s_arena, s_prof, true, e_s, tid_s, ep, pacc);
+  }
 #pragma unroll 1
-  for (int stage = 0; stage < NS; stage++) {
-    if (stage > 0) __syncthreads();
+  for (int stage = 1; stage < NS; stage++) {
+    __syncthreads();
     // opaque per stage: keeps the body's per-thread index math from being hoisted out of the
     // stage loop (it would stay live across every phase)
     int tid_s = tid, e_s = e;
     asm volatile("" : "+v"(tid_s), "+s"(e_s));
     tid_s &= C::BS - 1;  // restore the known range of the thread index
-    stage_body<NGL, NQ, SF, true>(tab[stage], s_arena, s_prof, stage == 0, e_s, tid_s, ep, pacc);
+    stage_body<NGL, NQ, SF, true, CStageArgs, 0, 0, 2>(tab[stage], s_arena, s_prof, false, e_s, tid_s, ep, pacc);
   }
   // the next launch's tags: every workgroup read the epoch at its start, so the last one to
   // finish (agent-scope counter) moves it on and resets the counters (every workgroup has passed

@@ -158,13 +158,16 @@ contains
     ! environment, write the processor-face descriptor exactly as hnumo_engine_create will read it
     ! -- through the descriptor's own pointers -- to <path>.<rank> before the first device call:
     ! int32 rank, nranks, num_nbh, nelem_owned, sum(num_send_recv), then nbh_proc(num_nbh),
-    ! num_send_recv(num_nbh), nbh_send_recv(sum).  Nothing is written without the variable.
+    ! num_send_recv(num_nbh), nbh_send_recv(sum).  Nothing is written without the variable.  The
+    ! ranks then meet at a barrier, so that rank 0 failing at its first device call cannot end the
+    ! job before every rank has written its file.
     subroutine dump_halo(h)
         use iso_c_binding, only: c_f_pointer
+        use mpi
         type(hnumo_halo_desc), intent(in) :: h
         character(len=1024) :: path
         character(len=16) :: rs
-        integer :: n, stat, u
+        integer :: n, stat, u, ierr
         integer(c_int32_t), pointer :: proc(:), num(:), lst(:)
         call get_environment_variable('HNUMO_BRIDGE_HALO_DUMP', path, status=stat)
         if (stat /= 0 .or. len_trim(path) == 0) return
@@ -180,6 +183,7 @@ contains
         write(u) h%rank, h%nranks, h%num_nbh, h%nelem_owned, int(n, c_int32_t)
         if (h%num_nbh > 0) write(u) proc, num, lst(1:n)
         close(u)
+        call mpi_barrier(MPI_COMM_WORLD, ierr)
     end subroutine dump_halo
 
     ! drop-in for ti_rk_bcl (ti_rk_bcl.F90:9-19): same arguments, same layouts

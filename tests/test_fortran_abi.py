@@ -101,10 +101,11 @@ def _bridge_halo_dump(parts, d):
     for r, pc in enumerate(parts):
         B.write_bundle(f"{fin}.{r}", pc, "step", 1, metrics=True)
     env = dict(os.environ, HNUMO_BRIDGE_HALO_DUMP=dump)
-    subprocess.run([O.MPIEXEC, "-launcher", "fork", "-n", str(len(parts)), O.DROPIN_DRIVER, fin, fout], cwd=d,
-                   capture_output=True, text=True, timeout=300, env=env)
+    p = subprocess.run([O.MPIEXEC, "-launcher", "fork", "-n", str(len(parts)), O.DROPIN_DRIVER, fin, fout], cwd=d,
+                       capture_output=True, text=True, timeout=300, env=env)
     out = []
     for r in range(len(parts)):
+        assert os.path.exists(f"{dump}.{r}"), ("no halo dump from rank", r, p.stdout[-1000:], p.stderr[-1000:])
         a = np.fromfile(f"{dump}.{r}", dtype="<i4")
         rank, nranks, nn, nown, n = (int(x) for x in a[:5])
         rest = a[5:]
